@@ -1,0 +1,138 @@
+/*
+ * rrtmgpnn.h -- C ABI of the MI355X-native RTE+RRTMGP-NN hot path.
+ *
+ * Plain pointers and sizes only (no torch / HIP types in the signatures): this is the
+ * boundary the reference's Fortran class layer binds through ISO_C_BINDING
+ * (see rte-rrtmgp-nn_amd/fortran/ and INTEGRATION.md).  All arrays use the reference's
+ * Fortran column-major layout, g-point fastest:
+ *     tau/lay_source/ssa/g      (ngpt, nlay,   ncol)
+ *     lev_source                (ngpt, nlay+1, ncol)
+ *     sfc_source/sfc_emis_gpt   (ngpt, ncol)
+ *     play/tlay/col_dry/gases   (nlay, ncol)        plev/tlev (nlay+1, ncol)
+ *     fluxes                    (nlay+1, ncol)
+ * Array arguments are DEVICE pointers (hipMalloc'd or torch tensors) unless the comment
+ * says "host".  Every call is asynchronous on the context's stream and reentrant across
+ * contexts (one context per host thread / OpenMP block, as the reference drivers'
+ * `!$OMP PARALLEL firstprivate(...)` loops require, rrtmgp_rfmip_lw.F90:364-367).
+ *
+ * Return value: RRTMGPNN_OK (0) or an error code; the message of the last failing call on
+ * this host thread is rrtmgpnn_last_error().  The reference class layer returns
+ * character(len=128) error_msg (empty on success); the Fortran glue maps one to the other.
+ */
+#ifndef RRTMGPNN_H
+#define RRTMGPNN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RRTMGPNN_OK               0
+#define RRTMGPNN_ERR_ARGUMENT     1
+#define RRTMGPNN_ERR_DEVICE       2
+#define RRTMGPNN_ERR_IO           3
+#define RRTMGPNN_ERR_UNSUPPORTED  4
+
+#define RRTMGPNN_ACT_LINEAR       0
+#define RRTMGPNN_ACT_SOFTSIGN     1
+#define RRTMGPNN_ACT_RELU         2
+#define RRTMGPNN_ACT_SIGMOID      3
+#define RRTMGPNN_ACT_HARD_SIGMOID 4
+
+typedef struct rrtmgpnn_context rrtmgpnn_context;
+typedef struct rrtmgpnn_network rrtmgpnn_network;
+
+/* ---- runtime ------------------------------------------------------------------------------ */
+int         rrtmgpnn_version(void);
+const char *rrtmgpnn_last_error(void);
+/* Creates a context on `device`; hip_stream may be NULL (a private non-blocking stream is made). */
+int rrtmgpnn_context_create(int device, void *hip_stream, rrtmgpnn_context **ctx);
+int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx);
+int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream);
+void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx);
+int rrtmgpnn_context_synchronize(rrtmgpnn_context *ctx);
+/* Device memory helpers for hosts without their own allocator (Fortran glue). */
+int rrtmgpnn_malloc(rrtmgpnn_context *ctx, long long bytes, void **dptr);
+int rrtmgpnn_free(rrtmgpnn_context *ctx, void *dptr);
+int rrtmgpnn_memcpy_h2d(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes);
+int rrtmgpnn_memcpy_d2h(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes);
+
+/* ---- neural networks: replaces rrtmgp_network_type (neural/mod_network_rrtmgp.F90:34-122) ---- */
+/* Load an RBIN model file (converted from the reference's netCDF model files). */
+int rrtmgpnn_network_load(rrtmgpnn_context *ctx, const char *path, rrtmgpnn_network **net);
+/* Build from host arrays.  weights[n] is layer n's kernel, (dims[n], dims[n+1]) C-order
+ * (= the netCDF variable nn_weights_<n+1> = the reference's w_transposed memory).
+ * output_mean/std may be NULL (Planck-fraction models). */
+int rrtmgpnn_network_create(rrtmgpnn_context *ctx, int nlayers, const int *dims, const int *activations,
+                            const float *const *weights, const float *const *biases,
+                            const float *input_min, const float *input_max,
+                            const float *output_mean, const float *output_std,
+                            const char *input_names /* nx*32 chars, space padded, may be NULL */,
+                            rrtmgpnn_network **net);
+int rrtmgpnn_network_destroy(rrtmgpnn_network *net);
+/* host outputs */
+int rrtmgpnn_network_get_dims(const rrtmgpnn_network *net, int *nlayers, int dims[8]);
+int rrtmgpnn_network_get_input_name(const rrtmgpnn_network *net, int i, char *buf, int buflen);
+int rrtmgpnn_network_get_input_scaling(const rrtmgpnn_network *net, float *input_min, float *input_max);
+
+/* ---- gas-optics kernels --------------------------------------------------------------------- */
+/* compute_nn_inputs (rrtmgp/mo_gas_optics_rrtmgp.F90:618-798).  gas_conc[k] (k>=2) is a device
+ * pointer to the concentration of input k with gas_ndims[k] in {0:(1), 1:(nlay), 2:(nlay,ncol)},
+ * or NULL when the gas is absent (reference uses ref_vmr = 0, :757-758).  Entries 0,1 ignored.
+ * gas_conc/gas_ndims are HOST arrays of length ninputs (<= 32).  nn_inputs (ninputs,nlay,ncol). */
+int rrtmgpnn_compute_nn_inputs(rrtmgpnn_context *ctx, int ncol, int nlay, int ninputs,
+                               const float *play, const float *tlay,
+                               const float *const *gas_conc, const int *gas_ndims,
+                               const rrtmgpnn_network *net, float *nn_inputs);
+/* get_col_dry (rrtmgp/mo_gas_optics_rrtmgp.F90:1662-1707), g0 = grav. */
+int rrtmgpnn_get_col_dry(rrtmgpnn_context *ctx, int ncol, int nlay, const float *vmr_h2o, const float *plev,
+                         float *col_dry);
+/* Level temperatures from layers (rrtmgp/mo_gas_optics_rrtmgp.F90:317-337). */
+int rrtmgpnn_interpolate_tlev(rrtmgpnn_context *ctx, int ncol, int nlay, const float *play, const float *plev,
+                              const float *tlay, float *tlev);
+/* predict_nn_lw_blas (rrtmgp/kernels/mo_gas_optics_kernels.F90:690-774).  nnets == 2: nets[0] =
+ * absorption (tau = (std*y+mean)^8 * col_dry), nets[1] = Planck fraction (pfrac = y^2);
+ * nnets == 1: single "both" model with 2*ngpt outputs (:744-772). */
+int rrtmgpnn_predict_nn_lw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs,
+                           const float *nn_inputs, const float *col_dry,
+                           const rrtmgpnn_network *const *nets, int nnets, float *tau, float *pfrac);
+/* predict_nn_sw_blas (:869-953) with INLINE_COMBINE: nets[0] absorption, nets[1] Rayleigh.
+ * ssa == NULL -> tau = tau_abs only (1scl).  Otherwise tau = tau_abs + tau_ray, ssa = tau_ray/tau.
+ * g != NULL -> zero-filled as gas_optics_ext does (mo_gas_optics_rrtmgp.F90:560-567). */
+int rrtmgpnn_predict_nn_sw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs,
+                           const float *nn_inputs, const float *col_dry,
+                           const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g);
+/* Generic MLP forward (network_type%output_sgemm_flat, neural/mod_network.F90:273-354):
+ * out(ny, nbatch) = net(x(nx, nbatch)), last-layer activation applied, no post-processing. */
+int rrtmgpnn_network_forward(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch,
+                             const float *x, float *out);
+/* compute_Planck_source_nn (rrtmgp/kernels/mo_gas_optics_kernels.F90:615-683).  sfc_lay 1-based.
+ * band_lims_gpt: HOST (2,nbnd) 1-based.  totplnk: DEVICE (nPlanckTemp, nbnd).
+ * pfrac is overwritten with lay_source. */
+int rrtmgpnn_compute_planck_source_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int nbnd, int ngpt,
+                                      int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
+                                      int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
+                                      float totplnk_delta, const float *totplnk, float *sfc_source,
+                                      float *sfc_source_Jac, float *pfrac, float *lev_source);
+
+/* ---- RTE solvers ---------------------------------------------------------------------------- */
+/* lw_solver_noscat_GaussQuad (rte/kernels/mo_rte_solver_kernels.F90:332-415) without rescaling or
+ * Jacobians.  Ds, weights: HOST arrays of nmus (<= 4) entries.  inc_flux may be NULL (zero). */
+int rrtmgpnn_lw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                              const float *Ds, const float *weights, const float *inc_flux,
+                              const float *tau, const float *lay_source, const float *lev_source,
+                              const float *sfc_emis_gpt, const float *sfc_source,
+                              float *flux_up, float *flux_dn);
+/* sw_solver_2stream (:541-692).  inc_flux_dif may be NULL (zero, rte/mo_rte_sw.F90:197-210). */
+int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                               const float *inc_flux, const float *inc_flux_dif,
+                               const float *tau, const float *ssa, const float *g, const float *mu0,
+                               const float *sfc_alb_dir_gpt, const float *sfc_alb_dif_gpt,
+                               float *flux_up, float *flux_dn, float *flux_dir);
+/* expand (rte/mo_rte_lw.F90:429-447): (nband,ncol) -> (ngpt,ncol).  band_lims_gpt HOST (2,nband). */
+int rrtmgpnn_expand_band_to_gpt(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const int *band_lims_gpt,
+                                const float *arr_in, float *arr_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RRTMGPNN_H */

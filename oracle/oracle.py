@@ -1,0 +1,252 @@
+"""oracle.py -- TEST INFRASTRUCTURE ONLY: numpy front-end of the CPU oracles.
+
+  * `Oracle`    : the C restatement (oracle/librrtmgpnn_oracle.so, built from rrtmgpnn_oracle.c)
+  * `Reference` : the reference's own Fortran compiled by oracle/Makefile.ref
+                  (oracle/_ref/librrtmgp_ref.so; only where /root/reference was available to build it)
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.  The
+product (rte-rrtmgp-nn_amd/) never does.  Arrays use numpy C order with reversed Fortran shapes
+(Fortran tau(ngpt,nlay,ncol) <-> numpy (ncol,nlay,ngpt)).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "rte-rrtmgp-nn_amd"))
+from rrtmgpnn import data  # noqa: E402
+
+ORACLE_SO = os.path.join(HERE, "librrtmgpnn_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "librrtmgp_ref.so")
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+c_int, c_float, c_long, c_vp = ctypes.c_int, ctypes.c_float, ctypes.c_long, ctypes.c_void_p
+
+
+def f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(c_vp) if a is not None else None
+
+
+class Oracle:
+    """C restatement of the hot path (rrtmgpnn_oracle.c)."""
+
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError("%s missing: run `make -C oracle`" % path)
+        L = self.L = ctypes.CDLL(path)
+        L.orc_compute_nn_inputs.argtypes = [c_int, c_int, c_int, _f32p, _f32p, ctypes.POINTER(c_vp),
+                                            _i32p, _f32p, _f32p, _f32p]
+        L.orc_get_col_dry.argtypes = [c_int, c_int, _f32p, _f32p, _f32p]
+        L.orc_mlp_forward.argtypes = [c_int, _i32p, ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), _i32p, c_long,
+                                      _f32p, _f32p]
+        L.orc_nn_tau_post.argtypes = [c_int, c_long, _f32p, _f32p, _f32p, _f32p, c_vp]
+        L.orc_square.argtypes = [c_long, _f32p]
+        L.orc_planck_source_nn.argtypes = [c_int, c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, c_int, _i32p,
+                                           c_float, c_float, _f32p, _f32p, _f32p, _f32p, _f32p]
+        L.orc_lw_solver_noscat_gaussquad.argtypes = [c_int, c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p,
+                                                     _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
+        L.orc_sw_solver_2stream.argtypes = [c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
+                                            _f32p, _f32p, _f32p, _f32p, _f32p]
+        L.orc_expand.argtypes = [c_int, c_int, c_int, _i32p, _f32p, _f32p]
+        L.orc_set_num_threads.argtypes = [c_int]
+        L.orc_num_threads.restype = c_int
+
+    def set_threads(self, n):
+        self.L.orc_set_num_threads(int(n))
+
+    # -- building blocks ---------------------------------------------------------------------
+    def nn_inputs(self, play, tlay, gases, model):
+        """gases: dict name -> (ncol,nlay) array or scalar; model: RBIN dict of the first network."""
+        from rrtmgpnn import rbin
+        names = rbin.unchars(model["input_names"])
+        nx = len(names)
+        ncol, nlay = play.shape
+        keep, ptrs, nds = [], [], []
+        for k, n in enumerate(names):
+            if k < 2 or n not in gases:
+                ptrs.append(None)
+                nds.append(2)
+                continue
+            v = np.asarray(gases[n], np.float32)
+            v = f32(v)
+            keep.append(v)
+            ptrs.append(_ptr(v))
+            nds.append({0: 0, 1: 1}.get(v.ndim, 2))
+        out = np.zeros((ncol, nlay, nx), np.float32)
+        self.L.orc_compute_nn_inputs(ncol, nlay, nx, f32(play), f32(tlay), (c_vp * nx)(*ptrs),
+                                     np.array(nds, np.int32), f32(model["input_min"]), f32(model["input_max"]), out)
+        return out
+
+    def col_dry(self, h2o, plev):
+        ncol, nlay = h2o.shape
+        out = np.zeros((ncol, nlay), np.float32)
+        self.L.orc_get_col_dry(ncol, nlay, f32(h2o), f32(plev), out)
+        return out
+
+    def mlp(self, model, x):
+        dims = np.asarray(model["dims"], np.int32)
+        nl = dims.size - 1
+        ws = [f32(model["w%d" % (n + 1)]) for n in range(nl)]
+        bs = [f32(model["b%d" % (n + 1)]) for n in range(nl)]
+        x = f32(x)
+        nb = x.size // dims[0]
+        out = np.zeros((nb, dims[-1]), np.float32)
+        self.L.orc_mlp_forward(nl, dims, (c_vp * nl)(*[_ptr(w) for w in ws]), (c_vp * nl)(*[_ptr(b) for b in bs]),
+                               np.asarray(model["activation"], np.int32), nb, x, out)
+        return out
+
+    def tau_post(self, model, y, col_dry, tau_abs_to_tot=None):
+        y = f32(y).copy()
+        ngpt = y.shape[-1]
+        nb = y.size // ngpt
+        self.L.orc_nn_tau_post(ngpt, nb, y, f32(model["output_mean"]), f32(model["output_std"]), f32(col_dry).reshape(-1),
+                               _ptr(tau_abs_to_tot) if tau_abs_to_tot is not None else None)
+        return y
+
+    def planck_source(self, kd, tlay, tlev, tsfc, pfrac, sfc_lay):
+        ncol, nlay, ngpt = pfrac.shape
+        lay = f32(pfrac).copy()
+        lev = np.zeros((ncol, nlay + 1, ngpt), np.float32)
+        sfc = np.zeros((ncol, ngpt), np.float32)
+        jac = np.zeros((ncol, ngpt), np.float32)
+        self.L.orc_planck_source_nn(ncol, nlay, kd["nband"], ngpt, kd["nPlanckTemp"], f32(tlay), f32(tlev), f32(tsfc),
+                                    int(sfc_lay), np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                    float(kd["temp_ref_min"][0]), float(kd["totplnk_delta"]), f32(kd["totplnk"]),
+                                    sfc, jac, lay, lev)
+        return lay, lev, sfc, jac
+
+    def lw_solver(self, tau, lay, lev, emis_gpt, sfc_src, top_at_1=True, nmus=1, inc_flux=None):
+        ncol, nlay, ngpt = tau.shape
+        Ds, W = gauss(nmus)
+        up = np.zeros((ncol, nlay + 1), np.float32)
+        dn = np.zeros((ncol, nlay + 1), np.float32)
+        inc = f32(inc_flux) if inc_flux is not None else np.zeros((ncol, ngpt), np.float32)
+        self.L.orc_lw_solver_noscat_gaussquad(ngpt, nlay, ncol, int(top_at_1), nmus, f32(Ds), f32(W), inc, f32(tau),
+                                              f32(lay), f32(lev), f32(emis_gpt), f32(sfc_src), up, dn)
+        return up, dn
+
+    def sw_solver(self, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True, inc_flux_dif=None):
+        ncol, nlay, ngpt = tau.shape
+        up = np.zeros((ncol, nlay + 1), np.float32)
+        dn = np.zeros((ncol, nlay + 1), np.float32)
+        dr = np.zeros((ncol, nlay + 1), np.float32)
+        dif = f32(inc_flux_dif) if inc_flux_dif is not None else np.zeros((ncol, ngpt), np.float32)
+        self.L.orc_sw_solver_2stream(ngpt, nlay, ncol, int(top_at_1), f32(inc_flux), dif, f32(tau), f32(ssa), f32(g),
+                                     f32(mu0), f32(alb_dir_gpt), f32(alb_dif_gpt), up, dn, dr)
+        return up, dn, dr
+
+    # -- class-level pipelines (gas_optics + rte) -------------------------------------------
+    def lw_gas_optics(self, prob, models, kd):
+        """gas_optics_int NN branch (rrtmgp/mo_gas_optics_rrtmgp.F90:239-428). models: [abs, pfrac]."""
+        x = self.nn_inputs(prob["play"], prob["tlay"], prob["gases"], models[0])
+        cd = self.col_dry(prob["gases"]["h2o"], prob["plev"])
+        ncol, nlay = prob["play"].shape
+        tau = self.tau_post(models[0], self.mlp(models[0], x.reshape(-1, x.shape[-1])), cd).reshape(ncol, nlay, -1)
+        pf = self.mlp(models[1], x.reshape(-1, x.shape[-1]))
+        pf = (pf * pf).astype(np.float32).reshape(ncol, nlay, -1)
+        sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
+        lay, lev, sfc, jac = self.planck_source(kd, prob["tlay"], prob["tlev"], prob["tsfc"], pf, sfc_lay)
+        return {"tau": tau, "lay_source": lay, "lev_source": lev, "sfc_source": sfc, "sfc_source_Jac": jac,
+                "pfrac": pf, "nn_inputs": x, "col_dry": cd}
+
+    def sw_gas_optics(self, prob, models):
+        """gas_optics_ext NN branch (:433-602), 2str: tau, ssa, g (= 0)."""
+        x = self.nn_inputs(prob["play"], prob["tlay"], prob["gases"], models[0])
+        cd = self.col_dry(prob["gases"]["h2o"], prob["plev"])
+        ncol, nlay = prob["play"].shape
+        xf = x.reshape(-1, x.shape[-1])
+        tau = self.tau_post(models[0], self.mlp(models[0], xf), cd)
+        ssa = self.tau_post(models[1], self.mlp(models[1], xf), cd, tau_abs_to_tot=tau)
+        return {"tau": tau.reshape(ncol, nlay, -1), "ssa": ssa.reshape(ncol, nlay, -1),
+                "g": np.zeros((ncol, nlay, tau.shape[-1]), np.float32), "nn_inputs": x, "col_dry": cd}
+
+    def clear_sky_lw(self, prob, models, kd, nmus=1):
+        go = self.lw_gas_optics(prob, models, kd)
+        ngpt = go["tau"].shape[-1]
+        emis = np.repeat(f32(prob["sfc_emis"])[:, None], ngpt, axis=1)
+        up, dn = self.lw_solver(go["tau"], go["lay_source"], go["lev_source"], emis, go["sfc_source"],
+                                prob["top_at_1"], nmus)
+        return up, dn, go
+
+    def clear_sky_sw(self, prob, models, kd_sw):
+        go = self.sw_gas_optics(prob, models)
+        ngpt = go["tau"].shape[-1]
+        toa = data.toa_flux(prob, kd_sw)
+        alb = np.repeat(f32(prob["sfc_alb"])[:, None], ngpt, axis=1)
+        up, dn, dr = self.sw_solver(go["tau"], go["ssa"], go["g"], prob["mu0"], toa, alb, alb, prob["top_at_1"])
+        m = ~prob["usecol"]
+        up[m] = 0.0
+        dn[m] = 0.0
+        return up, dn, dr, go
+
+
+def gauss(nmus):
+    """Gauss_Ds / gauss_wts of rte/mo_rte_lw.F90:113-125 (first-order quadrature, column nmus)."""
+    Ds = {1: [1.66], 2: [1.18350343, 2.81649655], 3: [1.09719858, 1.69338507, 4.70941630],
+          4: [1.06056257, 1.38282560, 2.40148179, 7.15513024]}[nmus]
+    W = {1: [0.5], 2: [0.3180413817, 0.1819586183], 3: [0.2009319137, 0.2292411064, 0.0698269799],
+         4: [0.1355069134, 0.2034645680, 0.1298475476, 0.0311809710]}[nmus]
+    return np.array(Ds, np.float32), np.array(W, np.float32)
+
+
+class Reference:
+    """The reference's own Fortran (rte_lw, rte_sw, network_type%output_sgemm_flat + MKL sgemm)."""
+
+    def __init__(self, path=REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError("%s missing: build with `make -f oracle/Makefile.ref` (needs /root/reference)" % path)
+        os.environ.setdefault("MKL_THREADING_LAYER", "SEQUENTIAL")
+        L = self.L = ctypes.CDLL(path)
+        L.ref_rte_lw.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, c_int, _f32p, _f32p, _f32p, _f32p,
+                                 _f32p, _f32p, _f32p, _f32p]
+        L.ref_rte_lw.restype = c_int
+        L.ref_rte_sw.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, _f32p, _f32p, _f32p, _f32p,
+                                 _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
+        L.ref_rte_sw.restype = c_int
+        L.ref_mlp.argtypes = [c_int, _i32p, _i32p, _f32p, _f32p, c_int, _f32p, _f32p]
+        L.ref_mlp.restype = c_int
+        L.ref_last_error.argtypes = [ctypes.c_char_p, c_int]
+
+    def _check(self, rc):
+        if rc != 0:
+            buf = ctypes.create_string_buffer(256)
+            self.L.ref_last_error(buf, 256)
+            raise RuntimeError("reference failed: %s" % buf.value.decode())
+
+    def rte_lw(self, kd, tau, lay, lev, sfc_src, sfc_jac, sfc_emis_band, top_at_1=True, nmus=1):
+        ncol, nlay, ngpt = tau.shape
+        up = np.zeros((ncol, nlay + 1), np.float32)
+        dn = np.zeros((ncol, nlay + 1), np.float32)
+        self._check(self.L.ref_rte_lw(ncol, nlay, kd["nband"], ngpt, np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                      f32(kd["band_lims_wvn"]), int(top_at_1), nmus, f32(tau), f32(lay), f32(lev),
+                                      f32(sfc_src), f32(sfc_jac), f32(sfc_emis_band), up, dn))
+        return up, dn
+
+    def rte_sw(self, kd, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True):
+        ncol, nlay, ngpt = tau.shape
+        up = np.zeros((ncol, nlay + 1), np.float32)
+        dn = np.zeros((ncol, nlay + 1), np.float32)
+        dr = np.zeros((ncol, nlay + 1), np.float32)
+        self._check(self.L.ref_rte_sw(ncol, nlay, kd["nband"], ngpt, np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                      f32(kd["band_lims_wvn"]), int(top_at_1), f32(tau), f32(ssa), f32(g), f32(mu0),
+                                      f32(inc_flux), f32(alb_dir_gpt), f32(alb_dif_gpt), up, dn, dr))
+        return up, dn, dr
+
+    def mlp(self, model, x):
+        dims = np.asarray(model["dims"], np.int32)
+        nl = dims.size - 1
+        w_all = np.concatenate([f32(model["w%d" % (n + 1)]).ravel() for n in range(nl)])
+        b_all = np.concatenate([f32(model["b%d" % (n + 1)]).ravel() for n in range(nl)])
+        x = f32(x)
+        nb = x.size // dims[0]
+        out = np.zeros((nb, dims[-1]), np.float32)
+        self._check(self.L.ref_mlp(nl, dims, np.asarray(model["activation"], np.int32), w_all, b_all, nb, x, out))
+        return out

@@ -1,0 +1,134 @@
+! ref_harness.F90 -- TEST INFRASTRUCTURE ONLY (never shipped, never linked by the product).
+!
+! bind(C) entry points around the REFERENCE's own compiled Fortran, so the tests can
+! pin the C restatement (oracle/rrtmgpnn_oracle.c) against the reference itself.
+! Built by oracle/Makefile.ref from the sources where they lie under /root/reference;
+! output goes to oracle/_ref/ only.  Exposes:
+!   ref_rte_lw   -> rte_lw (rte/mo_rte_lw.F90:60) on ty_optical_props_1scl + ty_source_func_lw
+!   ref_rte_sw   -> rte_sw (rte/mo_rte_sw.F90:48) on ty_optical_props_2str
+!   ref_mlp      -> network_type%output_sgemm_flat (neural/mod_network.F90:273) with MKL sgemm
+! The NN modules that need netcdf (mod_network_rrtmgp, mo_gas_optics_rrtmgp,
+! mo_gas_optics_kernels) are not built: netcdf-fortran is absent and we do not stub it.
+module ref_harness
+  use, intrinsic :: iso_c_binding
+  use mo_rte_kind,         only: wp
+  use mo_optical_props,    only: ty_optical_props_1scl, ty_optical_props_2str
+  use mo_source_functions, only: ty_source_func_lw
+  use mo_fluxes,           only: ty_fluxes_flexible
+  use mo_rte_lw,           only: rte_lw
+  use mo_rte_sw,           only: rte_sw
+  use mod_network,         only: network_type
+  implicit none
+  character(len=128), save :: last_msg = ''
+contains
+
+  integer(c_int) function ref_rte_lw(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, top_at_1, nmus, &
+                                     tau, lay_src, lev_src, sfc_src, sfc_src_jac, sfc_emis, &
+                                     flux_up, flux_dn) bind(C, name="ref_rte_lw")
+    integer(c_int), value :: ncol, nlay, nband, ngpt, top_at_1, nmus
+    integer(c_int), intent(in) :: band_lims_gpt(2, nband)
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband)
+    real(c_float),  intent(in) :: tau(ngpt, nlay, ncol), lay_src(ngpt, nlay, ncol), lev_src(ngpt, nlay+1, ncol)
+    real(c_float),  intent(in) :: sfc_src(ngpt, ncol), sfc_src_jac(ngpt, ncol), sfc_emis(nband, ncol)
+    real(c_float),  intent(out), target :: flux_up(nlay+1, ncol), flux_dn(nlay+1, ncol)
+
+    type(ty_optical_props_1scl) :: op
+    type(ty_source_func_lw)     :: src
+    type(ty_fluxes_flexible)    :: fl
+    real(wp), allocatable, target :: gup(:,:,:), gdn(:,:,:)
+    character(len=128) :: err
+
+    ref_rte_lw = 1
+    err = op%alloc_1scl(ncol, nlay, band_lims_wvn, band_lims_gpt)
+    if (err /= '') then; last_msg = err; return; end if
+    err = src%alloc(ncol, nlay, op)
+    if (err /= '') then; last_msg = err; return; end if
+    op%tau = tau
+    src%lay_source = lay_src
+    src%lev_source = lev_src
+    src%sfc_source = sfc_src
+    src%sfc_source_Jac = sfc_src_jac
+    fl%flux_up => flux_up
+    fl%flux_dn => flux_dn
+    if (nmus > 1) then
+      ! n_gauss_angles > 1 needs g-point flux storage (lw_solver_noscat_GaussQuad :383-412)
+      allocate(gup(ngpt, nlay+1, ncol), gdn(ngpt, nlay+1, ncol))
+      fl%gpt_flux_up => gup
+      fl%gpt_flux_dn => gdn
+    end if
+    err = rte_lw(op, top_at_1 /= 0, src, sfc_emis, fl, n_gauss_angles=int(nmus), use_2stream=.false.)
+    if (err /= '') then; last_msg = err; return; end if
+    ref_rte_lw = 0
+  end function ref_rte_lw
+
+  integer(c_int) function ref_rte_sw(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, top_at_1, &
+                                     tau, ssa, g, mu0, inc_flux, sfc_alb_dir, sfc_alb_dif, &
+                                     flux_up, flux_dn, flux_dir) bind(C, name="ref_rte_sw")
+    integer(c_int), value :: ncol, nlay, nband, ngpt, top_at_1
+    integer(c_int), intent(in) :: band_lims_gpt(2, nband)
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband)
+    real(c_float),  intent(in) :: tau(ngpt, nlay, ncol), ssa(ngpt, nlay, ncol), g(ngpt, nlay, ncol)
+    real(c_float),  intent(in) :: mu0(ncol), inc_flux(ngpt, ncol), sfc_alb_dir(ngpt, ncol), sfc_alb_dif(ngpt, ncol)
+    real(c_float),  intent(out), target :: flux_up(nlay+1, ncol), flux_dn(nlay+1, ncol), flux_dir(nlay+1, ncol)
+
+    type(ty_optical_props_2str) :: op
+    type(ty_fluxes_flexible)    :: fl
+    character(len=128) :: err
+
+    ref_rte_sw = 1
+    err = op%alloc_2str(ncol, nlay, band_lims_wvn, band_lims_gpt)
+    if (err /= '') then; last_msg = err; return; end if
+    op%tau = tau
+    op%ssa = ssa
+    op%g   = g
+    fl%flux_up     => flux_up
+    fl%flux_dn     => flux_dn
+    fl%flux_dn_dir => flux_dir
+    err = rte_sw(op, top_at_1 /= 0, mu0, inc_flux, sfc_alb_dir, sfc_alb_dif, fl)
+    if (err /= '') then; last_msg = err; return; end if
+    ref_rte_sw = 0
+  end function ref_rte_sw
+
+  ! MLP chain of the reference: h = act(W^T x + b) via MKL sgemm (neural/mod_network.F90:273-354).
+  ! w_all: concatenation of each layer's weights stored (n_in, n_out) C-order = w_transposed(n_out,n_in).
+  integer(c_int) function ref_mlp(nlayers, dims, acts, w_all, b_all, nbatch, x, out) bind(C, name="ref_mlp")
+    integer(c_int), value :: nlayers, nbatch
+    integer(c_int), intent(in) :: dims(nlayers+1), acts(nlayers)
+    real(c_float),  intent(in) :: w_all(*), b_all(*)
+    real(c_float),  intent(in) :: x(dims(1), nbatch)
+    real(c_float),  intent(out) :: out(dims(nlayers+1), nbatch)
+    type(network_type) :: net
+    integer :: n, ow, ob, nin, nout, j0, nb
+    integer, parameter :: chunk = 1024   ! output_sgemm_flat keeps (neurons, nbatch) automatic arrays on the stack
+    character(len=16), dimension(0:6) :: names = [character(len=16) :: 'linear', 'softsign', 'relu', 'sigmoid', &
+                                                  'hard_sigmoid', 'tanh', 'gaussian']
+
+    call net%init(dims)
+    ow = 0; ob = 0
+    do n = 1, nlayers
+      nin = dims(n); nout = dims(n+1)
+      net%layers(n)%w_transposed = reshape(w_all(ow+1:ow+nin*nout), [nout, nin])
+      net%layers(n)%w = transpose(net%layers(n)%w_transposed)
+      net%layers(n)%b = b_all(ob+1:ob+nout)
+      call net%layers(n)%set_activation(trim(names(acts(n))))
+      ow = ow + nin*nout; ob = ob + nout
+    end do
+    do j0 = 1, nbatch, chunk
+      nb = min(chunk, nbatch - j0 + 1)
+      call net%output_sgemm_flat(dims(1), dims(nlayers+1), nb, x(:, j0:j0+nb-1), out(:, j0:j0+nb-1))
+    end do
+    ref_mlp = 0
+  end function ref_mlp
+
+  subroutine ref_last_error(buf, n) bind(C, name="ref_last_error")
+    integer(c_int), value :: n
+    character(kind=c_char), intent(out) :: buf(n)
+    integer :: i
+    do i = 1, n
+      buf(i) = c_null_char
+    end do
+    do i = 1, min(n-1, len_trim(last_msg))
+      buf(i) = last_msg(i:i)
+    end do
+  end subroutine ref_last_error
+end module ref_harness

@@ -1,0 +1,489 @@
+/*
+ * rrtmgpnn_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C99, float32 like the reference's default wp = c_float,
+ * rte/mo_rte_kind.F90:29-33) of the RTE+RRTMGP-NN hot path.  It is the parity
+ * checker for the HIP kernels and the "port" CPU baseline in bench.py.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it;
+ * the product (rte-rrtmgp-nn_amd/) never does.
+ *
+ * Parity of this restatement is pinned against the reference itself:
+ *   - RTE solvers (lw_solver_noscat[_GaussQuad], sw_solver_2stream, adding) and
+ *     the MLP chain (network_type%output_sgemm_flat + MKL sgemm) are compiled
+ *     from /root/reference sources by oracle/Makefile.ref into oracle/_ref/
+ *     and compared in tests/test_oracle_vs_reference.py (container only); the
+ *     comparison's outputs are frozen as tests/golden/*.rbin fixtures.
+ *   - compute_nn_inputs, get_col_dry, the NN post-processing and
+ *     compute_Planck_source_nn live in reference modules that need netcdf
+ *     (unbuildable here); they are restated below line-by-line and pinned by the
+ *     known-answer property sum_g pfrac = 1 per band.
+ *
+ * Every function cites the reference lines it follows.  Array conventions are
+ * the reference's Fortran column-major ones: x(a,b,c) is x[a + na*(b + nb*c)].
+ * Compile with -ffp-contract=off: multiply-adds are written as fmaf() exactly
+ * where the order is meant to be fused.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define PI_F 3.14159265358979323846f
+
+/* ---------------------------------------------------------------------------------------------
+ * NN inputs: rrtmgp/mo_gas_optics_rrtmgp.F90:618-798 (compute_nn_inputs)
+ *   nn_inputs(1) = (tlay - min)/(max-min); (2) = (log(play) - ...); (3),(4) = (sqrt(sqrt(h2o/o3)) - ...)
+ *   others: concentration scalar/1-D/2-D min-max scaled; missing gas -> ref_vmr = 0
+ *   (nn_scenario_index local = 0 at :636 shadows the config module, :757-758).
+ * gas[k] for k >= 2 (0-based): pointer to conc, gas_ndims[k] in {0,1,2}, or NULL = missing.
+ * h2o (k=2) and o3 (k=3) must be 2-D (nlay,ncol).
+ * ------------------------------------------------------------------------------------------- */
+void orc_compute_nn_inputs(int ncol, int nlay, int nx, const float *play, const float *tlay,
+                           const float *const *gas, const int *gas_ndims,
+                           const float *in_min, const float *in_max, float *nn_inputs)
+{
+  for (int icol = 0; icol < ncol; icol++)
+    for (int ilay = 0; ilay < nlay; ilay++) {
+      size_t s = (size_t)ilay + (size_t)nlay * icol;
+      float *o = nn_inputs + (size_t)nx * s;
+      o[0] = (tlay[s] - in_min[0]) / (in_max[0] - in_min[0]);
+      o[1] = (logf(play[s]) - in_min[1]) / (in_max[1] - in_min[1]);
+      o[2] = (sqrtf(sqrtf(gas[2][s])) - in_min[2]) / (in_max[2] - in_min[2]);
+      o[3] = (sqrtf(sqrtf(gas[3][s])) - in_min[3]) / (in_max[3] - in_min[3]);
+      for (int k = 4; k < nx; k++) {
+        float c;
+        if (!gas[k]) c = 0.0f;
+        else if (gas_ndims[k] == 0) c = gas[k][0];
+        else if (gas_ndims[k] == 1) c = gas[k][ilay];
+        else c = gas[k][s];
+        o[k] = (c - in_min[k]) / (in_max[k] - in_min[k]);
+      }
+    }
+}
+
+/* rrtmgp/mo_gas_optics_rrtmgp.F90:1662-1707 (get_col_dry), constants mo_rrtmgp_constants.F90 */
+void orc_get_col_dry(int ncol, int nlay, const float *vmr_h2o, const float *plev, float *col_dry)
+{
+  const float m_dry = 0.028964f, m_h2o = 0.018016f, avogad = 6.02214076e23f, grav = 9.80665f;
+  for (int icol = 0; icol < ncol; icol++)
+    for (int ilev = 0; ilev < nlay; ilev++) {
+      const float *pl = plev + (size_t)(nlay + 1) * icol;
+      float v = vmr_h2o[ilev + (size_t)nlay * icol];
+      float delta_plev = fabsf(pl[ilev] - pl[ilev + 1]);
+      float fact = 1.0f / (1.0f + v);
+      float m_air = (m_dry + m_h2o * v) * fact;
+      col_dry[ilev + (size_t)nlay * icol] =
+          10.0f * delta_plev * avogad * fact / (1000.0f * m_air * 100.0f * grav);
+    }
+}
+
+/* neural/mod_activation.F90:107-184 (bias_and_activation variants) */
+static float activate(int act, float x)
+{
+  switch (act) {
+  case 1: return x / (fabsf(x) + 1.0f);                          /* softsign  :111-118 */
+  case 2: return fmaxf(0.0f, x);                                 /* relu      :52-60   */
+  case 3: return 1.0f / (1.0f + expf(-x));                       /* sigmoid   :79-86   */
+  case 4: return fmaxf(0.0f, fminf(1.0f, 0.2f * x + 0.5f));      /* hard_sigmoid       */
+  case 5: return tanhf(x);
+  case 6: return expf(-x * x);
+  default: return x;                                             /* linear    :163-184 */
+  }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Generic MLP forward, neural/mod_network.F90:273-354 (output_sgemm_flat) and
+ * neural/mod_network_rrtmgp.F90:125-236: a_{n} = act_n(W_n^T a_{n-1} + b_n).
+ * W[n] is stored (n_in, n_out) C-order (= the netCDF kernel, = w_transposed Fortran).
+ * The sum is an fmaf chain over ascending k (the GPU MFMA kernel reproduces this order).
+ * x(nx, nbatch), out(ny, nbatch); nbatch samples.
+ * ------------------------------------------------------------------------------------------- */
+void orc_mlp_forward(int nlayers, const int *dims, const float *const *W, const float *const *b,
+                     const int *act, long nbatch, const float *x, float *out)
+{
+  int maxd = 0;
+  for (int n = 0; n <= nlayers; n++) if (dims[n] > maxd) maxd = dims[n];
+#pragma omp parallel
+  {
+    float *a0 = (float *)malloc(sizeof(float) * maxd), *a1 = (float *)malloc(sizeof(float) * maxd);
+#pragma omp for schedule(static)
+    for (long j = 0; j < nbatch; j++) {
+      const float *in = x + (size_t)dims[0] * j;
+      for (int n = 0; n < nlayers; n++) {
+        int nin = dims[n], nout = dims[n + 1];
+        float *dst = (n == nlayers - 1) ? out + (size_t)nout * j : ((n & 1) ? a1 : a0);
+        const float *w = W[n];
+        for (int i = 0; i < nout; i++) {
+          float acc = 0.0f;
+          for (int k = 0; k < nin; k++) acc = fmaf(w[(size_t)k * nout + i], in[k], acc);
+          dst[i] = activate(act[n], acc + b[n][i]);
+        }
+        in = dst;
+      }
+    }
+    free(a0); free(a1);
+  }
+}
+
+/* (sigma*y + mu)^8 * coldry; neural/mod_network_rrtmgp.F90:209-219; y already includes bias
+ * (the caller's MLP applied the linear last-layer activation).  Optional SW combine
+ * :224-229 when tau_abs != NULL: tau_tot = tau_abs + tau_ray, ssa = tau_ray/tau_tot. */
+void orc_nn_tau_post(int ngpt, long nbatch, float *y, const float *mean, const float *std,
+                     const float *coldry, float *tau_abs_to_tot)
+{
+  for (long j = 0; j < nbatch; j++)
+    for (int i = 0; i < ngpt; i++) {
+      size_t idx = (size_t)i + (size_t)ngpt * j;
+      float t = std[i] * y[idx] + mean[i];
+      float t2 = t * t, t4 = t2 * t2, t8 = t4 * t4;
+      float v = t8 * coldry[j];
+      if (tau_abs_to_tot) {
+        tau_abs_to_tot[idx] = tau_abs_to_tot[idx] + v;
+        v = v / tau_abs_to_tot[idx];
+      }
+      y[idx] = v;
+    }
+}
+
+/* pfrac = y^2 ; neural/mod_network_rrtmgp.F90:309-312 */
+void orc_square(long n, float *y)
+{
+  for (long i = 0; i < n; i++) y[i] = y[i] * y[i];
+}
+
+/* rrtmgp/kernels/mo_gas_optics_kernels.F90:1024-1043 (interpolate1D) */
+static void interpolate1D(float val, float offset, float delta, int ntemp, int nbnd,
+                          const float *table, float *res)
+{
+  float val0 = (val - offset) / delta;
+  int iv = (int)val0; /* Fortran int(): truncation toward zero */
+  float frac = val0 - (float)iv;
+  int index = iv + 1;
+  if (index < 1) index = 1;
+  if (index > ntemp - 1) index = ntemp - 1;
+  for (int b = 0; b < nbnd; b++) {
+    const float *t = table + (size_t)ntemp * b; /* totplnk(nPlanckTemp, nbnd) */
+    res[b] = t[index - 1] + frac * (t[index] - t[index - 1]);
+  }
+}
+
+/* rrtmgp/kernels/mo_gas_optics_kernels.F90:615-683 (compute_Planck_source_nn)
+ * sfc_lay is 1-based (mo_gas_optics_rrtmgp.F90:402: merge(1,nlay,play(1,1) > play(nlay,1))).
+ * band_lims_gpt(2,nbnd) 1-based.  pfrac is overwritten with lay_source. */
+void orc_planck_source_nn(int ncol, int nlay, int nbnd, int ngpt, int ntemp,
+                          const float *tlay, const float *tlev, const float *tsfc, int sfc_lay,
+                          const int *band_lims_gpt, float temp_ref_min, float totplnk_delta,
+                          const float *totplnk, float *sfc_source, float *sfc_source_Jac,
+                          float *pfrac, float *lev_source)
+{
+  float *pf_sfc = (float *)malloc(sizeof(float) * nbnd * 4);
+  float *pf_sfcJ = pf_sfc + nbnd, *pf_lev = pf_sfc + 2 * nbnd, *pf_lay = pf_sfc + 3 * nbnd;
+  for (int icol = 0; icol < ncol; icol++) {
+    const float *tl = tlev + (size_t)(nlay + 1) * icol;
+    interpolate1D(tsfc[icol], temp_ref_min, totplnk_delta, ntemp, nbnd, totplnk, pf_sfc);
+    interpolate1D(tsfc[icol] + 1.0f, temp_ref_min, totplnk_delta, ntemp, nbnd, totplnk, pf_sfcJ);
+    interpolate1D(tl[nlay], temp_ref_min, totplnk_delta, ntemp, nbnd, totplnk, pf_lev);
+    float *pf = pfrac + (size_t)ngpt * nlay * icol;
+    float *lv = lev_source + (size_t)ngpt * (nlay + 1) * icol;
+    for (int b = 0; b < nbnd; b++)
+      for (int g = band_lims_gpt[2 * b] - 1; g < band_lims_gpt[2 * b + 1]; g++) {
+        lv[g + (size_t)ngpt * nlay] = pf[g + (size_t)ngpt * (nlay - 1)] * pf_lev[b];
+        float ps = pf[g + (size_t)ngpt * (sfc_lay - 1)];
+        sfc_source[g + (size_t)ngpt * icol] = ps * pf_sfc[b];
+        sfc_source_Jac[g + (size_t)ngpt * icol] = ps * (pf_sfcJ[b] - pf_sfc[b]);
+      }
+    for (int ilay = 0; ilay < nlay; ilay++) {
+      interpolate1D(tl[ilay], temp_ref_min, totplnk_delta, ntemp, nbnd, totplnk, pf_lev);
+      interpolate1D(tlay[ilay + (size_t)nlay * icol], temp_ref_min, totplnk_delta, ntemp, nbnd, totplnk, pf_lay);
+      for (int b = 0; b < nbnd; b++)
+        for (int g = band_lims_gpt[2 * b] - 1; g < band_lims_gpt[2 * b + 1]; g++) {
+          size_t i = g + (size_t)ngpt * ilay;
+          lv[i] = pf[i] * pf_lev[b];
+          pf[i] = pf[i] * pf_lay[b];
+        }
+    }
+  }
+  free(pf_sfc);
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * LW no-scattering solver, one angle: rte/kernels/mo_rte_solver_kernels.F90:119-330
+ * with lw_source_noscat :742-776 (top-at-1 indexing hard-coded: Appendix B-1 quirk, reproduced),
+ * lw_transport_noscat_dn :982-1009, lw_transport_noscat_up :950-980.
+ * If gpt_up/gpt_dn are non-NULL the g-point radiances*fac are ACCUMULATED into them (nmus>1 path,
+ * :383-412); otherwise broadband fluxes are written with the 4-way partial sums (:296-318).
+ * ------------------------------------------------------------------------------------------- */
+static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weight,
+                          const float *inc, const float *tau, const float *lay, const float *lev,
+                          const float *emis, const float *sfc, float *radn_up, float *radn_dn,
+                          float *tau_loc, float *trans, float *src_up, float *src_dn)
+{
+  const float tau_thresh = sqrtf(FLT_EPSILON);
+  int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
+  for (int g = 0; g < ngpt; g++)
+    radn_dn[g + (size_t)ngpt * top] = inc[g] / (2.0f * PI_F * weight);
+  for (int l = 0; l < nlay; l++)
+    for (int g = 0; g < ngpt; g++) {
+      size_t i = g + (size_t)ngpt * l;
+      tau_loc[i] = tau[i] * D;
+      trans[i] = expf(-tau_loc[i]);
+    }
+  for (int l = 0; l < nlay; l++)
+    for (int g = 0; g < ngpt; g++) {
+      size_t i = g + (size_t)ngpt * l;
+      float t = tau_loc[i], T = trans[i], fact;
+      if (t > tau_thresh) fact = (1.0f - T) / t - T;
+      else fact = t * (0.5f - 1.0f / 3.0f * t);
+      float lvdn = lev[g + (size_t)ngpt * (l + 1)], lvup = lev[i], ly = lay[i];
+      src_dn[i] = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
+      src_up[i] = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
+    }
+  if (top_at_1) {
+    for (int l = 1; l <= nlay; l++)
+      for (int g = 0; g < ngpt; g++)
+        radn_dn[g + (size_t)ngpt * l] = trans[g + (size_t)ngpt * (l - 1)] * radn_dn[g + (size_t)ngpt * (l - 1)] +
+                                        src_dn[g + (size_t)ngpt * (l - 1)];
+  } else {
+    for (int l = nlay - 1; l >= 0; l--)
+      for (int g = 0; g < ngpt; g++)
+        radn_dn[g + (size_t)ngpt * l] = trans[g + (size_t)ngpt * l] * radn_dn[g + (size_t)ngpt * (l + 1)] +
+                                        src_dn[g + (size_t)ngpt * l];
+  }
+  for (int g = 0; g < ngpt; g++) {
+    size_t i = g + (size_t)ngpt * sfcl;
+    radn_up[i] = radn_dn[i] * (1.0f - emis[g]) + emis[g] * sfc[g];
+  }
+  if (top_at_1) {
+    for (int l = nlay - 1; l >= 0; l--)
+      for (int g = 0; g < ngpt; g++)
+        radn_up[g + (size_t)ngpt * l] = trans[g + (size_t)ngpt * l] * radn_up[g + (size_t)ngpt * (l + 1)] +
+                                        src_up[g + (size_t)ngpt * l];
+  } else {
+    for (int l = 1; l <= nlay; l++)
+      for (int g = 0; g < ngpt; g++)
+        radn_up[g + (size_t)ngpt * l] = trans[g + (size_t)ngpt * (l - 1)] * radn_up[g + (size_t)ngpt * (l - 1)] +
+                                        src_up[g + (size_t)ngpt * (l - 1)];
+  }
+}
+
+/* lw_solver_noscat_GaussQuad :332-415 (+ lw_solver_noscat per angle); do_rescaling = false,
+ * compute_Jac = false (rte/mo_rte_rrtmgp_config.F90:28). Ds/weights have nmus entries. */
+void orc_lw_solver_noscat_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                    const float *Ds, const float *weights, const float *inc_flux,
+                                    const float *tau, const float *lay_source, const float *lev_source,
+                                    const float *sfc_emis, const float *sfc_source,
+                                    float *flux_up, float *flux_dn)
+{
+#pragma omp parallel
+  {
+    size_t nl = (size_t)ngpt * nlay, nv = (size_t)ngpt * (nlay + 1);
+    float *buf = (float *)malloc(sizeof(float) * (4 * nl + 4 * nv));
+    float *tau_loc = buf, *trans = buf + nl, *su = buf + 2 * nl, *sd = buf + 3 * nl;
+    float *ru = buf + 4 * nl, *rd = ru + nv, *acc_u = rd + nv, *acc_d = acc_u + nv;
+#pragma omp for schedule(static)
+    for (int icol = 0; icol < ncol; icol++) {
+      const float *tc = tau + nl * icol, *lc = lay_source + nl * icol, *vc = lev_source + nv * icol;
+      const float *ec = sfc_emis + (size_t)ngpt * icol, *sc = sfc_source + (size_t)ngpt * icol;
+      const float *ic = inc_flux + (size_t)ngpt * icol;
+      float *fu = flux_up + (size_t)(nlay + 1) * icol, *fd = flux_dn + (size_t)(nlay + 1) * icol;
+      for (int imu = 0; imu < nmus; imu++) {
+        lw_noscat_col(ngpt, nlay, top_at_1, Ds[imu], weights[imu], ic, tc, lc, vc, ec, sc, ru, rd,
+                      tau_loc, trans, su, sd);
+        float fac = 2.0f * PI_F * weights[imu];
+        if (nmus == 1) {
+          for (int l = 0; l <= nlay; l++) {
+            if (ngpt % 4 == 0) {
+              float su4[4] = {0, 0, 0, 0}, sd4[4] = {0, 0, 0, 0};
+              for (int g = 0; g < ngpt; g += 4)
+                for (int j = 0; j < 4; j++) {
+                  su4[j] = su4[j] + fac * ru[g + j + (size_t)ngpt * l];
+                  sd4[j] = sd4[j] + fac * rd[g + j + (size_t)ngpt * l];
+                }
+              fu[l] = su4[0] + su4[1] + su4[2] + su4[3];
+              fd[l] = sd4[0] + sd4[1] + sd4[2] + sd4[3];
+            } else {
+              float a = 0, b = 0;
+              for (int g = 0; g < ngpt; g++) { a += ru[g + (size_t)ngpt * l]; b += rd[g + (size_t)ngpt * l]; }
+              fu[l] = a; fd[l] = b;   /* quirk Appendix B-5: radiances, no fac, when ngpt%4 != 0 */
+            }
+          }
+        } else {
+          for (size_t i = 0; i < nv; i++) {
+            if (imu == 0) { acc_u[i] = fac * ru[i]; acc_d[i] = fac * rd[i]; }
+            else { acc_u[i] = acc_u[i] + fac * ru[i]; acc_d[i] = acc_d[i] + fac * rd[i]; }
+          }
+        }
+      }
+      if (nmus > 1) /* sum_broadband rte/kernels/mo_fluxes_broadband_kernels.F90:31-39 */
+        for (int l = 0; l <= nlay; l++) {
+          float a = 0, b = 0;
+          for (int g = 0; g < ngpt; g++) { a += acc_u[g + (size_t)ngpt * l]; b += acc_d[g + (size_t)ngpt * l]; }
+          fu[l] = a; fd[l] = b;
+        }
+    }
+    free(buf);
+  }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * SW two-stream: rte/kernels/mo_rte_solver_kernels.F90:541-692 (sw_solver_2stream),
+ * sw_two_stream_source :1366-1480, adding :1526-1637.  k_min = 1e-4 (sp, :76-82).
+ * ------------------------------------------------------------------------------------------- */
+void orc_sw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                           const float *inc_flux_dif, const float *tau, const float *ssa, const float *gg,
+                           const float *mu0, const float *sfc_alb_dir, const float *sfc_alb_dif,
+                           float *flux_up, float *flux_dn, float *flux_dir)
+{
+  const float k_min = 1.e-4f, eps = FLT_EPSILON;
+#pragma omp parallel
+  {
+    size_t nl = (size_t)ngpt * nlay, nv = (size_t)ngpt * (nlay + 1);
+    float *buf = (float *)malloc(sizeof(float) * (5 * nl + 5 * nv + ngpt));
+    float *Rdif = buf, *Tdif = buf + nl, *src_up = buf + 2 * nl, *src_dn = buf + 3 * nl, *denom = buf + 4 * nl;
+    float *rup = buf + 5 * nl, *rdn = rup + nv, *rdir = rdn + nv, *albedo = rdir + nv, *src = albedo + nv;
+    float *src_sfc = src + nv;
+#pragma omp for schedule(static)
+    for (int icol = 0; icol < ncol; icol++) {
+      const float *t = tau + nl * icol, *w0 = ssa + nl * icol, *g = gg + nl * icol;
+      float m0 = mu0[icol], mu0_inv = 1.0f / m0;
+      int top = top_at_1 ? 0 : nlay;
+      for (int i = 0; i < ngpt; i++) {
+        rdir[i + (size_t)ngpt * top] = inc_flux[i + (size_t)ngpt * icol] * m0;
+        rdn[i + (size_t)ngpt * top] = inc_flux_dif[i + (size_t)ngpt * icol];
+      }
+      float *dir_trans = NULL;
+      for (int j = 0; j < nlay; j++) {
+        int ilev = top_at_1 ? j : nlay - 1 - j;
+        float *dir_inc = rdir + (size_t)ngpt * (top_at_1 ? ilev : ilev + 1);
+        dir_trans = rdir + (size_t)ngpt * (top_at_1 ? ilev + 1 : ilev);
+        for (int i = 0; i < ngpt; i++) {
+          size_t x = i + (size_t)ngpt * ilev;
+          float Tnoscat = expf(-t[x] * mu0_inv);
+          float gamma1 = (8.0f - w0[x] * (5.0f + 3.0f * g[x])) * .25f;
+          float gamma2 = 3.0f * (w0[x] * (1.0f - g[x])) * .25f;
+          float gamma3 = (2.0f - 3.0f * m0 * g[x]) * .25f;
+          float gamma4 = 1.0f - gamma3;
+          float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
+          float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
+          float k = sqrtf(fmaxf((gamma1 - gamma2) * (gamma1 + gamma2), k_min));
+          float emk = expf(-t[x] * k);
+          float em2k = emk * emk;
+          float k2e = 2.0f * k * emk;
+          float RT = 1.0f / (k * (1.0f + em2k) + gamma1 * (1.0f - em2k));
+          Rdif[x] = RT * gamma2 * (1.0f - em2k);
+          Tdif[x] = RT * 2.0f * k * emk;
+          float k_mu = k * m0, k_mu2 = k_mu * k_mu, k_g3 = k * gamma3, k_g4 = k * gamma4;
+          float dd = (fabsf(1.0f - k_mu2) >= eps) ? (1.0f - k_mu2) : eps;
+          RT = w0[x] * RT / dd;
+          float Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
+                             k2e * (gamma3 - alpha2 * m0) * Tnoscat);
+          float Tdir = RT * (k2e * (gamma4 + alpha1 * m0) -
+                             Tnoscat * ((1.0f + k_mu) * (alpha1 + k_g4) - (1.0f - k_mu) * (alpha1 - k_g4) * em2k));
+          Rdir = fmaxf(0.0f, fminf(Rdir, (1.0f - Tnoscat)));
+          Tdir = fmaxf(0.0f, fminf(Tdir, (1.0f - Tnoscat - Rdir)));
+          src_up[x] = Rdir * dir_inc[i];
+          src_dn[x] = Tdir * dir_inc[i];
+          dir_trans[i] = Tnoscat * dir_inc[i];
+        }
+      }
+      const float *adir = sfc_alb_dir + (size_t)ngpt * icol, *adif = sfc_alb_dif + (size_t)ngpt * icol;
+      for (int i = 0; i < ngpt; i++) src_sfc[i] = dir_trans[i] * adir[i];
+      /* adding */
+      if (top_at_1) {
+        for (int i = 0; i < ngpt; i++) {
+          albedo[i + (size_t)ngpt * nlay] = adif[i];
+          src[i + (size_t)ngpt * nlay] = src_sfc[i];
+        }
+        for (int l = nlay - 1; l >= 0; l--)
+          for (int i = 0; i < ngpt; i++) {
+            size_t x = i + (size_t)ngpt * l, xp = x + ngpt;
+            denom[x] = 1.0f / (1.0f - Rdif[x] * albedo[xp]);
+            albedo[x] = Rdif[x] + Tdif[x] * Tdif[x] * albedo[xp] * denom[x];
+            src[x] = src_up[x] + Tdif[x] * denom[x] * (src[xp] + albedo[xp] * src_dn[x]);
+          }
+        for (int i = 0; i < ngpt; i++) rup[i] = rdn[i] * albedo[i] + src[i];
+        for (int l = 1; l <= nlay; l++)
+          for (int i = 0; i < ngpt; i++) {
+            size_t x = i + (size_t)ngpt * l, xm = x - ngpt;
+            rdn[x] = (Tdif[xm] * rdn[xm] + Rdif[xm] * src[x] + src_dn[xm]) * denom[xm];
+            rup[x] = rdn[x] * albedo[x] + src[x];
+          }
+      } else {
+        for (int i = 0; i < ngpt; i++) { albedo[i] = adif[i]; src[i] = src_sfc[i]; }
+        for (int l = 0; l < nlay; l++)
+          for (int i = 0; i < ngpt; i++) {
+            size_t x = i + (size_t)ngpt * l, xp = x + ngpt;
+            denom[x] = 1.0f / (1.0f - Rdif[x] * albedo[x]);
+            albedo[xp] = Rdif[x] + Tdif[x] * Tdif[x] * albedo[x] * denom[x];
+            src[xp] = src_up[x] + Tdif[x] * denom[x] * (src[x] + albedo[x] * src_dn[x]);
+          }
+        for (int i = 0; i < ngpt; i++) {
+          size_t x = i + (size_t)ngpt * nlay;
+          rup[x] = rdn[x] * albedo[x] + src[x];
+        }
+        for (int l = nlay - 1; l >= 0; l--)
+          for (int i = 0; i < ngpt; i++) {
+            size_t x = i + (size_t)ngpt * l, xp = x + ngpt;
+            rdn[x] = (Tdif[x] * rdn[xp] + Rdif[x] * src[x] + src_dn[x]) * denom[x];
+            rup[x] = rdn[x] * albedo[x] + src[x];
+          }
+      }
+      float *fu = flux_up + (size_t)(nlay + 1) * icol, *fd = flux_dn + (size_t)(nlay + 1) * icol;
+      float *fr = flux_dir + (size_t)(nlay + 1) * icol;
+      for (int l = 0; l <= nlay; l++) {
+        if (ngpt % 4 == 0) {
+          float su[4] = {0, 0, 0, 0}, sd[4] = {0, 0, 0, 0}, sr[4] = {0, 0, 0, 0};
+          for (int i = 0; i < ngpt; i += 4)
+            for (int j = 0; j < 4; j++) {
+              size_t x = i + j + (size_t)ngpt * l;
+              su[j] = su[j] + rup[x];
+              sr[j] = sr[j] + rdir[x];
+              sd[j] = sd[j] + rdn[x] + rdir[x];
+            }
+          fu[l] = su[0] + su[1] + su[2] + su[3];
+          fd[l] = sd[0] + sd[1] + sd[2] + sd[3];
+          fr[l] = sr[0] + sr[1] + sr[2] + sr[3];
+        } else {
+          float a = 0, b = 0, c = 0;
+          for (int i = 0; i < ngpt; i++) {
+            size_t x = i + (size_t)ngpt * l;
+            c += rdir[x]; a += rup[x]; b += rdn[x] + rdir[x];
+          }
+          fu[l] = a; fd[l] = b; fr[l] = c;
+        }
+      }
+    }
+    free(buf);
+  }
+}
+
+/* rte/mo_rte_lw.F90:429-447 (expand): band values -> g-points. band_lims 1-based (2,nbnd). */
+void orc_expand(int nband, int ngpt, int ncol, const int *band_lims, const float *arr_in, float *arr_out)
+{
+  for (int icol = 0; icol < ncol; icol++)
+    for (int b = 0; b < nband; b++)
+      for (int g = band_lims[2 * b] - 1; g < band_lims[2 * b + 1]; g++)
+        arr_out[g + (size_t)ngpt * icol] = arr_in[b + (size_t)nband * icol];
+}
+
+int orc_num_threads(void)
+{
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+void orc_set_num_threads(int n)
+{
+#ifdef _OPENMP
+  omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}

@@ -1,0 +1,513 @@
+// api.cpp -- the C ABI (include/rrtmgpnn.h): contexts, networks, argument checking and dispatch.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace rrtmgpnn {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string &msg) { g_last_error = msg; }
+
+int fail(int code, const std::string &msg)
+{
+  g_last_error = msg;
+  return code;
+}
+
+// ---- RBIN reader (format: tools/rbin.py) ----
+struct RbinArray {
+  int dtype = 0;
+  std::vector<int> dims;
+  std::vector<char> data;
+  size_t count() const
+  {
+    size_t n = 1;
+    for (int d : dims) n *= (size_t)d;
+    return n;
+  }
+};
+
+static int read_rbin(const char *path, std::map<std::string, RbinArray> &out)
+{
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return fail(RRTMGPNN_ERR_IO, std::string("cannot open ") + path);
+  char magic[4];
+  uint32_t ver = 0, count = 0;
+  f.read(magic, 4);
+  f.read((char *)&ver, 4);
+  f.read((char *)&count, 4);
+  if (!f || std::memcmp(magic, "RBIN", 4) != 0 || ver != 1)
+    return fail(RRTMGPNN_ERR_IO, std::string(path) + ": not an RBIN v1 file");
+  for (uint32_t e = 0; e < count; e++) {
+    char name[64];
+    uint32_t dt = 0, nd = 0;
+    f.read(name, 64);
+    f.read((char *)&dt, 4);
+    f.read((char *)&nd, 4);
+    if (!f || dt > 2 || nd > 8) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": corrupt entry header");
+    RbinArray a;
+    a.dtype = (int)dt;
+    for (uint32_t i = 0; i < nd; i++) {
+      uint32_t d = 0;
+      f.read((char *)&d, 4);
+      a.dims.push_back((int)d);
+    }
+    size_t isz = dt == 2 ? 1 : 4;
+    a.data.resize(a.count() * isz);
+    f.read(a.data.data(), (std::streamsize)a.data.size());
+    if (!f) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": truncated");
+    name[63] = 0;
+    out[std::string(name)] = std::move(a);
+  }
+  return RRTMGPNN_OK;
+}
+
+template <typename T>
+static std::vector<T> as_vec(const RbinArray &a)
+{
+  std::vector<T> v(a.count());
+  std::memcpy(v.data(), a.data.data(), v.size() * sizeof(T));
+  return v;
+}
+
+static int finalize_network(rrtmgpnn_network *net)
+{
+  // raw device image: all weights then all biases
+  size_t total = 0;
+  for (int n = 0; n < net->nlayers; n++) {
+    net->raw_w_off[n] = total;
+    total += net->w[n].size();
+  }
+  for (int n = 0; n < net->nlayers; n++) {
+    net->raw_b_off[n] = total;
+    total += net->b[n].size();
+  }
+  std::vector<float> raw(total);
+  for (int n = 0; n < net->nlayers; n++) {
+    std::memcpy(raw.data() + net->raw_w_off[n], net->w[n].data(), net->w[n].size() * 4);
+    std::memcpy(raw.data() + net->raw_b_off[n], net->b[n].data(), net->b[n].size() * 4);
+  }
+  RRTMGPNN_HIP(hipSetDevice(net->device));
+  RRTMGPNN_HIP(hipMalloc(&net->d_raw, total * 4));
+  RRTMGPNN_HIP(hipMemcpy(net->d_raw, raw.data(), total * 4, hipMemcpyHostToDevice));
+  return pack_network(net);
+}
+
+static int check_ctx(rrtmgpnn_context *ctx)
+{
+  if (!ctx) return fail(RRTMGPNN_ERR_ARGUMENT, "null context");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return fail(RRTMGPNN_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+  return RRTMGPNN_OK;
+}
+
+static int band_args(int nbnd, const int *lims, int ngpt, BandArgs &b)
+{
+  if (nbnd < 1 || nbnd > kMaxBands || !lims) return fail(RRTMGPNN_ERR_ARGUMENT, "band limits: need 1..64 bands");
+  b.nbnd = nbnd;
+  for (int i = 0; i < nbnd; i++) {
+    b.lims[2 * i] = lims[2 * i];
+    b.lims[2 * i + 1] = lims[2 * i + 1];
+    if (lims[2 * i] < 1 || lims[2 * i + 1] > ngpt || lims[2 * i] > lims[2 * i + 1])
+      return fail(RRTMGPNN_ERR_ARGUMENT, "band limits out of range [1, ngpt]");
+  }
+  return RRTMGPNN_OK;
+}
+
+}  // namespace rrtmgpnn
+
+using namespace rrtmgpnn;
+
+int rrtmgpnn_context::workspace(size_t bytes, void **out)
+{
+  if (bytes > ws_bytes) {
+    if (ws) {
+      (void)hipStreamSynchronize(stream);
+      (void)hipFree(ws);
+      ws = nullptr;
+      ws_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&ws, bytes);
+    if (e != hipSuccess) return fail(RRTMGPNN_ERR_DEVICE, std::string("workspace hipMalloc: ") + hipGetErrorString(e));
+    ws_bytes = bytes;
+  }
+  *out = ws;
+  return RRTMGPNN_OK;
+}
+
+extern "C" {
+
+int rrtmgpnn_version(void) { return 1; }
+
+const char *rrtmgpnn_last_error(void) { return g_last_error.c_str(); }
+
+int rrtmgpnn_context_create(int device, void *hip_stream, rrtmgpnn_context **ctx)
+{
+  if (!ctx) return fail(RRTMGPNN_ERR_ARGUMENT, "ctx out-pointer is null");
+  int ndev = 0;
+  RRTMGPNN_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(RRTMGPNN_ERR_ARGUMENT, "device ordinal out of range");
+  RRTMGPNN_HIP(hipSetDevice(device));
+  rrtmgpnn_context *c = new rrtmgpnn_context();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  if (hip_stream) {
+    c->stream = (hipStream_t)hip_stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return fail(RRTMGPNN_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    c->own_stream = true;
+  }
+  *ctx = c;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx)
+{
+  if (!ctx) return RRTMGPNN_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->ws) (void)hipFree(ctx->ws);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (ctx->own_stream) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    ctx->own_stream = false;
+  }
+  ctx->stream = (hipStream_t)hip_stream;
+  return RRTMGPNN_OK;
+}
+
+void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int rrtmgpnn_context_synchronize(rrtmgpnn_context *ctx)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  RRTMGPNN_HIP(hipStreamSynchronize(ctx->stream));
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_malloc(rrtmgpnn_context *ctx, long long bytes, void **dptr)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!dptr || bytes < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "malloc: bad arguments");
+  RRTMGPNN_HIP(hipMalloc(dptr, (size_t)(bytes ? bytes : 4)));
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_free(rrtmgpnn_context *ctx, void *dptr)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (dptr) RRTMGPNN_HIP(hipFree(dptr));
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_memcpy_h2d(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  RRTMGPNN_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+  RRTMGPNN_HIP(hipStreamSynchronize(ctx->stream));
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_memcpy_d2h(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  RRTMGPNN_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+  RRTMGPNN_HIP(hipStreamSynchronize(ctx->stream));
+  return RRTMGPNN_OK;
+}
+
+// ---- networks ----
+int rrtmgpnn_network_load(rrtmgpnn_context *ctx, const char *path, rrtmgpnn_network **net)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!path || !net) return fail(RRTMGPNN_ERR_ARGUMENT, "network_load: null argument");
+  std::map<std::string, RbinArray> m;
+  if (int rc = read_rbin(path, m)) return rc;
+  for (const char *k : {"dims", "activation", "input_min", "input_max"})
+    if (!m.count(k)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing " + k);
+  std::vector<int> dims = as_vec<int>(m["dims"]);
+  std::vector<int> act = as_vec<int>(m["activation"]);
+  int nl = (int)dims.size() - 1;
+  if (nl < 1 || nl > kMaxLayers || (int)act.size() != nl) return fail(RRTMGPNN_ERR_IO, "network_load: bad dims");
+  std::vector<std::vector<float>> W(nl), B(nl);
+  std::vector<const float *> wp(nl), bp(nl);
+  for (int n = 0; n < nl; n++) {
+    std::string wn = "w" + std::to_string(n + 1), bn = "b" + std::to_string(n + 1);
+    if (!m.count(wn) || !m.count(bn)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing layer " + wn);
+    W[n] = as_vec<float>(m[wn]);
+    B[n] = as_vec<float>(m[bn]);
+    if (W[n].size() != (size_t)dims[n] * dims[n + 1] || B[n].size() != (size_t)dims[n + 1])
+      return fail(RRTMGPNN_ERR_IO, std::string(path) + ": layer size mismatch");
+    wp[n] = W[n].data();
+    bp[n] = B[n].data();
+  }
+  std::vector<float> mn = as_vec<float>(m["input_min"]), mx = as_vec<float>(m["input_max"]);
+  std::vector<float> om, os;
+  if (m.count("output_mean")) {
+    om = as_vec<float>(m["output_mean"]);
+    os = as_vec<float>(m["output_std"]);
+  }
+  std::vector<char> names;
+  if (m.count("input_names")) names = m["input_names"].data;
+  return rrtmgpnn_network_create(ctx, nl, dims.data(), act.data(), wp.data(), bp.data(), mn.data(), mx.data(),
+                                 om.empty() ? nullptr : om.data(), os.empty() ? nullptr : os.data(),
+                                 names.empty() ? nullptr : names.data(), net);
+}
+
+int rrtmgpnn_network_create(rrtmgpnn_context *ctx, int nlayers, const int *dims, const int *activations,
+                            const float *const *weights, const float *const *biases, const float *input_min,
+                            const float *input_max, const float *output_mean, const float *output_std,
+                            const char *input_names, rrtmgpnn_network **out)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!out || !dims || !activations || !weights || !biases || !input_min || !input_max)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "network_create: null argument");
+  if (nlayers < 1 || nlayers > kMaxLayers) return fail(RRTMGPNN_ERR_ARGUMENT, "network_create: 1..7 layers");
+  if (dims[0] < 1 || dims[0] > kMaxInputs) return fail(RRTMGPNN_ERR_ARGUMENT, "network_create: 1..32 inputs");
+  rrtmgpnn_network *net = new rrtmgpnn_network();
+  net->device = ctx->device;
+  net->nlayers = nlayers;
+  for (int n = 0; n <= nlayers; n++) net->dims[n] = dims[n];
+  for (int n = 0; n < nlayers; n++) net->act[n] = activations[n];
+  net->w.resize(nlayers);
+  net->b.resize(nlayers);
+  for (int n = 0; n < nlayers; n++) {
+    if (dims[n + 1] < 1) {
+      delete net;
+      return fail(RRTMGPNN_ERR_ARGUMENT, "network_create: empty layer");
+    }
+    net->w[n].assign(weights[n], weights[n] + (size_t)dims[n] * dims[n + 1]);
+    net->b[n].assign(biases[n], biases[n] + dims[n + 1]);
+  }
+  int nx = dims[0], ny = dims[nlayers];
+  net->in_min.assign(input_min, input_min + nx);
+  net->in_max.assign(input_max, input_max + nx);
+  if (output_mean && output_std) {
+    net->out_mean.assign(output_mean, output_mean + ny);
+    net->out_std.assign(output_std, output_std + ny);
+  }
+  for (int i = 0; i < nx; i++) {
+    std::string s;
+    if (input_names) {
+      s.assign(input_names + 32 * i, 32);
+      size_t e = s.find_last_not_of(" \0", std::string::npos, 2);
+      s = (e == std::string::npos) ? std::string() : s.substr(0, e + 1);
+    }
+    net->input_names.push_back(s);
+  }
+  if (int rc = finalize_network(net)) {
+    rrtmgpnn_network_destroy(net);
+    return rc;
+  }
+  *out = net;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_network_destroy(rrtmgpnn_network *net)
+{
+  if (!net) return RRTMGPNN_OK;
+  (void)hipSetDevice(net->device);
+  if (net->d_raw) (void)hipFree(net->d_raw);
+  if (net->d_packed) (void)hipFree(net->d_packed);
+  delete net;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_network_get_dims(const rrtmgpnn_network *net, int *nlayers, int dims[8])
+{
+  if (!net || !nlayers || !dims) return fail(RRTMGPNN_ERR_ARGUMENT, "get_dims: null argument");
+  *nlayers = net->nlayers;
+  for (int n = 0; n < 8; n++) dims[n] = n <= net->nlayers ? net->dims[n] : 0;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_network_get_input_name(const rrtmgpnn_network *net, int i, char *buf, int buflen)
+{
+  if (!net || !buf || buflen < 1 || i < 0 || i >= net->dims[0])
+    return fail(RRTMGPNN_ERR_ARGUMENT, "get_input_name: bad argument");
+  std::snprintf(buf, (size_t)buflen, "%s", net->input_names[i].c_str());
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_network_get_input_scaling(const rrtmgpnn_network *net, float *mn, float *mx)
+{
+  if (!net || !mn || !mx) return fail(RRTMGPNN_ERR_ARGUMENT, "get_input_scaling: null argument");
+  for (int i = 0; i < net->dims[0]; i++) {
+    mn[i] = net->in_min[i];
+    mx[i] = net->in_max[i];
+  }
+  return RRTMGPNN_OK;
+}
+
+// ---- gas optics ----
+int rrtmgpnn_compute_nn_inputs(rrtmgpnn_context *ctx, int ncol, int nlay, int ninputs, const float *play,
+                               const float *tlay, const float *const *gas_conc, const int *gas_ndims,
+                               const rrtmgpnn_network *net, float *nn_inputs)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!net || !play || !tlay || !gas_conc || !gas_ndims || !nn_inputs || ncol < 0 || nlay < 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "compute_nn_inputs: bad argument");
+  if (ninputs != net->dims[0] || ninputs < 4 || ninputs > kMaxInputs)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "compute_nn_inputs: ninputs does not match the network");
+  if (!gas_conc[2] || !gas_conc[3] || gas_ndims[2] != 2 || gas_ndims[3] != 2)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "compute_nn_inputs: inputs 3 (h2o) and 4 (o3) must be 2-D (nlay,ncol)");
+  GasArgs g{};
+  for (int k = 0; k < ninputs; k++) {
+    g.p[k] = k >= 2 ? gas_conc[k] : nullptr;
+    g.nd[k] = k >= 2 ? gas_ndims[k] : 0;
+    if (k >= 2 && g.p[k] && (g.nd[k] < 0 || g.nd[k] > 2))
+      return fail(RRTMGPNN_ERR_ARGUMENT, "compute_nn_inputs: gas_ndims must be 0, 1 or 2");
+  }
+  std::vector<float> mm(2 * ninputs);
+  for (int k = 0; k < ninputs; k++) {
+    mm[k] = net->in_min[k];
+    mm[ninputs + k] = net->in_max[k];
+  }
+  return launch_nn_inputs(ctx, ncol, nlay, ninputs, play, tlay, g, mm.data(), nn_inputs);
+}
+
+int rrtmgpnn_get_col_dry(rrtmgpnn_context *ctx, int ncol, int nlay, const float *vmr_h2o, const float *plev,
+                         float *col_dry)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!vmr_h2o || !plev || !col_dry || ncol < 0 || nlay < 1) return fail(RRTMGPNN_ERR_ARGUMENT, "get_col_dry: bad argument");
+  return launch_col_dry(ctx, ncol, nlay, vmr_h2o, plev, col_dry);
+}
+
+int rrtmgpnn_interpolate_tlev(rrtmgpnn_context *ctx, int ncol, int nlay, const float *play, const float *plev,
+                              const float *tlay, float *tlev)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!play || !plev || !tlay || !tlev || ncol < 0 || nlay < 2)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "interpolate_tlev: bad argument (needs nlay >= 2)");
+  return launch_tlev(ctx, ncol, nlay, play, plev, tlay, tlev);
+}
+
+int rrtmgpnn_predict_nn_lw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *nn_inputs,
+                           const float *col_dry, const rrtmgpnn_network *const *nets, int nnets, float *tau,
+                           float *pfrac)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!nets || !nn_inputs || !col_dry || !tau || !pfrac || ncol < 0 || nlay < 1 || ngpt < 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_lw: bad argument");
+  long long N = (long long)ncol * nlay;
+  if (nnets == 2) {
+    const rrtmgpnn_network *A = nets[0], *B = nets[1];
+    if (!A || !B) return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_lw: null network");
+    if (A->dims[0] != ninputs || B->dims[0] != ninputs || A->dims[A->nlayers] != ngpt || B->dims[B->nlayers] != ngpt)
+      return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_lw: network sizes do not match (ninputs, ngpt)");
+    if (!A->has_out_scaling())
+      return fail(RRTMGPNN_ERR_ARGUMENT, "output_sgemm_tau: NN output scaling coefficients missing");
+    return launch_mlp(ctx, MLP_LW_PAIR, A, B, N, ngpt, nn_inputs, col_dry, tau, pfrac, nullptr);
+  } else if (nnets == 1) {
+    const rrtmgpnn_network *A = nets[0];
+    if (!A || A->dims[0] != ninputs || A->dims[A->nlayers] != 2 * ngpt)
+      return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_lw: single model must have 2*ngpt outputs");
+    if (!A->has_out_scaling())
+      return fail(RRTMGPNN_ERR_ARGUMENT, "output_sgemm_lw: NN output scaling coefficients missing");
+    return launch_mlp(ctx, MLP_LW_BOTH, A, nullptr, N, ngpt, nn_inputs, col_dry, tau, pfrac, nullptr);
+  }
+  return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_lw: nnets must be 1 or 2");
+}
+
+int rrtmgpnn_predict_nn_sw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *nn_inputs,
+                           const float *col_dry, const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!nets || !nets[0] || !nn_inputs || !col_dry || !tau || ncol < 0 || nlay < 1 || ngpt < 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_sw: bad argument");
+  const rrtmgpnn_network *A = nets[0];
+  if (A->dims[0] != ninputs || A->dims[A->nlayers] != ngpt)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_sw: network sizes do not match (ninputs, ngpt)");
+  if (!A->has_out_scaling()) return fail(RRTMGPNN_ERR_ARGUMENT, "output_sgemm_tau: NN output scaling coefficients missing");
+  long long N = (long long)ncol * nlay;
+  if (!ssa) return launch_mlp(ctx, MLP_SW_ABS, A, nullptr, N, ngpt, nn_inputs, col_dry, tau, nullptr, nullptr);
+  const rrtmgpnn_network *B = nets[1];
+  if (!B || B->dims[0] != ninputs || B->dims[B->nlayers] != ngpt || !B->has_out_scaling())
+    return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_sw: Rayleigh network missing or inconsistent");
+  return launch_mlp(ctx, MLP_SW_PAIR, A, B, N, ngpt, nn_inputs, col_dry, tau, ssa, g);
+}
+
+int rrtmgpnn_network_forward(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch, const float *x,
+                             float *out)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!net || !x || !out || nbatch < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "network_forward: bad argument");
+  if (net->d_packed) return launch_mlp(ctx, MLP_PLAIN, net, nullptr, nbatch, net->dims[net->nlayers], x, nullptr, out, nullptr, nullptr);
+  return launch_mlp_generic(ctx, net, nbatch, x, out);
+}
+
+int rrtmgpnn_compute_planck_source_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int nbnd, int ngpt, int nPlanckTemp,
+                                      const float *tlay, const float *tlev, const float *tsfc, int sfc_lay,
+                                      const int *band_lims_gpt, float temp_ref_min, float totplnk_delta,
+                                      const float *totplnk, float *sfc_source, float *sfc_source_Jac, float *pfrac,
+                                      float *lev_source)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!tlay || !tlev || !tsfc || !totplnk || !sfc_source || !sfc_source_Jac || !pfrac || !lev_source || ncol < 0 ||
+      nlay < 1 || ngpt < 1 || nPlanckTemp < 2 || sfc_lay < 1 || sfc_lay > nlay || !(totplnk_delta > 0.0f))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "compute_planck_source_nn: bad argument");
+  BandArgs b;
+  if (int rc = band_args(nbnd, band_lims_gpt, ngpt, b)) return rc;
+  return launch_planck_source(ctx, ncol, nlay, ngpt, nPlanckTemp, tlay, tlev, tsfc, sfc_lay, b, temp_ref_min,
+                              totplnk_delta, totplnk, sfc_source, sfc_source_Jac, pfrac, lev_source);
+}
+
+int rrtmgpnn_lw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                              const float *Ds, const float *weights, const float *inc_flux, const float *tau,
+                              const float *lay_source, const float *lev_source, const float *sfc_emis_gpt,
+                              const float *sfc_source, float *flux_up, float *flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!Ds || !weights || !tau || !lay_source || !lev_source || !sfc_emis_gpt || !sfc_source || !flux_up || !flux_dn ||
+      ngpt < 1 || nlay < 1 || ncol < 0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw_solver_noscat: bad argument");
+  return launch_lw_noscat(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, lay_source, lev_source,
+                          sfc_emis_gpt, sfc_source, flux_up, flux_dn);
+}
+
+int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                               const float *inc_flux, const float *inc_flux_dif, const float *tau, const float *ssa,
+                               const float *g, const float *mu0, const float *sfc_alb_dir_gpt,
+                               const float *sfc_alb_dif_gpt, float *flux_up, float *flux_dn, float *flux_dir)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!inc_flux || !tau || !ssa || !g || !mu0 || !sfc_alb_dir_gpt || !sfc_alb_dif_gpt || !flux_up || !flux_dn ||
+      !flux_dir || ngpt < 1 || nlay < 1 || ncol < 0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "sw_solver_2stream: bad argument");
+  return launch_sw_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, sfc_alb_dir_gpt,
+                           sfc_alb_dif_gpt, flux_up, flux_dn, flux_dir);
+}
+
+int rrtmgpnn_expand_band_to_gpt(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const int *band_lims_gpt,
+                                const float *arr_in, float *arr_out)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!arr_in || !arr_out || ncol < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "expand: bad argument");
+  BandArgs b;
+  if (int rc = band_args(nband, band_lims_gpt, ngpt, b)) return rc;
+  return launch_expand(ctx, nband, ngpt, ncol, b, arr_in, arr_out);
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// internal.hpp -- shared declarations of the rrtmgpnn runtime (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/rrtmgpnn.h"
+
+namespace rrtmgpnn {
+
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+#define RRTMGPNN_HIP(call)                                                                           \
+  do {                                                                                               \
+    hipError_t e_ = (call);                                                                          \
+    if (e_ != hipSuccess)                                                                            \
+      return ::rrtmgpnn::fail(RRTMGPNN_ERR_DEVICE, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Launch-error check after a kernel launch.
+#define RRTMGPNN_LAUNCH_CHECK(name)                                                                  \
+  do {                                                                                               \
+    hipError_t e_ = hipGetLastError();                                                               \
+    if (e_ != hipSuccess)                                                                            \
+      return ::rrtmgpnn::fail(RRTMGPNN_ERR_DEVICE, std::string(name) + " launch: " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kMaxLayers = 7;   // network layers (excluding input)
+constexpr int kMaxInputs = 32;  // NN input features
+constexpr int kMaxBands = 64;
+
+}  // namespace rrtmgpnn
+
+// Device workspace owned by a context: grown on demand, never shrunk, so steady-state calls
+// (and hipGraph capture of them) perform no allocation.
+struct rrtmgpnn_context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int num_cus = 256;
+  void *ws = nullptr;
+  size_t ws_bytes = 0;
+  int workspace(size_t bytes, void **out);
+};
+
+// A network: host copy of the model + device images.
+//   d_raw    : plain weights (n_in, n_out) per layer + biases (generic forward path)
+//   d_packed : MFMA operand image for the fused 3-layer kernel (see kernels_nn.hip)
+struct rrtmgpnn_network {
+  int device = 0;
+  int nlayers = 0;
+  int dims[rrtmgpnn::kMaxLayers + 1] = {0};
+  int act[rrtmgpnn::kMaxLayers] = {0};
+  std::vector<std::vector<float>> w, b;
+  std::vector<float> in_min, in_max, out_mean, out_std;
+  std::vector<std::string> input_names;
+  float *d_raw = nullptr;
+  size_t raw_w_off[rrtmgpnn::kMaxLayers] = {0}, raw_b_off[rrtmgpnn::kMaxLayers] = {0};
+  // packed MFMA image (3-layer networks only)
+  float *d_packed = nullptr;
+  int packed_floats = 0;
+  int k1s = 0, h1t = 0, h2t = 0, ngt = 0;
+  int off_l1 = 0, off_l2 = 0, off_l3 = 0, off_b1 = 0, off_b2 = 0, off_b3 = 0, off_std = 0, off_mean = 0;
+  bool has_out_scaling() const { return !out_mean.empty(); }
+};
+
+namespace rrtmgpnn {
+// kernels_nn.hip
+struct GasArgs {
+  const float *p[kMaxInputs];
+  int nd[kMaxInputs];
+};
+int launch_nn_inputs(rrtmgpnn_context *ctx, int ncol, int nlay, int nx, const float *play, const float *tlay,
+                     const GasArgs &gas, const float *in_min_max /*host 2*nx*/, float *out);
+int launch_col_dry(rrtmgpnn_context *ctx, int ncol, int nlay, const float *h2o, const float *plev, float *col_dry);
+int launch_tlev(rrtmgpnn_context *ctx, int ncol, int nlay, const float *play, const float *plev, const float *tlay,
+                float *tlev);
+enum MlpMode { MLP_PLAIN = 0, MLP_LW_PAIR = 1, MLP_SW_PAIR = 2, MLP_SW_ABS = 3, MLP_LW_BOTH = 4 };
+int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
+               long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
+               float *out2);
+int launch_mlp_generic(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch, const float *x,
+                       float *out);
+int pack_network(rrtmgpnn_network *net);
+// kernels_rte.hip
+struct BandArgs {
+  int lims[2 * kMaxBands];
+  int nbnd;
+};
+int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ntemp, const float *tlay,
+                         const float *tlev, const float *tsfc, int sfc_lay, const BandArgs &bands,
+                         float temp_ref_min, float totplnk_delta, const float *totplnk, float *sfc_source,
+                         float *sfc_source_Jac, float *pfrac, float *lev_source);
+int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
+                     const float *wts, const float *inc_flux, const float *tau, const float *lay_source,
+                     const float *lev_source, const float *sfc_emis, const float *sfc_source, float *flux_up,
+                     float *flux_dn);
+int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                      const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
+                      const float *mu0, const float *alb_dir, const float *alb_dif, float *flux_up,
+                      float *flux_dn, float *flux_dir);
+int launch_expand(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const BandArgs &bands, const float *in,
+                  float *out);
+}  // namespace rrtmgpnn

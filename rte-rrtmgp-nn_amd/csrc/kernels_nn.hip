@@ -1,0 +1,587 @@
+// kernels_nn.hip -- NN gas-optics kernels for gfx950 (MI355X).
+//
+//  * nn_inputs_kernel : compute_nn_inputs (rrtmgp/mo_gas_optics_rrtmgp.F90:618-798)
+//  * col_dry_kernel   : get_col_dry       (rrtmgp/mo_gas_optics_rrtmgp.F90:1662-1707)
+//  * tlev_kernel      : level temperatures (rrtmgp/mo_gas_optics_rrtmgp.F90:317-337)
+//  * mlp_pair_kernel  : the whole 3-layer MLP (softsign, softsign, linear) of ONE OR TWO networks
+//    that share the same inputs, fused with their post-processing:
+//       LW pair : tau = (std*(y+b)+mean)^8 * col_dry  and  pfrac = (y+b)^2
+//                 (neural/mod_network_rrtmgp.F90:125-317, predict_nn_lw_blas_sp
+//                  rrtmgp/kernels/mo_gas_optics_kernels.F90:690-774)
+//       SW pair : tau_abs, tau_ray -> tau = tau_abs + tau_ray, ssa = tau_ray/tau, g = 0
+//                 (:869-953 with INLINE_COMBINE, mod_network_rrtmgp.F90:224-229,
+//                  mo_gas_optics_rrtmgp.F90:560-567)
+//       LW both : one model with 2*ngpt outputs (output_sgemm_lw + :744-772)
+//    The reference runs this as three SGEMMs per model with activations materialised in
+//    (neurons x nlay*ncol) HBM arrays; here each wave keeps its 16 samples' activations in
+//    MFMA accumulators and chains layers register-to-register.
+//
+// MFMA mapping (v_mfma_f32_16x16x4_f32, exact f32, fmaf-chain numerics):
+//   lane l: j = l & 15, q = l >> 4.  A operand A[i=j][k=q], B operand B[k=q][n=j],
+//   accumulator register r holds D[row = 4q + r][col = j].
+//   Hidden layers compute H^T (units x samples):  A = packed W^T, B = activations.
+//   The output layer computes Y (samples x g-points): A = H2 taken straight from the hidden
+//   accumulators (sample on the lane, units in registers), B = packed W3.
+//   Hidden units are stored PERMUTED in the accumulators: physical row R = 4q + r of tile m
+//   holds logical unit u = 16m + 4r + q.  With that permutation, K-step (m, t) of the next
+//   layer feeds unit 16m + 4t + q from lane group q, i.e. every dot product is accumulated in
+//   ascending k order -- bit-identical to a sequential fmaf chain (the oracle's order).
+#include "internal.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace rrtmgpnn {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// compute_nn_inputs + col_dry are elementwise over (lay, col).
+// ------------------------------------------------------------------------------------------
+struct NnInArgs {
+  float mn[kMaxInputs];
+  float mx[kMaxInputs];
+};
+
+__global__ void nn_inputs_kernel(int ncol, int nlay, int nx, const float *__restrict__ play,
+                                 const float *__restrict__ tlay, GasArgs gas, NnInArgs sc, float *__restrict__ out)
+{
+  long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long N = (long long)ncol * nlay;
+  if (s >= N) return;
+  int ilay = (int)(s % nlay);
+  float *o = out + (size_t)nx * s;
+  o[0] = (tlay[s] - sc.mn[0]) / (sc.mx[0] - sc.mn[0]);
+  o[1] = (logf(play[s]) - sc.mn[1]) / (sc.mx[1] - sc.mn[1]);
+  o[2] = (sqrtf(sqrtf(gas.p[2][s])) - sc.mn[2]) / (sc.mx[2] - sc.mn[2]);
+  o[3] = (sqrtf(sqrtf(gas.p[3][s])) - sc.mn[3]) / (sc.mx[3] - sc.mn[3]);
+  for (int k = 4; k < nx; k++) {
+    float c;
+    const float *p = gas.p[k];
+    if (!p) c = 0.0f;
+    else if (gas.nd[k] == 0) c = p[0];
+    else if (gas.nd[k] == 1) c = p[ilay];
+    else c = p[s];
+    o[k] = (c - sc.mn[k]) / (sc.mx[k] - sc.mn[k]);
+  }
+}
+
+__global__ void col_dry_kernel(int ncol, int nlay, const float *__restrict__ h2o, const float *__restrict__ plev,
+                               float *__restrict__ col_dry)
+{
+  long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long long)ncol * nlay) return;
+  int icol = (int)(s / nlay), ilev = (int)(s % nlay);
+  const float m_dry = 0.028964f, m_h2o = 0.018016f, avogad = 6.02214076e23f, grav = 9.80665f;
+  const float *pl = plev + (size_t)(nlay + 1) * icol;
+  float v = h2o[s];
+  float delta_plev = fabsf(pl[ilev] - pl[ilev + 1]);
+  float fact = 1.0f / (1.0f + v);
+  float m_air = (m_dry + m_h2o * v) * fact;
+  col_dry[s] = 10.0f * delta_plev * avogad * fact / (1000.0f * m_air * 100.0f * grav);
+}
+
+__global__ void tlev_kernel(int ncol, int nlay, const float *__restrict__ play, const float *__restrict__ plev,
+                            const float *__restrict__ tlay, float *__restrict__ tlev)
+{
+  long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= (long long)ncol * (nlay + 1)) return;
+  int icol = (int)(s / (nlay + 1)), ilev = (int)(s % (nlay + 1));
+  const float *pa = play + (size_t)nlay * icol, *pv = plev + (size_t)(nlay + 1) * icol;
+  const float *ta = tlay + (size_t)nlay * icol;
+  float r;
+  if (ilev == 0)
+    r = ta[0] + (pv[0] - pa[0]) * (ta[1] - ta[0]) / (pa[1] - pa[0]);
+  else if (ilev == nlay)
+    r = ta[nlay - 1] + (pv[nlay] - pa[nlay - 1]) * (ta[nlay - 1] - ta[nlay - 2]) / (pa[nlay - 1] - pa[nlay - 2]);
+  else
+    r = (pa[ilev - 1] * ta[ilev - 1] * (pv[ilev] - pa[ilev]) + pa[ilev] * ta[ilev] * (pa[ilev - 1] - pv[ilev])) /
+        (pv[ilev] * (pa[ilev - 1] - pa[ilev]));
+  tlev[s] = r;
+}
+
+int launch_nn_inputs(rrtmgpnn_context *ctx, int ncol, int nlay, int nx, const float *play, const float *tlay,
+                     const GasArgs &gas, const float *in_min_max, float *out)
+{
+  NnInArgs sc;
+  for (int k = 0; k < nx; k++) { sc.mn[k] = in_min_max[k]; sc.mx[k] = in_min_max[nx + k]; }
+  long long N = (long long)ncol * nlay;
+  if (N == 0) return RRTMGPNN_OK;
+  hipLaunchKernelGGL(nn_inputs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream, ncol, nlay,
+                     nx, play, tlay, gas, sc, out);
+  RRTMGPNN_LAUNCH_CHECK("nn_inputs_kernel");
+  return RRTMGPNN_OK;
+}
+
+int launch_col_dry(rrtmgpnn_context *ctx, int ncol, int nlay, const float *h2o, const float *plev, float *col_dry)
+{
+  long long N = (long long)ncol * nlay;
+  if (N == 0) return RRTMGPNN_OK;
+  hipLaunchKernelGGL(col_dry_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream, ncol, nlay, h2o,
+                     plev, col_dry);
+  RRTMGPNN_LAUNCH_CHECK("col_dry_kernel");
+  return RRTMGPNN_OK;
+}
+
+int launch_tlev(rrtmgpnn_context *ctx, int ncol, int nlay, const float *play, const float *plev, const float *tlay,
+                float *tlev)
+{
+  long long N = (long long)ncol * (nlay + 1);
+  if (N == 0) return RRTMGPNN_OK;
+  hipLaunchKernelGGL(tlev_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream, ncol, nlay, play,
+                     plev, tlay, tlev);
+  RRTMGPNN_LAUNCH_CHECK("tlev_kernel");
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Activations: neural/mod_activation.F90 (bias added before, as bias_and_activation does).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float activate(int act, float x)
+{
+  switch (act) {
+  case RRTMGPNN_ACT_SOFTSIGN: return x / (fabsf(x) + 1.0f);
+  case RRTMGPNN_ACT_RELU: return fmaxf(0.0f, x);
+  case RRTMGPNN_ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
+  case RRTMGPNN_ACT_HARD_SIGMOID: return fmaxf(0.0f, fminf(1.0f, 0.2f * x + 0.5f));
+  case 5: return tanhf(x);
+  case 6: return expf(-x * x);
+  default: return x;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Packed image layout (floats) of a 3-layer network [nx, h1, h2, ny]:
+//   K1S = ceil(nx/4), H1T = ceil(h1/16), H2T = ceil(h2/16), NGT = ceil(ny/16)
+//   L1 [H1T][K1S][64]        lane(i,q): W1[k=4t+q][u(i)]         u(i) = 16mo + 4(i&3) + (i>>2)
+//   L2 [H2T][4*H1T][64]      lane(i,q): W2[k=16m+4t+q][u(i)]
+//   L3 [NGT][4*H2T][64]      lane(j,q): W3[k=16m+4t+q][g=16go+j]
+//   B1 [H1T*16], B2 [H2T*16] bias by PHYSICAL row R: b[16m + 4(R&3) + (R>>2)]
+//   B3, STD, MEAN [NGT*16]   by g
+// ------------------------------------------------------------------------------------------
+struct ImgLayout {
+  int l1, l2, l3, b1, b2, b3, sd, mn, total;
+};
+__host__ __device__ inline ImgLayout img_layout(int K1S, int H1T, int H2T, int NGT)
+{
+  ImgLayout L;
+  L.l1 = 0;
+  L.l2 = L.l1 + H1T * K1S * 64;
+  L.l3 = L.l2 + H2T * H1T * 4 * 64;
+  L.b1 = L.l3 + NGT * H2T * 4 * 64;
+  L.b2 = L.b1 + H1T * 16;
+  L.b3 = L.b2 + H2T * 16;
+  L.sd = L.b3 + NGT * 16;
+  L.mn = L.sd + NGT * 16;
+  L.total = L.mn + NGT * 16;
+  return L;
+}
+
+int pack_network(rrtmgpnn_network *net)
+{
+  if (net->nlayers != 3) return RRTMGPNN_OK;  // generic path only
+  const int nx = net->dims[0], h1 = net->dims[1], h2 = net->dims[2], ny = net->dims[3];
+  if (nx > kMaxInputs || h1 > 128 || h2 > 128) return RRTMGPNN_OK;
+  const int K1S = (nx + 3) / 4, H1T = (h1 + 15) / 16, H2T = (h2 + 15) / 16, NGT = (ny + 15) / 16;
+  ImgLayout L = img_layout(K1S, H1T, H2T, NGT);
+  std::vector<float> img(L.total, 0.0f);
+  const std::vector<float> &W1 = net->w[0], &W2 = net->w[1], &W3 = net->w[2];
+  auto unit = [](int m, int i) { return 16 * m + 4 * (i & 3) + (i >> 2); };
+  for (int mo = 0; mo < H1T; mo++)
+    for (int t = 0; t < K1S; t++)
+      for (int l = 0; l < 64; l++) {
+        int i = l & 15, q = l >> 4, k = 4 * t + q, u = unit(mo, i);
+        img[L.l1 + (mo * K1S + t) * 64 + l] = (k < nx && u < h1) ? W1[(size_t)k * h1 + u] : 0.0f;
+      }
+  for (int mo = 0; mo < H2T; mo++)
+    for (int s = 0; s < 4 * H1T; s++)
+      for (int l = 0; l < 64; l++) {
+        int i = l & 15, q = l >> 4, m = s >> 2, t = s & 3, k = 16 * m + 4 * t + q, u = unit(mo, i);
+        img[L.l2 + (mo * 4 * H1T + s) * 64 + l] = (k < h1 && u < h2) ? W2[(size_t)k * h2 + u] : 0.0f;
+      }
+  for (int go = 0; go < NGT; go++)
+    for (int s = 0; s < 4 * H2T; s++)
+      for (int l = 0; l < 64; l++) {
+        int j = l & 15, q = l >> 4, m = s >> 2, t = s & 3, k = 16 * m + 4 * t + q, g = 16 * go + j;
+        img[L.l3 + (go * 4 * H2T + s) * 64 + l] = (k < h2 && g < ny) ? W3[(size_t)k * ny + g] : 0.0f;
+      }
+  for (int m = 0; m < H1T; m++)
+    for (int R = 0; R < 16; R++) {
+      int u = unit(m, R);
+      img[L.b1 + 16 * m + R] = u < h1 ? net->b[0][u] : 0.0f;
+    }
+  for (int m = 0; m < H2T; m++)
+    for (int R = 0; R < 16; R++) {
+      int u = unit(m, R);
+      img[L.b2 + 16 * m + R] = u < h2 ? net->b[1][u] : 0.0f;
+    }
+  for (int g = 0; g < NGT * 16; g++) {
+    img[L.b3 + g] = g < ny ? net->b[2][g] : 0.0f;
+    img[L.sd + g] = (g < ny && net->has_out_scaling()) ? net->out_std[g] : 0.0f;
+    img[L.mn + g] = (g < ny && net->has_out_scaling()) ? net->out_mean[g] : 0.0f;
+  }
+  float *d = nullptr;
+  RRTMGPNN_HIP(hipMalloc(&d, sizeof(float) * img.size()));
+  RRTMGPNN_HIP(hipMemcpy(d, img.data(), sizeof(float) * img.size(), hipMemcpyHostToDevice));
+  net->d_packed = d;
+  net->packed_floats = L.total;
+  net->k1s = K1S; net->h1t = H1T; net->h2t = H2T; net->ngt = NGT;
+  net->off_l1 = L.l1; net->off_l2 = L.l2; net->off_l3 = L.l3; net->off_b1 = L.b1; net->off_b2 = L.b2;
+  net->off_b3 = L.b3; net->off_std = L.sd; net->off_mean = L.mn;
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused MLP kernel.
+// ------------------------------------------------------------------------------------------
+struct MlpArgs {
+  const float *x;        // (nx, nbatch)
+  const float *col_dry;  // (nbatch)
+  float *out0, *out1, *out2;
+  const float *imgA, *imgB;
+  int nx;
+  int ngpt;    // g-points of the physical outputs
+  int ngt;     // output g-tiles per network (NGT)
+  int imgA_floats, imgB_floats;
+  int actA[3], actB[3];
+  long long nbatch;
+};
+
+__device__ __forceinline__ float pow8(float t)
+{
+  float t2 = t * t, t4 = t2 * t2;
+  return t4 * t4;
+}
+
+// Hidden layers of one network for a 16-sample tile: returns H2 accumulators.
+template <int K1S, int H1T, int H2T>
+__device__ __forceinline__ void mlp_hidden(const float *__restrict__ img, int NGT, const float (&xv)[K1S], int lane,
+                                           int act1, int act2, floatx4 (&h2)[H2T])
+{
+  const ImgLayout L = img_layout(K1S, H1T, H2T, NGT);
+  const int q = lane >> 4;
+  floatx4 h1[H1T];
+#pragma unroll
+  for (int mo = 0; mo < H1T; mo++) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < K1S; t++)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(img[L.l1 + (mo * K1S + t) * 64 + lane], xv[t], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc[r] = activate(act1, acc[r] + img[L.b1 + 16 * mo + 4 * q + r]);
+    h1[mo] = acc;
+  }
+#pragma unroll
+  for (int mo = 0; mo < H2T; mo++) {
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < H1T; m++)
+#pragma unroll
+      for (int t = 0; t < 4; t++)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(img[L.l2 + (mo * 4 * H1T + 4 * m + t) * 64 + lane], h1[m][t], acc,
+                                                   0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc[r] = activate(act2, acc[r] + img[L.b2 + 16 * mo + 4 * q + r]);
+    h2[mo] = acc;
+  }
+}
+
+template <int H2T>
+__device__ __forceinline__ floatx4 mlp_out_tile(const float *__restrict__ img, int l3, int go, const floatx4 (&h2)[H2T],
+                                                int lane)
+{
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < H2T; m++)
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(h2[m][t], img[l3 + (go * 4 * H2T + 4 * m + t) * 64 + lane], acc, 0, 0,
+                                                 0);
+  return acc;
+}
+
+constexpr int kMlpThreads = 512;
+
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE>
+__global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
+{
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  // Stage both weight images in LDS (read by every tile of every wave of this block).
+  {
+    const int nA = a.imgA_floats, nB = (MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0;
+    for (int i = threadIdx.x; i < nA; i += blockDim.x) lds[i] = a.imgA[i];
+    for (int i = threadIdx.x; i < nB; i += blockDim.x) lds[nA + i] = a.imgB[i];
+  }
+  __syncthreads();
+  const float *imgA = lds;
+  const float *imgB = lds + a.imgA_floats;
+  const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
+  const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int NGT = a.ngt, nx = a.nx, ngpt = a.ngpt;
+  const ImgLayout LA = img_layout(AK, AH1, AH2, NGT);
+  const ImgLayout LB = img_layout(BK, BH1, BH2, NGT);
+  const long long ntiles = (a.nbatch + 15) / 16;
+
+  for (long long tile = (long long)blockIdx.x * nwaves + wave; tile < ntiles; tile += (long long)gridDim.x * nwaves) {
+    const long long s0 = tile * 16;
+    // Layer-1 B operand: x[sample s0+j][k = 4t+q]
+    float xv[AK];
+    {
+      const long long s = s0 + j;
+#pragma unroll
+      for (int t = 0; t < AK; t++) {
+        int k = 4 * t + q;
+        xv[t] = (s < a.nbatch && k < nx) ? a.x[(size_t)s * nx + k] : 0.0f;
+      }
+    }
+    floatx4 hA[AH2];
+    mlp_hidden<AK, AH1, AH2>(imgA, NGT, xv, lane, a.actA[0], a.actA[1], hA);
+    floatx4 hB[BH2];
+    if constexpr (MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) {
+      static_assert(BK == AK, "paired networks share their inputs");
+      mlp_hidden<BK, BH1, BH2>(imgB, NGT, xv, lane, a.actB[0], a.actB[1], hB);
+    }
+    // Per-lane sample rows of the output tile: s = s0 + 4q + r
+    float cd[4];
+    if constexpr (MODE != MLP_PLAIN && MODE != MLP_LW_BOTH) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        long long s = s0 + 4 * q + r;
+        cd[r] = s < a.nbatch ? a.col_dry[s] : 0.0f;
+      }
+    } else if constexpr (MODE == MLP_LW_BOTH) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        long long s = s0 + 4 * q + r;
+        cd[r] = s < a.nbatch ? a.col_dry[s] : 0.0f;
+      }
+    }
+    for (int go = 0; go < NGT; go++) {
+      const int g = 16 * go + j;
+      floatx4 yA = mlp_out_tile<AH2>(imgA, LA.l3, go, hA, lane);
+      const float bA = imgA[LA.b3 + g];
+      if constexpr (MODE == MLP_PLAIN) {
+        const int ny = ngpt;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          long long s = s0 + 4 * q + r;
+          if (s < a.nbatch && g < ny) a.out0[(size_t)s * ny + g] = activate(a.actA[2], yA[r] + bA);
+        }
+      } else if constexpr (MODE == MLP_LW_BOTH) {
+        // single model, outputs [0,ngpt) -> tau, [ngpt, 2 ngpt) -> pfrac (mo_gas_optics_kernels.F90:754-766)
+        const float sd = imgA[LA.sd + g], mn = imgA[LA.mn + g];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          long long s = s0 + 4 * q + r;
+          if (s >= a.nbatch) continue;
+          float y = yA[r] + bA;
+          if (g < ngpt) {
+            float t = sd * y;
+            t = t + mn;
+            a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];
+          } else if (g < 2 * ngpt) {
+            a.out1[(size_t)s * ngpt + (g - ngpt)] = y * y;
+          }
+        }
+      } else {
+        const float sdA = imgA[LA.sd + g], mnA = imgA[LA.mn + g];
+        if constexpr (MODE == MLP_SW_ABS) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            long long s = s0 + 4 * q + r;
+            if (s >= a.nbatch || g >= ngpt) continue;
+            float t = sdA * (yA[r] + bA);
+            t = t + mnA;
+            a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];
+          }
+        } else {
+          floatx4 yB = mlp_out_tile<BH2>(imgB, LB.l3, go, hB, lane);
+          const float bB = imgB[LB.b3 + g];
+          if constexpr (MODE == MLP_LW_PAIR) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              long long s = s0 + 4 * q + r;
+              if (s >= a.nbatch || g >= ngpt) continue;
+              float t = sdA * (yA[r] + bA);
+              t = t + mnA;
+              a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];  // tau
+              float p = yB[r] + bB;
+              a.out1[(size_t)s * ngpt + g] = p * p;  // pfrac
+            }
+          } else {  // MLP_SW_PAIR
+            const float sdB = imgB[LB.sd + g], mnB = imgB[LB.mn + g];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              long long s = s0 + 4 * q + r;
+              if (s >= a.nbatch || g >= ngpt) continue;
+              float ta = sdA * (yA[r] + bA);
+              ta = ta + mnA;
+              float vabs = pow8(ta) * cd[r];
+              float tr = sdB * (yB[r] + bB);
+              tr = tr + mnB;
+              float vray = pow8(tr) * cd[r];
+              float tot = vabs + vray;
+              a.out0[(size_t)s * ngpt + g] = tot;          // tau = tau_abs + tau_ray
+              a.out1[(size_t)s * ngpt + g] = vray / tot;   // ssa
+              if (a.out2) a.out2[(size_t)s * ngpt + g] = 0.0f;  // g
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE>
+static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
+{
+  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE>;
+  size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
+  if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
+  RRTMGPNN_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  long long ntiles = (a.nbatch + 15) / 16;
+  const int wpb = kMlpThreads / 64;
+  int per_cu = std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1)));
+  per_cu = std::min(per_cu, 2048 / kMlpThreads);
+  long long want = (ntiles + wpb - 1) / wpb;
+  long long grid = std::min<long long>(want, (long long)ctx->num_cus * per_cu);
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kMlpThreads), lds, ctx->stream, a);
+  RRTMGPNN_LAUNCH_CHECK("mlp_pair_kernel");
+  return RRTMGPNN_OK;
+}
+
+// Shape dispatch: the shipped models (Appendix A of SURVEY.md).
+//   LW g256 pair: abs 18-58-58-256 (K1S 5, H 4,4) + pfrac 18-16-16-256 (5, 1,1)
+//   SW g224 pair: 7-16-16-224 (2, 1,1) x 2
+//   LW g128 both: 18-64-64-256 (5, 4,4)
+#define RRTMGPNN_MLP_SHAPES(X) \
+  X(5, 4, 4)                   \
+  X(5, 1, 1)                   \
+  X(2, 1, 1)                   \
+  X(2, 2, 2)                   \
+  X(5, 2, 2)                   \
+  X(5, 5, 5)                   \
+  X(5, 3, 3)                   \
+  X(5, 8, 8)
+
+static bool shape_is(const rrtmgpnn_network *n, int k, int h1, int h2)
+{
+  return n && n->d_packed && n->k1s == k && n->h1t == h1 && n->h2t == h2;
+}
+
+int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
+               long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1, float *out2)
+{
+  if (nbatch <= 0) return RRTMGPNN_OK;
+  if (!A || !A->d_packed) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: network has no MFMA image (needs 3 layers)");
+  bool paired = (mode == MLP_LW_PAIR || mode == MLP_SW_PAIR);
+  if (paired && (!B || !B->d_packed)) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: second network has no MFMA image");
+  if (paired && (A->ngt != B->ngt || A->k1s != B->k1s || A->dims[0] != B->dims[0]))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "mlp: paired networks differ in inputs or outputs");
+  MlpArgs a{};
+  a.x = x; a.col_dry = col_dry; a.out0 = out0; a.out1 = out1; a.out2 = out2;
+  a.imgA = A->d_packed; a.imgA_floats = A->packed_floats;
+  a.imgB = paired ? B->d_packed : nullptr; a.imgB_floats = paired ? B->packed_floats : 0;
+  a.nx = A->dims[0]; a.ngpt = ngpt; a.ngt = A->ngt; a.nbatch = nbatch;
+  for (int i = 0; i < 3; i++) { a.actA[i] = A->act[i]; a.actB[i] = paired ? B->act[i] : 0; }
+
+#define TRY_PAIR(AK, AH1, AH2, BK, BH1, BH2, MODE) \
+  if (shape_is(A, AK, AH1, AH2) && shape_is(B, BK, BH1, BH2)) return launch_mlp_t<AK, AH1, AH2, BK, BH1, BH2, MODE>(ctx, a);
+#define TRY_ONE(AK, AH1, AH2, MODE) \
+  if (shape_is(A, AK, AH1, AH2)) return launch_mlp_t<AK, AH1, AH2, AK, 1, 1, MODE>(ctx, a);
+
+  switch (mode) {
+  case MLP_LW_PAIR:
+    TRY_PAIR(5, 4, 4, 5, 1, 1, MLP_LW_PAIR)
+    TRY_PAIR(5, 5, 5, 5, 2, 2, MLP_LW_PAIR)
+    TRY_PAIR(5, 4, 4, 5, 2, 2, MLP_LW_PAIR)
+    break;
+  case MLP_SW_PAIR:
+    TRY_PAIR(2, 1, 1, 2, 1, 1, MLP_SW_PAIR)
+    TRY_PAIR(2, 2, 2, 2, 1, 1, MLP_SW_PAIR)
+    TRY_PAIR(2, 2, 2, 2, 2, 2, MLP_SW_PAIR)
+    break;
+  case MLP_SW_ABS:
+#define X(K, H1, H2) TRY_ONE(K, H1, H2, MLP_SW_ABS)
+    RRTMGPNN_MLP_SHAPES(X)
+#undef X
+    break;
+  case MLP_LW_BOTH:
+#define X(K, H1, H2) TRY_ONE(K, H1, H2, MLP_LW_BOTH)
+    RRTMGPNN_MLP_SHAPES(X)
+#undef X
+    break;
+  case MLP_PLAIN:
+#define X(K, H1, H2) TRY_ONE(K, H1, H2, MLP_PLAIN)
+    RRTMGPNN_MLP_SHAPES(X)
+#undef X
+    break;
+  }
+#undef TRY_PAIR
+#undef TRY_ONE
+  return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: no compiled MFMA kernel for this network shape");
+}
+
+// ------------------------------------------------------------------------------------------
+// Generic (any depth/width) forward, one thread per sample: correctness path for networks the
+// fused kernel is not instantiated for.  Hidden widths <= 256.
+// ------------------------------------------------------------------------------------------
+struct GenArgs {
+  const float *raw;
+  long long w_off[kMaxLayers], b_off[kMaxLayers];
+  int dims[kMaxLayers + 1];
+  int act[kMaxLayers];
+  int nlayers;
+};
+
+__global__ void mlp_generic_kernel(GenArgs g, long long nbatch, const float *__restrict__ x, float *__restrict__ out)
+{
+  long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nbatch) return;
+  float a[256], b[256];
+  int nin = g.dims[0];
+  for (int k = 0; k < nin; k++) a[k] = x[(size_t)s * nin + k];
+  for (int n = 0; n < g.nlayers; n++) {
+    int nout = g.dims[n + 1];
+    const float *W = g.raw + g.w_off[n];
+    const float *B = g.raw + g.b_off[n];
+    bool last = (n == g.nlayers - 1);
+    for (int i = 0; i < nout; i++) {
+      float acc = 0.0f;
+      for (int k = 0; k < nin; k++) acc = fmaf(W[(size_t)k * nout + i], a[k], acc);
+      float v = activate(g.act[n], acc + B[i]);
+      if (last) out[(size_t)s * nout + i] = v;
+      else b[i] = v;
+    }
+    if (!last)
+      for (int i = 0; i < nout; i++) a[i] = b[i];
+    nin = nout;
+  }
+}
+
+int launch_mlp_generic(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch, const float *x,
+                       float *out)
+{
+  if (nbatch <= 0) return RRTMGPNN_OK;
+  GenArgs g{};
+  g.raw = net->d_raw;
+  g.nlayers = net->nlayers;
+  for (int n = 0; n <= net->nlayers; n++) {
+    g.dims[n] = net->dims[n];
+    if (n > 0 && n < net->nlayers && net->dims[n] > 256)
+      return fail(RRTMGPNN_ERR_UNSUPPORTED, "generic mlp: hidden width > 256");
+  }
+  if (net->dims[0] > 256) return fail(RRTMGPNN_ERR_UNSUPPORTED, "generic mlp: input width > 256");
+  for (int n = 0; n < net->nlayers; n++) {
+    g.w_off[n] = (long long)net->raw_w_off[n];
+    g.b_off[n] = (long long)net->raw_b_off[n];
+    g.act[n] = net->act[n];
+  }
+  hipLaunchKernelGGL(mlp_generic_kernel, dim3((unsigned)((nbatch + 127) / 128)), dim3(128), 0, ctx->stream, g, nbatch,
+                     x, out);
+  RRTMGPNN_LAUNCH_CHECK("mlp_generic_kernel");
+  return RRTMGPNN_OK;
+}
+
+}  // namespace rrtmgpnn

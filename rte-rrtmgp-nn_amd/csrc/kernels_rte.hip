@@ -1,0 +1,390 @@
+// kernels_rte.hip -- Planck source and RTE solvers for gfx950 (MI355X).
+//
+// Layout: g-point fastest, exactly the reference's (ngpt, nlay[+1], ncol) arrays.  One block per
+// column, one lane per g-point: every layer step of a wave reads 64 consecutive g-points
+// (256 B, coalesced), and the vertical recurrence runs in registers.  Broadband fluxes are
+// reduced in-kernel (wave shuffle -> per-wave LDS partials -> fixed-order sum: deterministic).
+//
+//  * planck_source_kernel : compute_Planck_source_nn (rrtmgp/kernels/mo_gas_optics_kernels.F90:615-683)
+//  * lw_noscat_kernel     : lw_solver_noscat[_GaussQuad] (rte/kernels/mo_rte_solver_kernels.F90:119-415)
+//  * sw_2stream kernels   : sw_solver_2stream + sw_two_stream_source + adding (:541-692, :1366-1637)
+#include "internal.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+namespace rrtmgpnn {
+
+static constexpr float kPi = 3.14159265358979323846f;
+
+__device__ __forceinline__ float wave_sum(float v)
+{
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Planck source.  grid (nlay, ncol), block >= ngpt.  The block of layer `ilay` owns pfrac(:,ilay)
+// and also writes lev_source(:,nlay+1) (ilay == nlay-1) and the surface sources (ilay == sfc_lay-1)
+// from its in-register pfrac, before pfrac is overwritten with lay_source (no cross-block race).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float interp1d(float val, float offset, float delta, int ntemp, const float *__restrict__ t)
+{
+  float val0 = (val - offset) / delta;
+  int iv = (int)val0;  // Fortran int(): truncation
+  float frac = val0 - (float)iv;
+  int index = min(ntemp - 1, max(1, iv + 1));
+  float lo = t[index - 1], hi = t[index];
+  return lo + frac * (hi - lo);
+}
+
+__device__ __forceinline__ int band_of(const BandArgs &b, int g)
+{
+  for (int i = 0; i < b.nbnd; i++)
+    if (g >= b.lims[2 * i] - 1 && g < b.lims[2 * i + 1]) return i;
+  return 0;
+}
+
+__global__ void planck_source_kernel(int ncol, int nlay, int ngpt, int ntemp, const float *__restrict__ tlay,
+                                     const float *__restrict__ tlev, const float *__restrict__ tsfc, int sfc_lay,
+                                     BandArgs bands, float tmin, float tdelta, const float *__restrict__ totplnk,
+                                     float *__restrict__ sfc_src, float *__restrict__ sfc_jac, float *__restrict__ pfrac,
+                                     float *__restrict__ lev_src)
+{
+  const int ilay = blockIdx.x, icol = blockIdx.y, g = threadIdx.x;
+  if (g >= ngpt) return;
+  const int b = band_of(bands, g);
+  const float *tab = totplnk + (size_t)ntemp * b;
+  const size_t il = (size_t)g + (size_t)ngpt * (ilay + (size_t)nlay * icol);
+  const size_t iv = (size_t)g + (size_t)ngpt * (ilay + (size_t)(nlay + 1) * icol);
+  const float pf = pfrac[il];
+  const float *tl = tlev + (size_t)(nlay + 1) * icol;
+  lev_src[iv] = pf * interp1d(tl[ilay], tmin, tdelta, ntemp, tab);
+  if (ilay == nlay - 1) lev_src[iv + ngpt] = pf * interp1d(tl[nlay], tmin, tdelta, ntemp, tab);
+  if (ilay == sfc_lay - 1) {
+    float ts = tsfc[icol];
+    float ps = interp1d(ts, tmin, tdelta, ntemp, tab);
+    float pj = interp1d(ts + 1.0f, tmin, tdelta, ntemp, tab);
+    sfc_src[g + (size_t)ngpt * icol] = pf * ps;
+    sfc_jac[g + (size_t)ngpt * icol] = pf * (pj - ps);
+  }
+  pfrac[il] = pf * interp1d(tlay[ilay + (size_t)nlay * icol], tmin, tdelta, ntemp, tab);
+}
+
+int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ntemp, const float *tlay,
+                         const float *tlev, const float *tsfc, int sfc_lay, const BandArgs &bands, float temp_ref_min,
+                         float totplnk_delta, const float *totplnk, float *sfc_source, float *sfc_source_Jac,
+                         float *pfrac, float *lev_source)
+{
+  if (ncol == 0 || nlay == 0) return RRTMGPNN_OK;
+  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "planck source: ngpt > 1024");
+  int threads = (ngpt + 63) / 64 * 64;
+  hipLaunchKernelGGL(planck_source_kernel, dim3(nlay, ncol), dim3(threads), 0, ctx->stream, ncol, nlay, ngpt, ntemp,
+                     tlay, tlev, tsfc, sfc_lay, bands, temp_ref_min, totplnk_delta, totplnk, sfc_source,
+                     sfc_source_Jac, pfrac, lev_source);
+  RRTMGPNN_LAUNCH_CHECK("planck_source_kernel");
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// LW no-scattering solver.  block = one column, lane = g-point.  Down pass stores nothing: the up
+// pass re-reads tau/lay/lev for its layer (L2/MALL-hot) and recomputes trans and the source, which
+// are bitwise identical to the down pass' values.  Source indexing follows lw_source_noscat
+// (:742-776): source_dn uses lev(l+1), source_up uses lev(l) for EVERY orientation (quirk B-1).
+// LDS: part[wave][2][nlay+1] per-wave partial sums.
+// ------------------------------------------------------------------------------------------
+struct LwAngles {
+  float D[4], w[4];
+  int nmus;
+};
+
+__global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwAngles ang,
+                                 const float *__restrict__ inc_flux, const float *__restrict__ tau,
+                                 const float *__restrict__ lay, const float *__restrict__ lev,
+                                 const float *__restrict__ emis, const float *__restrict__ sfc,
+                                 float *__restrict__ flux_up, float *__restrict__ flux_dn)
+{
+  extern __shared__ float part[];
+  const int icol = blockIdx.x, g = threadIdx.x, lane = g & 63, wave = g >> 6, nw = blockDim.x >> 6;
+  const bool on = g < ngpt;
+  const int nlev = nlay + 1;
+  const float tau_thresh = sqrtf(FLT_EPSILON);
+  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
+  float *pd = part + (size_t)wave * 2 * nlev, *pu = pd + nlev;
+  for (int l = lane; l < nlev; l += 64) { pd[l] = 0.0f; pu[l] = 0.0f; }
+  const float e = on ? emis[g + (size_t)ngpt * icol] : 0.0f;
+  const float ss = on ? sfc[g + (size_t)ngpt * icol] : 0.0f;
+  const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
+  const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
+
+  for (int imu = 0; imu < ang.nmus; imu++) {
+    const float D = ang.D[imu], fac = 2.0f * kPi * ang.w[imu];
+    float I = inc / (2.0f * kPi * ang.w[imu]);
+    {
+      float s = wave_sum(on ? fac * I : 0.0f);
+      if (lane == 0) pd[top] += s;
+    }
+    // downward: lw_transport_noscat_dn (:982-1009)
+    for (int j = 0; j < nlay; j++) {
+      const int l = top_at_1 ? j : nlay - 1 - j;
+      float Inext = 0.0f;
+      if (on) {
+        const size_t i = (size_t)g + (size_t)ngpt * l;
+        float t = tau[cl + i] * D;
+        float T = expf(-t);
+        float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+        float lvdn = lev[cv + i + ngpt], ly = lay[cl + i];
+        float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
+        Inext = T * I + S;
+      }
+      I = Inext;
+      float s = wave_sum(on ? fac * I : 0.0f);
+      if (lane == 0) pd[top_at_1 ? l + 1 : l] += s;
+    }
+    // surface reflection and emission (:269)
+    float U = I * (1.0f - e) + e * ss;
+    {
+      float s = wave_sum(on ? fac * U : 0.0f);
+      if (lane == 0) pu[sfcl] += s;
+    }
+    // upward: lw_transport_noscat_up (:950-980)
+    for (int j = 0; j < nlay; j++) {
+      const int l = top_at_1 ? nlay - 1 - j : j;
+      float Unext = 0.0f;
+      if (on) {
+        const size_t i = (size_t)g + (size_t)ngpt * l;
+        float t = tau[cl + i] * D;
+        float T = expf(-t);
+        float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+        float lvup = lev[cv + i], ly = lay[cl + i];
+        float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
+        Unext = T * U + S;
+      }
+      U = Unext;
+      float s = wave_sum(on ? fac * U : 0.0f);
+      if (lane == 0) pu[top_at_1 ? l : l + 1] += s;
+    }
+  }
+  __syncthreads();
+  for (int l = g; l < nlev; l += blockDim.x) {
+    float su = 0.0f, sd = 0.0f;
+    for (int w = 0; w < nw; w++) {
+      sd += part[(size_t)w * 2 * nlev + l];
+      su += part[(size_t)w * 2 * nlev + nlev + l];
+    }
+    flux_up[l + (size_t)nlev * icol] = su;
+    flux_dn[l + (size_t)nlev * icol] = sd;
+  }
+}
+
+int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
+                     const float *wts, const float *inc_flux, const float *tau, const float *lay_source,
+                     const float *lev_source, const float *sfc_emis, const float *sfc_source, float *flux_up,
+                     float *flux_dn)
+{
+  if (ncol == 0) return RRTMGPNN_OK;
+  if (nmus < 1 || nmus > 4) return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: nmus must be 1..4");
+  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: ngpt > 1024");
+  LwAngles a{};
+  a.nmus = nmus;
+  for (int i = 0; i < nmus; i++) { a.D[i] = Ds[i]; a.w[i] = wts[i]; }
+  int threads = (ngpt + 63) / 64 * 64;
+  size_t lds = sizeof(float) * (size_t)(threads / 64) * 2 * (nlay + 1);
+  if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many layers for LDS partials");
+  hipLaunchKernelGGL(lw_noscat_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a,
+                     inc_flux, tau, lay_source, lev_source, sfc_emis, sfc_source, flux_up, flux_dn);
+  RRTMGPNN_LAUNCH_CHECK("lw_noscat_kernel");
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// SW two-stream solver.  block = one column, lane = g-point.
+//   pass 1 (top->bottom): direct beam F_dir per level (stored), Sum_g F_dir -> flux_dir
+//   pass 2 (bottom->top): sw_two_stream_source coefficients (Tnoscat recomputed bit-identically
+//          from tau and mu0), adding's albedo/src/denom (Shonk & Hogan Eqs 9-11); stores per level
+//          alpha, src and the downward recurrence coefficients a_l = Tdif*denom,
+//          b_l = (Rdif*src(below) + S_dn)*denom
+//   pass 3 (top->bottom): flux_dn(next) = a*flux_dn + b (Eq 13), flux_up = flux_dn*alpha + src (Eq 12)
+// Workspace ws: 4 arrays (ngpt, nlay+1, ncol): [F_dir -> alpha], src, a, b.
+// ------------------------------------------------------------------------------------------
+struct SwCoef {
+  float Rdif, Tdif, Sup, Sdn, Tnoscat;
+};
+
+__device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, float mu0, float mu0_inv, float dir_inc)
+{
+  const float k_min = 1.e-4f, eps = FLT_EPSILON;
+  SwCoef c;
+  float Tnoscat = expf(-tau * mu0_inv);
+  float gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
+  float gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
+  float gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
+  float gamma4 = 1.0f - gamma3;
+  float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
+  float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
+  float k = sqrtf(fmaxf((gamma1 - gamma2) * (gamma1 + gamma2), k_min));
+  float emk = expf(-tau * k);
+  float em2k = emk * emk;
+  float k2e = 2.0f * k * emk;
+  float RT = 1.0f / (k * (1.0f + em2k) + gamma1 * (1.0f - em2k));
+  c.Rdif = RT * gamma2 * (1.0f - em2k);
+  c.Tdif = RT * 2.0f * k * emk;
+  float k_mu = k * mu0, k_mu2 = k_mu * k_mu, k_g3 = k * gamma3, k_g4 = k * gamma4;
+  float dd = (fabsf(1.0f - k_mu2) >= eps) ? (1.0f - k_mu2) : eps;
+  RT = w0 * RT / dd;
+  float Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
+                     k2e * (gamma3 - alpha2 * mu0) * Tnoscat);
+  float Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
+                     Tnoscat * ((1.0f + k_mu) * (alpha1 + k_g4) - (1.0f - k_mu) * (alpha1 - k_g4) * em2k));
+  Rdir = fmaxf(0.0f, fminf(Rdir, (1.0f - Tnoscat)));
+  Tdir = fmaxf(0.0f, fminf(Tdir, (1.0f - Tnoscat - Rdir)));
+  c.Sup = Rdir * dir_inc;
+  c.Sdn = Tdir * dir_inc;
+  c.Tnoscat = Tnoscat;
+  return c;
+}
+
+__global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, const float *__restrict__ inc_flux,
+                                  const float *__restrict__ inc_dif, const float *__restrict__ tau,
+                                  const float *__restrict__ ssa, const float *__restrict__ gg,
+                                  const float *__restrict__ mu0p, const float *__restrict__ alb_dir,
+                                  const float *__restrict__ alb_dif, float *__restrict__ ws,
+                                  float *__restrict__ flux_up, float *__restrict__ flux_dn, float *__restrict__ flux_dir)
+{
+  extern __shared__ float part[];
+  const int icol = blockIdx.x, g = threadIdx.x, lane = g & 63, wave = g >> 6, nw = blockDim.x >> 6;
+  const bool on = g < ngpt;
+  const int nlev = nlay + 1;
+  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
+  const size_t plane = (size_t)ngpt * nlev * ncol;
+  float *wA = ws + cv, *wS = ws + plane + cv, *wa = ws + 2 * plane + cv, *wb = ws + 3 * plane + cv;
+  float *pu = part + (size_t)wave * 3 * nlev, *pd = pu + nlev, *pr = pd + nlev;
+  const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
+  // level index helpers: "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
+  auto lev_above = [&](int l) { return top_at_1 ? l : l + 1; };
+  auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
+  const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
+
+  // ---- pass 1: direct beam ----
+  float Fd = on ? inc_flux[g + (size_t)ngpt * icol] * mu0 : 0.0f;
+  if (on) wA[(size_t)g + (size_t)ngpt * top] = Fd;
+  {
+    float s = wave_sum(Fd);
+    if (lane == 0) pr[top] = s;
+  }
+  for (int j = 0; j < nlay; j++) {
+    const int l = top_at_1 ? j : nlay - 1 - j;
+    if (on) {
+      float Tn = expf(-tau[cl + (size_t)g + (size_t)ngpt * l] * mu0_inv);
+      Fd = Tn * Fd;
+      wA[(size_t)g + (size_t)ngpt * lev_below(l)] = Fd;
+    }
+    float s = wave_sum(on ? Fd : 0.0f);
+    if (lane == 0) pr[lev_below(l)] = s;
+  }
+  // ---- pass 2: bottom -> top adding (albedo, src) ----
+  float alb_b = on ? alb_dif[g + (size_t)ngpt * icol] : 0.0f;  // albedo at the level below
+  float src_b = on ? Fd * alb_dir[g + (size_t)ngpt * icol] : 0.0f;
+  if (on) {
+    wA[(size_t)g + (size_t)ngpt * sfcl] = alb_b;
+    wS[(size_t)g + (size_t)ngpt * sfcl] = src_b;
+  }
+  for (int j = 0; j < nlay; j++) {
+    const int l = top_at_1 ? nlay - 1 - j : j;
+    if (!on) continue;
+    const size_t i = (size_t)g + (size_t)ngpt * l;
+    const size_t ia = (size_t)g + (size_t)ngpt * lev_above(l);
+    float Fin = wA[ia];
+    SwCoef c = sw_two_stream(tau[cl + i], ssa[cl + i], gg[cl + i], mu0, mu0_inv, Fin);
+    float denom = 1.0f / (1.0f - c.Rdif * alb_b);
+    float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
+    float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+    // coefficients of flux_dn(below) = a * flux_dn(above) + b  (Eq 13)
+    wa[(size_t)g + (size_t)ngpt * l] = c.Tdif * denom;
+    wb[(size_t)g + (size_t)ngpt * l] = (c.Rdif * src_b + c.Sdn) * denom;
+    wA[ia] = alb;
+    wS[ia] = src;
+    alb_b = alb;
+    src_b = src;
+  }
+  // ---- pass 3: top -> bottom fluxes ----
+  float Fdn = (on && inc_dif) ? inc_dif[g + (size_t)ngpt * icol] : 0.0f;
+  {
+    float up = on ? Fdn * alb_b + src_b : 0.0f;  // alb_b/src_b now hold the top level's values
+    float su = wave_sum(up), sd = wave_sum(on ? Fdn : 0.0f);
+    if (lane == 0) { pu[top] = su; pd[top] = sd; }
+  }
+  for (int j = 0; j < nlay; j++) {
+    const int l = top_at_1 ? j : nlay - 1 - j;
+    float up = 0.0f;
+    if (on) {
+      const size_t ib = (size_t)g + (size_t)ngpt * lev_below(l);
+      Fdn = wa[(size_t)g + (size_t)ngpt * l] * Fdn + wb[(size_t)g + (size_t)ngpt * l];
+      up = Fdn * wA[ib] + wS[ib];
+    }
+    float su = wave_sum(up), sd = wave_sum(on ? Fdn : 0.0f);
+    if (lane == 0) { pu[lev_below(l)] = su; pd[lev_below(l)] = sd; }
+  }
+  __syncthreads();
+  for (int l = g; l < nlev; l += blockDim.x) {
+    float su = 0.0f, sd = 0.0f, sr = 0.0f;
+    for (int w = 0; w < nw; w++) {
+      const float *p = part + (size_t)w * 3 * nlev;
+      su += p[l];
+      sd += p[nlev + l];
+      sr += p[2 * nlev + l];
+    }
+    flux_up[l + (size_t)nlev * icol] = su;
+    flux_dn[l + (size_t)nlev * icol] = sd + sr;  // total = diffuse + direct
+    flux_dir[l + (size_t)nlev * icol] = sr;
+  }
+}
+
+int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                      const float *inc_flux_dif, const float *tau, const float *ssa, const float *g, const float *mu0,
+                      const float *alb_dir, const float *alb_dif, float *flux_up, float *flux_dn, float *flux_dir)
+{
+  if (ncol == 0) return RRTMGPNN_OK;
+  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: ngpt > 1024");
+  void *ws = nullptr;
+  int rc = ctx->workspace(sizeof(float) * 4 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
+  if (rc) return rc;
+  int threads = (ngpt + 63) / 64 * 64;
+  size_t lds = sizeof(float) * (size_t)(threads / 64) * 3 * (nlay + 1);
+  if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
+  hipLaunchKernelGGL(sw_2stream_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1,
+                     inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, (float *)ws, flux_up, flux_dn,
+                     flux_dir);
+  RRTMGPNN_LAUNCH_CHECK("sw_2stream_kernel");
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// expand band -> g-point (rte/mo_rte_lw.F90:429-447)
+// ------------------------------------------------------------------------------------------
+__global__ void expand_kernel(int nband, int ngpt, int ncol, BandArgs b, const float *__restrict__ in,
+                              float *__restrict__ out)
+{
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngpt * ncol) return;
+  int g = (int)(i % ngpt), icol = (int)(i / ngpt);
+  int bd = -1;
+  for (int k = 0; k < b.nbnd; k++)
+    if (g >= b.lims[2 * k] - 1 && g < b.lims[2 * k + 1]) { bd = k; break; }
+  if (bd >= 0) out[i] = in[bd + (size_t)nband * icol];
+}
+
+int launch_expand(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const BandArgs &bands, const float *in,
+                  float *out)
+{
+  long long n = (long long)ngpt * ncol;
+  if (n == 0) return RRTMGPNN_OK;
+  hipLaunchKernelGGL(expand_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, nband, ngpt, ncol,
+                     bands, in, out);
+  RRTMGPNN_LAUNCH_CHECK("expand_kernel");
+  return RRTMGPNN_OK;
+}
+
+}  // namespace rrtmgpnn

@@ -1,0 +1,90 @@
+"""ctypes binding of librrtmgpnn.so (the C ABI declared in include/rrtmgpnn.h).
+
+The shared library is built in-tree (rte-rrtmgp-nn_amd/librrtmgpnn.so, `make -C rte-rrtmgp-nn_amd`).
+There is deliberately NO fallback: if the HIP library cannot be loaded the product path
+raises, so a test can never pass on a silent CPU implementation.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "librrtmgpnn.so"))
+
+c_int, c_float, c_ll, c_vp, c_char_p = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_char_p
+P = ctypes.POINTER
+
+# name -> (restype, argtypes); mirrors include/rrtmgpnn.h one-to-one.
+SIGNATURES = {
+    "rrtmgpnn_version": (c_int, []),
+    "rrtmgpnn_last_error": (c_char_p, []),
+    "rrtmgpnn_context_create": (c_int, [c_int, c_vp, P(c_vp)]),
+    "rrtmgpnn_context_destroy": (c_int, [c_vp]),
+    "rrtmgpnn_context_set_stream": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_context_stream": (c_vp, [c_vp]),
+    "rrtmgpnn_context_synchronize": (c_int, [c_vp]),
+    "rrtmgpnn_malloc": (c_int, [c_vp, c_ll, P(c_vp)]),
+    "rrtmgpnn_free": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_memcpy_h2d": (c_int, [c_vp, c_vp, c_vp, c_ll]),
+    "rrtmgpnn_memcpy_d2h": (c_int, [c_vp, c_vp, c_vp, c_ll]),
+    "rrtmgpnn_network_load": (c_int, [c_vp, c_char_p, P(c_vp)]),
+    "rrtmgpnn_network_create": (c_int, [c_vp, c_int, P(c_int), P(c_int), P(c_vp), P(c_vp), c_vp, c_vp, c_vp, c_vp,
+                                        c_char_p, P(c_vp)]),
+    "rrtmgpnn_network_destroy": (c_int, [c_vp]),
+    "rrtmgpnn_network_get_dims": (c_int, [c_vp, P(c_int), P(c_int)]),
+    "rrtmgpnn_network_get_input_name": (c_int, [c_vp, c_int, c_char_p, c_int]),
+    "rrtmgpnn_network_get_input_scaling": (c_int, [c_vp, c_vp, c_vp]),
+    "rrtmgpnn_compute_nn_inputs": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, P(c_vp), P(c_int), c_vp, c_vp]),
+    "rrtmgpnn_get_col_dry": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_interpolate_tlev": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_predict_nn_lw": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, P(c_vp), c_int, c_vp, c_vp]),
+    "rrtmgpnn_predict_nn_sw": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, P(c_vp), c_vp, c_vp, c_vp]),
+    "rrtmgpnn_network_forward": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),
+    "rrtmgpnn_compute_planck_source_nn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                                  P(c_int), c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_lw_solver_noscat": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float), P(c_float), c_vp, c_vp,
+                                          c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_sw_solver_2stream": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_expand_band_to_gpt": (c_int, [c_vp, c_int, c_int, c_int, P(c_int), c_vp, c_vp]),
+}
+
+
+class RrtmgpnnError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the HIP library is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RrtmgpnnError("librrtmgpnn.so not found at %s: build it with `make -C rte-rrtmgp-nn_amd` "
+                                "(no CPU fallback exists by design)" % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(h, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().rrtmgpnn_last_error().decode(errors="replace")
+        raise RrtmgpnnError("%s failed (code %d): %s" % (what or "rrtmgpnn call", rc, msg))
+
+
+def int_array(vals):
+    return (c_int * len(vals))(*[int(v) for v in vals])
+
+
+def float_array(vals):
+    return (c_float * len(vals))(*[float(v) for v in vals])
+
+
+def ptr_array(ptrs):
+    return (c_vp * len(ptrs))(*[p if p else None for p in ptrs])

@@ -1,0 +1,181 @@
+"""Model files, surrogate k-distribution tables and problem generators (host side, numpy).
+
+Arrays are returned in C order with the REVERSED Fortran shape, i.e. the same memory as the
+reference's column-major arrays:  Fortran p_lay(nlay, ncol) <-> numpy (ncol, nlay).
+
+`rfmip_problem()` reproduces the RFMIP clear-sky drivers' pre-processing
+(examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:265-305,385-390 and rrtmgp_rfmip_sw.F90:273-287,
+317, 408-434) for a single block of all 1800 columns (100 sites x 18 experiments,
+column = site + 100*expt as read_and_block_* reshape them, mo_rfmip_io.F90:74-680).
+`synthetic_problem()` builds the larger synthetic configurations (C4, C5 of BASELINE.json).
+"""
+import os
+
+import numpy as np
+
+from . import rbin
+
+DATA_DIR = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "data"))
+
+MODEL_FILES = {
+    "lw_abs": "nn_lw_g256_abs.rbin",
+    "lw_pfrac": "nn_lw_g256_pfrac.rbin",
+    "sw_abs": "nn_sw_g224_abs.rbin",
+    "sw_ray": "nn_sw_g224_ray.rbin",
+    "lw_g128_both": "nn_lw_g128_both.rbin",
+}
+
+F32_EPS = np.float32(np.finfo(np.float32).eps)
+
+
+def path(name):
+    return os.path.join(DATA_DIR, MODEL_FILES.get(name, name))
+
+
+def load_model(name):
+    return rbin.read(path(name))
+
+
+def load_kdist(which):
+    """Surrogate k-distribution tables ('lw' -> g256, 'sw' -> g224); see tools/convert_reference_data.py."""
+    d = rbin.read(os.path.join(DATA_DIR, "kdist_lw_g256.rbin" if which == "lw" else "kdist_sw_g224.rbin"))
+    out = {k: v for k, v in d.items()}
+    out["nband"] = int(d["band_lims_gpt"].shape[0])
+    out["ngpt"] = int(d["band_lims_gpt"][-1, 1])
+    if which == "lw":
+        out["nPlanckTemp"] = int(d["totplnk"].shape[1])
+        tmin, tmax = np.float32(d["temp_ref_min"][0]), np.float32(d["temp_ref_max"][0])
+        # totplnk_delta = (temp_ref_max - temp_ref_min) / (nPlanckTemp - 1)  (mo_gas_optics_rrtmgp.F90:1218)
+        out["totplnk_delta"] = np.float32((tmax - tmin) / np.float32(out["nPlanckTemp"] - 1))
+    return out
+
+
+def spacing(x):
+    x = np.float32(x)
+    return np.float32(np.nextafter(x, np.float32(np.inf)) - x)
+
+
+def set_tsi(solar_source, tsi):
+    """ty_gas_optics_rrtmgp%set_tsi (rrtmgp/mo_gas_optics_rrtmgp.F90:1097-1120), float32."""
+    s = np.asarray(solar_source, np.float32)
+    norm = np.float32(1.0) / np.float32(s.sum(dtype=np.float32))
+    return (s * np.float32(tsi) * norm).astype(np.float32)
+
+
+LW_GAS_ORDER = ["h2o", "o3", "co2", "n2o", "ch4", "cfc11", "cfc12", "co", "ccl4", "cfc22", "hfc143a",
+                "hfc125", "hfc23", "hfc32", "hfc134a", "cf4", "o2", "n2"]
+
+
+def rfmip_problem(lw_press_clamp=True):
+    """All 1800 RFMIP clear-sky columns (nlay = 60, top at index 1).
+
+    Returns dict with play (ncol,nlay), plev (ncol,nlay+1), tlay, tlev, tsfc (ncol), gases
+    {name: (ncol,nlay)}, sfc_emis (ncol), sfc_alb (ncol), sza, tsi, mu0, usecol, top_at_1.
+    """
+    d = rbin.read(os.path.join(DATA_DIR, "rfmip_clear_sky.rbin"))
+    nexp, nsite, nlay = d["temp_layer"].shape
+    ncol = nsite * nexp
+    site = np.tile(np.arange(nsite), nexp)
+    expt = np.repeat(np.arange(nexp), nsite)
+    kd = load_kdist("lw")
+    pmin = np.float32(kd["press_ref_min"][0])
+    play = d["pres_layer"][site].astype(np.float32)
+    plev = d["pres_level"][site].astype(np.float32)
+    top_at_1 = bool(play[0, 0] < play[0, nlay - 1])
+    if lw_press_clamp:  # rrtmgp_rfmip_lw.F90:287  where(p_lay < press_min) p_lay = press_min + spacing(press_min)
+        play = np.where(play < pmin, pmin + spacing(pmin), play).astype(np.float32)
+    # rrtmgp_rfmip_lw.F90:300-305 / rrtmgp_rfmip_sw.F90:273-278
+    if top_at_1:
+        plev[:, 0] = pmin + F32_EPS
+    else:
+        plev[:, nlay] = pmin + F32_EPS
+    gases = {"h2o": d["h2o"][expt, site].astype(np.float32), "o3": d["o3"][expt, site].astype(np.float32)}
+    for g in LW_GAS_ORDER[2:]:
+        gases[g] = np.repeat(d["gm_" + g][expt][:, None], nlay, axis=1).astype(np.float32)
+    sza = d["solar_zenith_angle"][site].astype(np.float32)
+    # rrtmgp_rfmip_sw.F90:285-287, 432-434
+    usecol = sza < np.float32(90.0) - np.float32(2.0) * spacing(90.0)
+    deg_to_rad = np.float32(np.arccos(np.float32(-1.0)) / np.float32(180.0))
+    mu0 = np.where(usecol, np.cos(sza * deg_to_rad, dtype=np.float32), np.float32(1.0)).astype(np.float32)
+    return {
+        "ncol": ncol, "nlay": nlay, "top_at_1": top_at_1,
+        "play": np.ascontiguousarray(play), "plev": np.ascontiguousarray(plev),
+        "tlay": d["temp_layer"][expt, site].astype(np.float32),
+        "tlev": d["temp_level"][expt, site].astype(np.float32),
+        "tsfc": d["surface_temperature"][expt, site].astype(np.float32),
+        "gases": gases,
+        "sfc_emis": d["surface_emissivity"][site].astype(np.float32),
+        "sfc_alb": d["surface_albedo"][site].astype(np.float32),
+        "sza": sza, "mu0": mu0, "usecol": usecol,
+        "tsi": d["total_solar_irradiance"][site].astype(np.float32),
+    }
+
+
+def synthetic_problem(ncol, nlay=60, seed=20251015, t_sigma=2.0, h2o_sigma=0.2):
+    """Synthetic clear-sky columns built from RFMIP profiles (BASELINE configs C4/C5).
+
+    Each column takes an RFMIP (site, expt) drawn by PCG64(seed); for nlay != 60 the profile is
+    interpolated linearly in ln(p) onto nlay layers between the surface and press_ref_min.
+    T += N(0, t_sigma K) clipped to the NN training range [160, 320.5] K; h2o *= lognormal(0, h2o_sigma)
+    clipped to the NN range [xmin^4, xmax^4].
+    """
+    base = rfmip_problem()
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pick = rng.integers(0, base["ncol"], size=ncol)
+    kd = load_kdist("lw")
+    pmin = np.float32(kd["press_ref_min"][0])
+    nl0 = base["nlay"]
+    if nlay == nl0:
+        play = base["play"][pick].copy()
+        plev = base["plev"][pick].copy()
+        tlay = base["tlay"][pick].copy()
+        tlev = base["tlev"][pick].copy()
+        gases = {k: v[pick].copy() for k, v in base["gases"].items()}
+    else:
+        # new level grid: log-spaced from surface pressure to press_ref_min (top at index 0)
+        psfc = base["plev"][pick, nl0].astype(np.float64)
+        frac = np.linspace(0.0, 1.0, nlay + 1)[None, :]
+        lev = np.exp(np.log(psfc)[:, None] * frac + np.log(np.float64(pmin) * 1.0001) * (1.0 - frac))
+        lay = np.sqrt(lev[:, :-1] * lev[:, 1:])
+        src_lay = np.log(base["play"][pick].astype(np.float64))
+        src_lev = np.log(base["plev"][pick].astype(np.float64))
+        src_lev[:, 0] = np.log(np.float64(pmin))
+
+        def interp(src_lnp, vals, dst_lnp):
+            out = np.empty(dst_lnp.shape)
+            for i in range(dst_lnp.shape[0]):
+                out[i] = np.interp(dst_lnp[i], src_lnp[i], vals[i])
+            return out
+
+        lnl, lnv = np.log(lay), np.log(lev)
+        tlay = interp(src_lay, base["tlay"][pick], lnl)
+        tlev = interp(src_lev, base["tlev"][pick], lnv)
+        gases = {k: interp(src_lay, v[pick], lnl) for k, v in base["gases"].items()}
+        play, plev = lay, lev
+        plev[:, 0] = pmin + F32_EPS
+    tlay = np.clip(tlay + rng.normal(0.0, t_sigma, size=tlay.shape), 160.0, 320.5)
+    tlev = np.clip(tlev + rng.normal(0.0, t_sigma, size=tlev.shape), 160.0, 320.5)
+    h2o_lo, h2o_hi = 0.0101 ** 4, 0.5077 ** 4
+    gases["h2o"] = np.clip(gases["h2o"] * rng.lognormal(0.0, h2o_sigma, size=gases["h2o"].shape), h2o_lo, h2o_hi)
+    out = {
+        "ncol": ncol, "nlay": nlay, "top_at_1": True,
+        "play": np.ascontiguousarray(play, np.float32), "plev": np.ascontiguousarray(plev, np.float32),
+        "tlay": np.ascontiguousarray(tlay, np.float32), "tlev": np.ascontiguousarray(tlev, np.float32),
+        "tsfc": np.clip(base["tsfc"][pick] + rng.normal(0.0, t_sigma, size=ncol), 160.0, 340.0).astype(np.float32),
+        "gases": {k: np.ascontiguousarray(v, np.float32) for k, v in gases.items()},
+        "sfc_emis": base["sfc_emis"][pick].copy(), "sfc_alb": base["sfc_alb"][pick].copy(),
+        "sza": base["sza"][pick].copy(), "mu0": base["mu0"][pick].copy(), "usecol": base["usecol"][pick].copy(),
+        "tsi": base["tsi"][pick].copy(),
+    }
+    return out
+
+
+def toa_flux(problem, kd_sw, tsi_default=1361.0):
+    """SW incident flux per (col, gpt): gas_optics_ext's toa_src = solar_source after set_tsi(1361)
+    (rrtmgp_rfmip_sw.F90:317; mo_gas_optics_rrtmgp.F90:594-599), renormalised per column to the
+    RFMIP TSI (rrtmgp_rfmip_sw.F90:408-427).  Returns (ncol, ngpt) float32."""
+    sol = set_tsi(kd_sw["solar_source"], tsi_default)
+    ncol = problem["ncol"]
+    toa = np.broadcast_to(sol, (ncol, sol.size)).astype(np.float32)
+    def_tsi = toa.sum(axis=1, dtype=np.float32)
+    return (toa * (problem["tsi"] / def_tsi)[:, None]).astype(np.float32)
