@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""bench.py -- clear-sky LW+SW fluxes (RTE+RRTMGP-NN hot path) on 1..N MI355X.
+
+Metric (BASELINE.json): atmospheric columns/s for LW+SW clear-sky fluxes.  Workload at N=1:
+configs[2] "RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics both streams"
+(the real RFMIP inputs shipped with the reference + the reference's NN weights).  A step is
+gas_optics(LW, NN) + rte_lw + gas_optics(SW, NN) + rte_sw over the block, inputs resident in HBM.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+GPU, each processing its own 1800-column block (weak scaling: columns are independent, no
+collective in the data path); barrier + synchronize around the timed region, max over ranks.
+After timing, the broadband fluxes are all-gathered once over RCCL (the final flux reduction the
+north star names), timed separately ("gather_ms"), outside `value`.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rte-rrtmgp-nn_amd"))
+
+METRIC = "atmospheric columns/sec (LW+SW clear-sky fluxes), 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: FP32 matrix 157.3 TFLOP/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
+                    help="c3: RFMIP 1800x60 (default, the metric's config); c4: 10000x60 synthetic clear-sky; "
+                         "c5: 125000x137 synthetic per GPU")
+    ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+# Algorithmic work per unit.  FLOPs count 2*n_in*n_out per sample and layer.
+def mlp_flops(dims):
+    return 2 * sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+
+
+def stage_work(name, step):
+    """(kind, amount per launch): 'flop' for MFMA stages, 'byte' for HBM stages (algorithmic)."""
+    ncol, nlay = step.ncol, step.nlay
+    N = ncol * nlay
+    glw, gsw = step.ng_lw, step.ng_sw
+    f4 = 4
+    if name == "predict_nn_lw":
+        from rrtmgpnn import data
+        fl = sum(mlp_flops([int(v) for v in data.load_model(m)["dims"]]) for m in ("lw_abs", "lw_pfrac"))
+        return "flop", fl * N, "bytes", N * (step.nx_lw + 1 + 2 * glw) * f4
+    if name == "predict_nn_sw":
+        from rrtmgpnn import data
+        fl = sum(mlp_flops([int(v) for v in data.load_model(m)["dims"]]) for m in ("sw_abs", "sw_ray"))
+        return "flop", fl * N, "bytes", N * (step.nx_sw + 1 + 3 * gsw) * f4
+    if name == "lw_solver":
+        # tau, lay (G x L) + lev (G x (L+1)) + emis, sfc (G) read; flux up/dn (L+1) written
+        return "byte", ncol * ((2 * glw * nlay + glw * (nlay + 1) + 2 * glw) * f4 + 2 * (nlay + 1) * f4), None, None
+    if name == "sw_solver":
+        # tau, ssa, g (G x L) + toa, alb_dir, alb_dif (G) + mu0 read; up/dn/dir written
+        return "byte", ncol * ((3 * gsw * nlay + 3 * gsw + 1) * f4 + 3 * (nlay + 1) * f4), None, None
+    if name == "planck_source":
+        # pfrac read, lay (in place) + lev + sfc + sfcJac written
+        return "byte", ncol * ((glw * nlay + glw * nlay + glw * (nlay + 1) + 2 * glw) * f4), None, None
+    return "byte", 0, None, None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
+                                device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from rrtmgpnn import data
+    from rrtmgpnn.pipeline import ClearSkyStep
+
+    if args.config == "c3":
+        prob = data.rfmip_problem()
+        workload = "C3: RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics (g256 LW + g224 SW)"
+        data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
+    elif args.config == "c4":
+        prob = data.synthetic_problem(10000, 60, seed=20251015 + rank)
+        workload = "C4-shaped clear-sky: 10000 synthetic columns x 60 layers (clouds not yet included)"
+        data_desc = "synthetic columns drawn from RFMIP profiles (PCG64 seed 20251015+rank)"
+    else:
+        prob = data.synthetic_problem(125000, 137, seed=20251015 + rank)
+        workload = "C5 shard: 125000 synthetic columns x 137 layers per GPU, clear-sky LW+SW"
+        data_desc = "synthetic columns interpolated from RFMIP profiles (PCG64 seed 20251015+rank)"
+    step = ClearSkyStep(prob, device=local)
+    ncol, nlay = step.ncol, step.nlay
+
+    use_graph = not args.no_graph
+    run = step.step
+    if use_graph:
+        step.capture()
+        run = step.replay
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_cols = ncol * world * args.steps
+    value = total_cols / elapsed
+
+    # ---- per-stage kernel times, HIP events on the context's stream (eager launches) ----
+    stages = {}
+    s = step.ctx.stream
+    reps = max(3, min(20, args.steps))
+    for name, fn, cargs in step.calls:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s):
+            fn(*cargs)  # warm
+            ev0.record(s)
+            for _ in range(reps):
+                fn(*cargs)
+            ev1.record(s)
+        ev1.synchronize()
+        stages[name] = ev0.elapsed_time(ev1) / reps  # ms per launch
+    # dominant kernel and its roofline
+    best = None
+    for name, ms in stages.items():
+        kind, amount, _, _ = stage_work(name, step)
+        if amount <= 0:
+            continue
+        if best is None or ms > stages[best[0]]:
+            best = (name, kind, amount)
+    roof = None
+    stage_roofs = {}
+    for name, ms in stages.items():
+        kind, amount, k2, a2 = stage_work(name, step)
+        if amount <= 0:
+            continue
+        if kind == "flop":
+            ach = amount / (ms * 1e-3) / 1e12
+            stage_roofs[name] = {"bound": "mfma", "achieved_tflops": round(ach, 2),
+                                 "frac": round(ach / FP32_MFMA_PEAK_TFS, 4),
+                                 "algorithmic_gbs": round(a2 / (ms * 1e-3) / 1e9, 1)}
+        else:
+            ach = amount / (ms * 1e-3) / 1e9
+            stage_roofs[name] = {"bound": "hbm", "achieved_gbs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)}
+    if best is not None:
+        name, kind, amount = best
+        ms = stages[name]
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            tk = tj.get(args.config, {}).get(name)
+            if tk is not None:
+                traffic = tk
+        except (OSError, ValueError):
+            pass
+        if kind == "flop":
+            ach = amount / (ms * 1e-3) / 1e12
+            roof = {"kernel": name, "bound": "mfma", "achieved": round(ach, 3), "peak": FP32_MFMA_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFS, 4), "traffic": traffic,
+                    "algorithmic_per_launch": amount, "avg_launch_ms": round(ms, 4)}
+        else:
+            ach = amount / (ms * 1e-3) / 1e9
+            roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_per_launch": amount,
+                    "avg_launch_ms": round(ms, 4)}
+
+    # ---- final flux all-gather over RCCL (outside the timed region) ----
+    gather_ms = None
+    if world > 1:
+        flat = torch.cat([step.lw_up.reshape(-1), step.lw_dn.reshape(-1), step.sw_up.reshape(-1),
+                          step.sw_dn.reshape(-1), step.sw_dir.reshape(-1)])
+        outs = [torch.empty_like(flat) for _ in range(world)]
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        dist.all_gather(outs, flat)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+
+    # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(prob, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "columns/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": data_desc,
+            "config": {"workload": workload, "ncol_per_gpu": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
+                       "ngpt_sw": step.ng_sw, "parallelism": "column-sharded, 1 process per GPU",
+                       "launch": "hipGraph replay" if use_graph else "eager"},
+            "column_layers_per_s": round(value * nlay, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "stage_roofline": stage_roofs,
+            "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(prob, target_s):
+    """Time the oracle (C restatement; its solvers and MLP are bit-identical to the reference Fortran+MKL
+    compiled here, see tests/test_oracle_reference.py) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    try:
+        import oracle as O
+        orc = O.Oracle()
+    except Exception as e:  # oracle library not built
+        return {"value": None, "unit": "columns/s", "cores": 0, "kind": "port", "sample": "unavailable: %s" % e}
+    from rrtmgpnn import data
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    orc.set_threads(threads)
+    models_lw = [data.load_model("lw_abs"), data.load_model("lw_pfrac")]
+    models_sw = [data.load_model("sw_abs"), data.load_model("sw_ray")]
+    kd, kds = data.load_kdist("lw"), data.load_kdist("sw")
+
+    def subset(n):
+        idx = np.arange(n) % prob["ncol"]
+        sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == prob["ncol"] else v)
+               for k, v in prob.items()}
+        sub["gases"] = {k: v[idx] for k, v in prob["gases"].items()}
+        sub["ncol"] = n
+        return sub
+
+    n = 64
+    while True:
+        sub = subset(n)
+        t0 = time.perf_counter()
+        orc.clear_sky_lw(sub, models_lw, kd)
+        orc.clear_sky_sw(sub, models_sw, kds)
+        dt = time.perf_counter() - t0
+        if dt * 4 > target_s or n >= prob["ncol"] * 4:
+            break
+        n = int(min(n * max(2.0, min(8.0, target_s / max(dt, 1e-3) / 2)), prob["ncol"] * 4))
+    return {"value": round(n / dt, 1), "unit": "columns/s", "cores": threads, "kind": "port",
+            "sample": "%d columns of the same workload (LW+SW gas optics + RTE), %.1f s, OpenMP over columns" % (n, dt)}
+
+
+if __name__ == "__main__":
+    main()

@@ -438,7 +438,13 @@ static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
   auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE>;
   size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
-  RRTMGPNN_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  // Raise the dynamic-LDS limit once per instantiation (kept out of the per-call path so the launch
+  // sequence is capturable into a hipGraph).
+  static size_t lds_set = 0;
+  if (lds > lds_set) {
+    RRTMGPNN_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    lds_set = 160 * 1024;
+  }
   long long ntiles = (a.nbatch + 15) / 16;
   const int wpb = kMlpThreads / 64;
   int per_cu = std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1)));

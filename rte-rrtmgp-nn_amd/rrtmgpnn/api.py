@@ -1,0 +1,495 @@
+"""Host-side mirror of the reference's class layer, on torch device tensors, over the C ABI.
+
+Names, argument meaning and error behaviour follow the reference:
+  rrtmgp_network_type            neural/mod_network_rrtmgp.F90:34-122       -> RrtmgpNetwork
+  ty_gas_concs                   rrtmgp/mo_gas_concentrations.F90:50-444    -> GasConcs
+  ty_optical_props_1scl/2str     rte/mo_optical_props.F90:62-210           -> OpticalProps1scl/2str
+  ty_source_func_lw              rte/mo_source_functions.F90:26-136        -> SourceFuncLW
+  ty_fluxes_broadband            rte/mo_fluxes.F90:46-67                   -> FluxesBroadband
+  ty_gas_optics_rrtmgp%gas_optics  rrtmgp/mo_gas_optics_rrtmgp.F90:239-602 -> GasOpticsRRTMGP.gas_optics
+  rte_lw                         rte/mo_rte_lw.F90:60-424                  -> rte_lw
+  rte_sw                         rte/mo_rte_sw.F90:48-266                  -> rte_sw
+Class-level functions RETURN an error message ('' on success), never raise for user errors, like the
+reference's `character(len=128) error_msg`; `stop_on_err` turns one into an exception.
+
+Layout: torch tensors in C order with the Fortran shape reversed (reference tau(ngpt,nlay,ncol) is
+tensor (ncol, nlay, ngpt) here): the bytes are identical, so the kernels see the reference layout.
+All compute runs in HIP kernels of librrtmgpnn.so; there is no torch/CPU compute path.
+"""
+import numpy as np
+import torch
+
+from . import _lib, data, rbin
+from ._lib import check, float_array, int_array, ptr_array
+
+_CTX = {}
+
+
+class Context:
+    """A rrtmgpnn_context bound to a device and a HIP stream (default: torch's current stream)."""
+
+    def __init__(self, device=0, stream=None):
+        L = _lib.lib()
+        self.device = int(device)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.stream = s
+        h = _lib.c_vp()
+        check(L.rrtmgpnn_context_create(self.device, s.cuda_stream, h), "context_create")
+        self.h = h
+
+    def use_stream(self, stream):
+        check(_lib.lib().rrtmgpnn_context_set_stream(self.h, stream.cuda_stream), "context_set_stream")
+        self.stream = stream
+
+    def synchronize(self):
+        check(_lib.lib().rrtmgpnn_context_synchronize(self.h), "context_synchronize")
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                _lib.lib().rrtmgpnn_context_destroy(self.h)
+        except Exception:
+            pass
+
+
+def context(device=None):
+    """Per-device default context on torch's current stream."""
+    if device is None:
+        device = torch.cuda.current_device()
+    dev = int(device)
+    c = _CTX.get(dev)
+    cur = torch.cuda.current_stream(dev)
+    if c is None:
+        c = _CTX[dev] = Context(dev, cur)
+    elif c.stream.cuda_stream != cur.cuda_stream:
+        c.use_stream(cur)
+    return c
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _f32dev(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=torch.float32).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(x, dtype=np.float32), device=device)
+
+
+def stop_on_err(msg):
+    if msg:
+        raise RuntimeError(msg)
+
+
+# ---------------------------------------------------------------------------------------------
+class RrtmgpNetwork:
+    """rrtmgp_network_type: an MLP plus its input/output scaling (neural/mod_network_rrtmgp.F90:34-53)."""
+
+    def __init__(self, device=None):
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.h = None
+
+    def load_netcdf(self, filename):
+        """Reference name kept (mod_network_rrtmgp.F90:58); reads the RBIN conversion of the netCDF model."""
+        m = rbin.read(filename)
+        self.dims = [int(v) for v in m["dims"]]
+        self.activation = [int(v) for v in m["activation"]]
+        self.input_names = rbin.unchars(m["input_names"]) if "input_names" in m else [""] * self.dims[0]
+        self.coeffs_input_min = m["input_min"]
+        self.coeffs_input_max = m["input_max"]
+        self.coeffs_output_mean = m.get("output_mean")
+        self.coeffs_output_std = m.get("output_std")
+        self.model = m
+        ctx = context(self.device)
+        h = _lib.c_vp()
+        check(_lib.lib().rrtmgpnn_network_load(ctx.h, filename.encode(), h), "network_load(%s)" % filename)
+        self.h = h
+        return self
+
+    load = load_netcdf
+
+    @property
+    def nlayers(self):
+        return len(self.dims) - 1
+
+    def output_sgemm_flat(self, x):
+        """network_type%output_sgemm_flat (neural/mod_network.F90:273): x (nbatch, nx) -> (nbatch, ny)."""
+        x = _f32dev(x, "cuda:%d" % self.device)
+        nb = x.numel() // self.dims[0]
+        out = torch.empty((nb, self.dims[-1]), dtype=torch.float32, device=x.device)
+        check(_lib.lib().rrtmgpnn_network_forward(context(self.device).h, self.h, nb, _p(x), _p(out)), "network_forward")
+        return out
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.lib().rrtmgpnn_network_destroy(self.h)
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------------------------------------
+class GasConcs:
+    """ty_gas_concs: per-gas scalar / (nlay) / (ncol,nlay) volume mixing ratios (device tensors)."""
+
+    def init(self, gas_names):
+        self.gas_name = [g.strip().lower() for g in gas_names]
+        if len(set(self.gas_name)) != len(self.gas_name):
+            return "ty_gas_concs%init(): duplicate gas names"
+        self.concs = {}
+        return ""
+
+    def set_vmr(self, gas, w, device=None):
+        gas = gas.strip().lower()
+        if gas not in self.gas_name:
+            return "ty_gas_concs%set_vmr(): trying to set " + gas + " but name not present"
+        if isinstance(w, (float, int, np.floating)):
+            if w < 0 or w > 1:
+                return "ty_gas_concs%set_vmr(): concentrations should be >= 0, <= 1"
+            self.concs[gas] = torch.tensor([float(w)], dtype=torch.float32,
+                                           device=device or "cuda:%d" % torch.cuda.current_device())
+            return ""
+        t = _f32dev(w, device or "cuda:%d" % torch.cuda.current_device())
+        if t.numel() and (bool((t < 0).any()) or bool((t > 1).any())):
+            return "ty_gas_concs%set_vmr(): concentrations should be >= 0, <= 1"
+        self.concs[gas] = t
+        return ""
+
+    def get_gas_names(self):
+        return list(self.gas_name)
+
+    def ndims(self, gas):
+        t = self.concs[gas]
+        return 0 if t.numel() == 1 and t.dim() <= 1 else t.dim()
+
+
+# ---------------------------------------------------------------------------------------------
+class OpticalProps:
+    """ty_optical_props: spectral discretisation (band limits in wavenumber and g-point)."""
+
+    def init(self, band_lims_wvn, band_lims_gpt=None, name=""):
+        wv = np.asarray(band_lims_wvn, np.float32).reshape(-1, 2)
+        if band_lims_gpt is None:
+            band_lims_gpt = np.stack([np.arange(1, wv.shape[0] + 1)] * 2, axis=1)
+        gp = np.asarray(band_lims_gpt, np.int32).reshape(-1, 2)
+        if (wv < 0).any():
+            return "optical_props%init(): band_lims_wvn has values <  0., respectively"
+        if gp.min() < 1:
+            return "optical_props%init(): band_lims_gpt has values < 1"
+        self.band_lims_wvn, self.band_lims_gpt, self.name = wv, gp, name
+        return ""
+
+    def init_from(self, other):
+        return self.init(other.band_lims_wvn, other.band_lims_gpt, getattr(other, "name", ""))
+
+    def get_nband(self):
+        return int(self.band_lims_gpt.shape[0])
+
+    def get_ngpt(self):
+        return int(self.band_lims_gpt[:, 1].max())
+
+    def get_band_lims_gpoint(self):
+        return self.band_lims_gpt.copy()
+
+    def get_band_lims_wavenumber(self):
+        return self.band_lims_wvn.copy()
+
+    def get_gpoint_bands(self):
+        b = np.zeros(self.get_ngpt(), np.int32)
+        for i, (lo, hi) in enumerate(self.band_lims_gpt):
+            b[lo - 1:hi] = i + 1
+        return b
+
+
+class _OpticalPropsArry(OpticalProps):
+    def get_ncol(self):
+        return int(self.tau.shape[0])
+
+    def get_nlay(self):
+        return int(self.tau.shape[1])
+
+
+class OpticalProps1scl(_OpticalPropsArry):
+    def alloc_1scl(self, ncol, nlay, spec=None, device=None):
+        if spec is not None:
+            e = self.init_from(spec)
+            if e:
+                return e
+        if ncol <= 0 or nlay <= 0:
+            return "optical_props%alloc: must provide positive extents for ncol, nlay"
+        dev = device or "cuda:%d" % torch.cuda.current_device()
+        self.tau = torch.zeros((ncol, nlay, self.get_ngpt()), dtype=torch.float32, device=dev)
+        return ""
+
+
+class OpticalProps2str(_OpticalPropsArry):
+    def alloc_2str(self, ncol, nlay, spec=None, device=None):
+        if spec is not None:
+            e = self.init_from(spec)
+            if e:
+                return e
+        if ncol <= 0 or nlay <= 0:
+            return "optical_props%alloc: must provide positive extents for ncol, nlay"
+        dev = device or "cuda:%d" % torch.cuda.current_device()
+        shape = (ncol, nlay, self.get_ngpt())
+        self.tau = torch.zeros(shape, dtype=torch.float32, device=dev)
+        self.ssa = torch.zeros(shape, dtype=torch.float32, device=dev)
+        self.g = torch.zeros(shape, dtype=torch.float32, device=dev)
+        return ""
+
+
+class SourceFuncLW(OpticalProps):
+    def alloc(self, ncol, nlay, spec=None, device=None):
+        if spec is not None:
+            e = self.init_from(spec)
+            if e:
+                return e
+        if ncol <= 0 or nlay <= 0:
+            return "source_func_lw%alloc: must provide positive extents for ncol, nlay"
+        dev = device or "cuda:%d" % torch.cuda.current_device()
+        ng = self.get_ngpt()
+        self.lay_source = torch.zeros((ncol, nlay, ng), dtype=torch.float32, device=dev)
+        self.lev_source = torch.zeros((ncol, nlay + 1, ng), dtype=torch.float32, device=dev)
+        self.sfc_source = torch.zeros((ncol, ng), dtype=torch.float32, device=dev)
+        self.sfc_source_Jac = torch.zeros((ncol, ng), dtype=torch.float32, device=dev)
+        return ""
+
+    def get_ncol(self):
+        return int(self.lay_source.shape[0])
+
+    def get_nlay(self):
+        return int(self.lay_source.shape[1])
+
+
+class FluxesBroadband:
+    """ty_fluxes_broadband: (ncol, nlay+1) outputs the caller allocates (pointers into caller memory)."""
+
+    def __init__(self, flux_up=None, flux_dn=None, flux_dn_dir=None, flux_net=None):
+        self.flux_up, self.flux_dn, self.flux_dn_dir, self.flux_net = flux_up, flux_dn, flux_dn_dir, flux_net
+
+    def are_desired(self):
+        return any(x is not None for x in (self.flux_up, self.flux_dn, self.flux_dn_dir, self.flux_net))
+
+
+# ---------------------------------------------------------------------------------------------
+class GasOpticsRRTMGP(OpticalProps):
+    """ty_gas_optics_rrtmgp, NN branch.  The lookup-table branch needs the k-distribution files that are
+    missing from the reference and is not provided."""
+
+    def load(self, which, device=None):
+        """Load the (surrogate) k-distribution tables, 'lw' (g256) or 'sw' (g224)."""
+        kd = data.load_kdist(which)
+        e = self.init(kd["band_lims_wvn"], kd["band_lims_gpt"])
+        if e:
+            return e
+        self.kd = kd
+        self.dev = device or "cuda:%d" % torch.cuda.current_device()
+        self.press_ref_min = float(kd["press_ref_min"][0])
+        self.temp_ref_min = float(kd["temp_ref_min"][0])
+        self.temp_ref_max = float(kd["temp_ref_max"][0])
+        if which == "lw":
+            self.totplnk = torch.as_tensor(kd["totplnk"], device=self.dev)  # (nbnd, nPlanckTemp) = Fortran (nT, nbnd)
+            self.totplnk_delta = float(kd["totplnk_delta"])
+            self.solar_source = None
+        else:
+            self.totplnk = None
+            self.solar_source = np.asarray(kd["solar_source"], np.float32).copy()
+        return ""
+
+    def source_is_internal(self):
+        return self.totplnk is not None
+
+    def source_is_external(self):
+        return self.solar_source is not None
+
+    def get_press_min(self):
+        return self.press_ref_min
+
+    def get_temp_min(self):
+        return self.temp_ref_min
+
+    def get_temp_max(self):
+        return self.temp_ref_max
+
+    def get_nPlanckTemp(self):
+        return int(self.totplnk.shape[1])
+
+    def set_tsi(self, tsi):
+        if tsi < 0:
+            return "tsi out of range"
+        self.solar_source = data.set_tsi(self.solar_source, tsi)
+        return ""
+
+    # -- helpers ----
+    def _nn_inputs(self, ctx, play, tlay, gas_desc, net):
+        ncol, nlay = play.shape
+        nx = net.dims[0]
+        ptrs, nds, keep = [], [], []
+        for k, name in enumerate(net.input_names):
+            if k < 2 or name not in gas_desc.concs:
+                ptrs.append(None)
+                nds.append(2)
+                continue
+            t = gas_desc.concs[name]
+            keep.append(t)
+            ptrs.append(t.data_ptr())
+            nds.append(gas_desc.ndims(name))
+        if net.input_names[2] not in gas_desc.concs or net.input_names[3] not in gas_desc.concs:
+            return None, "compute_nn_inputs: gas " + net.input_names[2] + "/" + net.input_names[3] + " not found"
+        x = torch.empty((ncol, nlay, nx), dtype=torch.float32, device=play.device)
+        check(_lib.lib().rrtmgpnn_compute_nn_inputs(ctx.h, ncol, nlay, nx, _p(play), _p(tlay), ptr_array(ptrs),
+                                                    int_array(nds), net.h, _p(x)), "compute_nn_inputs")
+        return x, ""
+
+    def gas_optics(self, play, plev, tlay, *args, **kw):
+        """LW: gas_optics(play, plev, tlay, tsfc, gas_desc, optical_props, sources, col_dry=, tlev=, neural_nets=)
+        SW: gas_optics(play, plev, tlay, gas_desc, optical_props, toa_src, col_dry=, neural_nets=)"""
+        if self.source_is_internal():
+            return self._gas_optics_int(play, plev, tlay, *args, **kw)
+        return self._gas_optics_ext(play, plev, tlay, *args, **kw)
+
+    def _common(self, play, plev, tlay, gas_desc, optical_props, col_dry):
+        ncol, nlay = play.shape
+        if plev.shape != (ncol, nlay + 1) or tlay.shape != (ncol, nlay):
+            return None, "gas_optics(): array plev/tlay has wrong size"
+        if optical_props.get_ngpt() != self.get_ngpt() or optical_props.get_ncol() != ncol or \
+                optical_props.get_nlay() != nlay:
+            return None, "gas_optics(): optical properties inconsistently sized"
+        ctx = context(play.device.index)
+        if col_dry is None:
+            if "h2o" not in gas_desc.concs:
+                return None, "gas_optics(): h2o concentration is required"
+            col_dry = torch.empty((ncol, nlay), dtype=torch.float32, device=play.device)
+            check(_lib.lib().rrtmgpnn_get_col_dry(ctx.h, ncol, nlay, _p(gas_desc.concs["h2o"]), _p(plev), _p(col_dry)),
+                  "get_col_dry")
+        return (ctx, col_dry), ""
+
+    def _gas_optics_int(self, play, plev, tlay, tsfc, gas_desc, optical_props, sources, col_dry=None, tlev=None,
+                        neural_nets=None):
+        if neural_nets is None:
+            return "gas_optics(): the lookup-table branch is not available (k-distribution files missing); pass neural_nets"
+        r, e = self._common(play, plev, tlay, gas_desc, optical_props, col_dry)
+        if e:
+            return e
+        ctx, cd = r
+        ncol, nlay = play.shape
+        ngpt = self.get_ngpt()
+        L = _lib.lib()
+        if tlev is None:  # mo_gas_optics_rrtmgp.F90:317-337
+            tlev = torch.empty((ncol, nlay + 1), dtype=torch.float32, device=play.device)
+            check(L.rrtmgpnn_interpolate_tlev(ctx.h, ncol, nlay, _p(play), _p(plev), _p(tlay), _p(tlev)), "tlev")
+        x, e = self._nn_inputs(ctx, play, tlay, gas_desc, neural_nets[0])
+        if e:
+            return e
+        nets = ptr_array([n.h.value for n in neural_nets])
+        check(L.rrtmgpnn_predict_nn_lw(ctx.h, ncol, nlay, ngpt, neural_nets[0].dims[0], _p(x), _p(cd), nets,
+                                       len(neural_nets), _p(optical_props.tau), _p(sources.lay_source)),
+              "predict_nn_lw")
+        sfc_lay = 1 if float(play[0, 0]) > float(play[0, nlay - 1]) else nlay  # :402
+        check(L.rrtmgpnn_compute_planck_source_nn(
+            ctx.h, ncol, nlay, self.get_nband(), ngpt, self.get_nPlanckTemp(), _p(tlay), _p(tlev), _p(tsfc), sfc_lay,
+            int_array(self.band_lims_gpt.ravel()), self.temp_ref_min, self.totplnk_delta, _p(self.totplnk),
+            _p(sources.sfc_source), _p(sources.sfc_source_Jac), _p(sources.lay_source), _p(sources.lev_source)),
+            "compute_planck_source_nn")
+        return ""
+
+    def _gas_optics_ext(self, play, plev, tlay, gas_desc, optical_props, toa_src, col_dry=None, neural_nets=None):
+        if neural_nets is None:
+            return "gas_optics(): the lookup-table branch is not available (k-distribution files missing); pass neural_nets"
+        r, e = self._common(play, plev, tlay, gas_desc, optical_props, col_dry)
+        if e:
+            return e
+        ctx, cd = r
+        ncol, nlay = play.shape
+        ngpt = self.get_ngpt()
+        x, e = self._nn_inputs(ctx, play, tlay, gas_desc, neural_nets[0])
+        if e:
+            return e
+        nets = ptr_array([n.h.value for n in neural_nets])
+        is2 = isinstance(optical_props, OpticalProps2str)
+        check(_lib.lib().rrtmgpnn_predict_nn_sw(
+            ctx.h, ncol, nlay, ngpt, neural_nets[0].dims[0], _p(x), _p(cd), nets, _p(optical_props.tau),
+            _p(optical_props.ssa) if is2 else None, _p(optical_props.g) if is2 else None), "predict_nn_sw")
+        if tuple(toa_src.shape) != (ncol, ngpt):
+            return "gas_optics(): array toa_src has wrong size"
+        toa_src.copy_(torch.as_tensor(self.solar_source, device=toa_src.device).expand(ncol, ngpt))  # :594-599
+        return ""
+
+
+# ---------------------------------------------------------------------------------------------
+GAUSS_DS = {1: [1.66], 2: [1.18350343, 2.81649655], 3: [1.09719858, 1.69338507, 4.70941630],
+            4: [1.06056257, 1.38282560, 2.40148179, 7.15513024]}
+GAUSS_WTS = {1: [0.5], 2: [0.3180413817, 0.1819586183], 3: [0.2009319137, 0.2292411064, 0.0698269799],
+             4: [0.1355069134, 0.2034645680, 0.1298475476, 0.0311809710]}
+
+
+def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_gauss_angles=None,
+           use_2stream=False, lw_Ds=None, flux_up_Jac=None, flux_dn_Jac=None):
+    """rte/mo_rte_lw.F90:60-424.  sfc_emis (ncol, nband)."""
+    if not fluxes.are_desired():
+        return "rte_lw: no space allocated for fluxes"
+    nmu = 1 if n_gauss_angles is None else int(n_gauss_angles)
+    if nmu > 4:
+        return "rte_lw: asking for too many quadrature points for no-scattering calculation"
+    if nmu < 1:
+        return "rte_lw: have to ask for at least one quadrature point for no-scattering calculation"
+    if not isinstance(optical_props, OpticalProps1scl):
+        return "rte_lw: two-stream / rescaled longwave solvers are not implemented (1scl only)"
+    if use_2stream:
+        return "rte_lw: can't use two-stream methods with only absorption optical depth"
+    if lw_Ds is not None:
+        return "rte_lw: lw_Ds (column-dependent diffusivity) is not implemented"
+    if flux_up_Jac is not None or flux_dn_Jac is not None:
+        return "rte_lw: compute_Jac is .false. in this configuration (rte/mo_rte_rrtmgp_config.F90:28)"
+    ncol, nlay, ngpt = optical_props.tau.shape
+    nband = optical_props.get_nband()
+    if tuple(sfc_emis.shape) != (ncol, nband):
+        return "rte_lw: sfc_emis inconsistently sized"
+    if inc_flux is not None and tuple(inc_flux.shape) != (ncol, ngpt):
+        return "rte_lw: inc_flux inconsistently sized"
+    ctx = context(optical_props.tau.device.index)
+    L = _lib.lib()
+    emis = _f32dev(sfc_emis, optical_props.tau.device)
+    emis_gpt = torch.empty((ncol, ngpt), dtype=torch.float32, device=emis.device)
+    check(L.rrtmgpnn_expand_band_to_gpt(ctx.h, nband, ngpt, ncol, int_array(optical_props.band_lims_gpt.ravel()),
+                                        _p(emis), _p(emis_gpt)), "expand")
+    up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=emis.device)
+    dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=emis.device)
+    check(L.rrtmgpnn_lw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu, float_array(GAUSS_DS[nmu]),
+                                      float_array(GAUSS_WTS[nmu]), _p(inc_flux), _p(optical_props.tau),
+                                      _p(sources.lay_source), _p(sources.lev_source), _p(emis_gpt),
+                                      _p(sources.sfc_source), _p(up), _p(dn)), "lw_solver_noscat")
+    if fluxes.flux_net is not None:
+        torch.sub(dn, up, out=fluxes.flux_net)
+    return ""
+
+
+def rte_sw(atmos, top_at_1, mu0, inc_flux, sfc_alb_dir_gpt, sfc_alb_dif_gpt, fluxes, inc_flux_dif=None):
+    """rte/mo_rte_sw.F90:48-266 (fork: albedos per g-point (ncol, ngpt))."""
+    if not fluxes.are_desired():
+        return "rte_sw: no space allocated for fluxes"
+    if not isinstance(atmos, OpticalProps2str):
+        return "rte_sw: the no-scattering (1scl) shortwave solver is not implemented (2str only)"
+    ncol, nlay, ngpt = atmos.tau.shape
+    if tuple(mu0.shape) != (ncol,):
+        return "rte_sw: mu0 inconsistently sized"
+    if tuple(inc_flux.shape) != (ncol, ngpt):
+        return "rte_sw: inc_flux inconsistently sized"
+    if tuple(sfc_alb_dir_gpt.shape) != (ncol, ngpt):
+        return "rte_sw: sfc_alb_dir inconsistently sized"
+    if tuple(sfc_alb_dif_gpt.shape) != (ncol, ngpt):
+        return "rte_sw: sfc_alb_dif inconsistently sized"
+    if inc_flux_dif is not None and tuple(inc_flux_dif.shape) != (ncol, ngpt):
+        return "rte_sw: inc_flux_dif inconsistently sized"
+    ctx = context(atmos.tau.device.index)
+    dev = atmos.tau.device
+    up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=dev)
+    dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=dev)
+    dr = fluxes.flux_dn_dir if fluxes.flux_dn_dir is not None else torch.empty((ncol, nlay + 1), device=dev)
+    check(_lib.lib().rrtmgpnn_sw_solver_2stream(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
+                                                _p(inc_flux_dif), _p(atmos.tau), _p(atmos.ssa), _p(atmos.g), _p(mu0),
+                                                _p(sfc_alb_dir_gpt), _p(sfc_alb_dif_gpt), _p(up), _p(dn), _p(dr)),
+          "sw_solver_2stream")
+    if fluxes.flux_net is not None:
+        torch.sub(dn, up, out=fluxes.flux_net)
+    return ""

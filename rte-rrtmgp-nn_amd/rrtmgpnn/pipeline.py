@@ -1,0 +1,149 @@
+"""Device-resident clear-sky LW+SW step: the hot path of BASELINE.json's metric.
+
+One `ClearSkyStep` owns every input and output of one column block in HBM and replays
+    gas_optics_int (NN)  ->  rte_lw (no-scattering)      [LW, g256]
+    gas_optics_ext (NN)  ->  rte_sw (two-stream)         [SW, g224]
+with the same kernels as the class-level API (api.py), but with all ctypes arguments prepared once
+so the host cost per step is just the launches (or one hipGraph replay).
+
+What one step computes is exactly the drivers' per-block work
+(examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:399-441, rrtmgp_rfmip_sw.F90:374-451):
+compute_nn_inputs, get_col_dry, both NN models per stream with post-processing, the Planck sources,
+the band->g emissivity expansion, both solvers and the broadband reductions.  Constant driver-side
+inputs that do not depend on the atmospheric state are prepared once: the SW incident flux
+(solar_source after set_tsi, renormalised to each column's TSI) and the per-g-point albedos.
+col_dry is computed once per step and shared by LW and SW (same h2o and plev).
+"""
+import numpy as np
+import torch
+
+from . import _lib, data
+from ._lib import check, float_array, int_array, ptr_array
+from .api import GAUSS_DS, GAUSS_WTS, Context
+
+
+def _t(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
+
+
+class ClearSkyStep:
+    def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
+                 sw_models=("sw_abs", "sw_ray")):
+        self.dev = torch.device("cuda", device)
+        self.ctx = ctx or Context(device)
+        L = self.L = _lib.lib()
+        self.kd_lw, self.kd_sw = data.load_kdist("lw"), data.load_kdist("sw")
+        self.ncol, self.nlay = ncol, nlay = prob["ncol"], prob["nlay"]
+        self.top_at_1 = int(bool(prob["top_at_1"]))
+        dev = self.dev
+
+        def net(name):
+            h = _lib.c_vp()
+            check(L.rrtmgpnn_network_load(self.ctx.h, data.path(name).encode(), h), "network_load " + name)
+            return h
+
+        self.lw_nets = [net(n) for n in lw_models]
+        self.sw_nets = [net(n) for n in sw_models]
+        self.lw_names = data.rbin.unchars(data.load_model(lw_models[0])["input_names"])
+        self.sw_names = data.rbin.unchars(data.load_model(sw_models[0])["input_names"])
+        self.nx_lw, self.nx_sw = len(self.lw_names), len(self.sw_names)
+        self.ng_lw, self.ng_sw = self.kd_lw["ngpt"], self.kd_sw["ngpt"]
+        self.nb_lw = self.kd_lw["nband"]
+
+        # ---- inputs (HBM resident) ----
+        self.play, self.plev = _t(prob["play"], dev), _t(prob["plev"], dev)
+        self.tlay, self.tlev, self.tsfc = _t(prob["tlay"], dev), _t(prob["tlev"], dev), _t(prob["tsfc"], dev)
+        self.gases = {k: _t(v, dev) for k, v in prob["gases"].items()}
+        self.sfc_emis = _t(np.repeat(prob["sfc_emis"][:, None], self.nb_lw, axis=1), dev)  # (ncol, nband)
+        self.mu0 = _t(prob["mu0"], dev)
+        self.toa = _t(data.toa_flux(prob, self.kd_sw), dev)
+        self.alb = _t(np.repeat(prob["sfc_alb"][:, None], self.ng_sw, axis=1), dev)
+        self.totplnk = _t(self.kd_lw["totplnk"], dev)
+        self.sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
+
+        # ---- intermediates / outputs ----
+        f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
+        self.col_dry = f(ncol, nlay)
+        self.x_lw, self.x_sw = f(ncol, nlay, self.nx_lw), f(ncol, nlay, self.nx_sw)
+        self.tau_lw, self.lay_src = f(ncol, nlay, self.ng_lw), f(ncol, nlay, self.ng_lw)
+        self.lev_src = f(ncol, nlay + 1, self.ng_lw)
+        self.sfc_src, self.sfc_jac, self.emis_gpt = f(ncol, self.ng_lw), f(ncol, self.ng_lw), f(ncol, self.ng_lw)
+        self.tau_sw, self.ssa_sw, self.g_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
+        self.lw_up, self.lw_dn = f(ncol, nlay + 1), f(ncol, nlay + 1)
+        self.sw_up, self.sw_dn, self.sw_dir = f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1)
+
+        # ---- prepared ctypes argument lists ----
+        def gas_args(names):
+            ptrs, nds = [], []
+            for k, n in enumerate(names):
+                t = self.gases.get(n) if k >= 2 else None
+                ptrs.append(t.data_ptr() if t is not None else None)
+                nds.append(2)
+            return ptr_array(ptrs), int_array(nds)
+
+        p = lambda t: t.data_ptr()  # noqa: E731
+        self._g_lw, self._nd_lw = gas_args(self.lw_names)
+        self._g_sw, self._nd_sw = gas_args(self.sw_names)
+        self._nets_lw = ptr_array([h.value for h in self.lw_nets])
+        self._nets_sw = ptr_array([h.value for h in self.sw_nets])
+        self._lims_lw = int_array(self.kd_lw["band_lims_gpt"].ravel())
+        self._Ds, self._W = float_array(GAUSS_DS[nmus]), float_array(GAUSS_WTS[nmus])
+        self.nmus = nmus
+        c = self.ctx.h
+        self.calls = [
+            ("get_col_dry", L.rrtmgpnn_get_col_dry, (c, ncol, nlay, p(self.gases["h2o"]), p(self.plev), p(self.col_dry))),
+            ("nn_inputs_lw", L.rrtmgpnn_compute_nn_inputs,
+             (c, ncol, nlay, self.nx_lw, p(self.play), p(self.tlay), self._g_lw, self._nd_lw, self.lw_nets[0],
+              p(self.x_lw))),
+            ("predict_nn_lw", L.rrtmgpnn_predict_nn_lw,
+             (c, ncol, nlay, self.ng_lw, self.nx_lw, p(self.x_lw), p(self.col_dry), self._nets_lw, len(self.lw_nets),
+              p(self.tau_lw), p(self.lay_src))),
+            ("planck_source", L.rrtmgpnn_compute_planck_source_nn,
+             (c, ncol, nlay, self.nb_lw, self.ng_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev),
+              p(self.tsfc), self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]),
+              float(self.kd_lw["totplnk_delta"]), p(self.totplnk), p(self.sfc_src), p(self.sfc_jac),
+              p(self.lay_src), p(self.lev_src))),
+            ("expand_emis", L.rrtmgpnn_expand_band_to_gpt,
+             (c, self.nb_lw, self.ng_lw, ncol, self._lims_lw, p(self.sfc_emis), p(self.emis_gpt))),
+            ("lw_solver", L.rrtmgpnn_lw_solver_noscat,
+             (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None, p(self.tau_lw),
+              p(self.lay_src), p(self.lev_src), p(self.emis_gpt), p(self.sfc_src), p(self.lw_up), p(self.lw_dn))),
+            ("nn_inputs_sw", L.rrtmgpnn_compute_nn_inputs,
+             (c, ncol, nlay, self.nx_sw, p(self.play), p(self.tlay), self._g_sw, self._nd_sw, self.sw_nets[0],
+              p(self.x_sw))),
+            ("predict_nn_sw", L.rrtmgpnn_predict_nn_sw,
+             (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.x_sw), p(self.col_dry), self._nets_sw, p(self.tau_sw),
+              p(self.ssa_sw), p(self.g_sw))),
+            ("sw_solver", L.rrtmgpnn_sw_solver_2stream,
+             (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
+              p(self.g_sw), p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
+        ]
+        self.graph = None
+
+    def step(self):
+        for name, fn, args in self.calls:
+            rc = fn(*args)
+            if rc:
+                check(rc, name)
+
+    def capture(self):
+        """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`."""
+        self.step()  # warm-up: kernel attributes + workspace allocation happen outside capture
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.dev)
+        old = self.ctx.stream
+        with torch.cuda.stream(s):
+            self.ctx.use_stream(s)
+            with torch.cuda.graph(g, stream=s):
+                self.step()
+        self.ctx.use_stream(old)
+        self.graph = g
+        return g
+
+    def replay(self):
+        self.graph.replay()
+
+    def fluxes(self):
+        """Host copies of the broadband fluxes, with SW zeroed where sza >= 90 is applied by the caller."""
+        return {k: getattr(self, k).cpu().numpy() for k in ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir")}

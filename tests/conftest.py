@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rte-rrtmgp-nn_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box with -m gpu)")
+
+
+@pytest.fixture(scope="session")
+def orc():
+    import oracle as O
+    return O.Oracle()
+
+
+@pytest.fixture(scope="session")
+def rfmip():
+    from rrtmgpnn import data
+    return data.rfmip_problem()
+
+
+def subset(prob, idx):
+    import numpy as np
+    idx = np.asarray(idx)
+    sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == prob["ncol"] else v)
+           for k, v in prob.items()}
+    sub["gases"] = {k: v[idx] for k, v in prob["gases"].items()}
+    sub["ncol"] = len(idx)
+    return sub

@@ -1,0 +1,305 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle on the same inputs.
+
+Tolerances (float32 throughout, north star: <= 1e-3 W/m2 RMS flux error):
+  * MLP raw outputs: <= 2 ulp (the MFMA kernel accumulates every dot product in the oracle's k order)
+  * optical depths / sources: relative 2e-5 (libm vs device expf/logf/sqrtf differ by <= 1-2 ulp,
+    amplified 8x by the (.)^8 post-processing)
+  * broadband fluxes: RMS <= 1e-3 W/m2 and max abs <= 1e-2 W/m2
+"""
+import numpy as np
+import pytest
+
+from conftest import subset
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    torch.cuda.set_device(0)
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def models():
+    from rrtmgpnn import data
+    return {k: data.load_model(k) for k in ("lw_abs", "lw_pfrac", "sw_abs", "sw_ray", "lw_g128_both")}
+
+
+def T(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
+
+
+def rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
+
+
+def assert_flux(got, ref, what):
+    r, m = rms(got, ref), float(np.max(np.abs(got - ref)))
+    assert r <= 1e-3 and m <= 1e-2, "%s: RMS %.3g, max %.3g W/m2" % (what, r, m)
+
+
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["lw_abs", "lw_pfrac", "sw_abs", "sw_ray", "lw_g128_both"])
+@pytest.mark.parametrize("nbatch", [1, 15, 16, 4097])
+def test_mlp_forward_matches_oracle(dev, orc, models, name, nbatch):
+    from rrtmgpnn import api, data
+    m = models[name]
+    rng = np.random.default_rng(nbatch)
+    x = rng.uniform(-0.2, 1.2, size=(nbatch, int(m["dims"][0]))).astype(np.float32)
+    net = api.RrtmgpNetwork(0).load_netcdf(data.path(name))
+    y = net.output_sgemm_flat(T(x, dev)).cpu().numpy()
+    np.testing.assert_array_max_ulp(y, orc.mlp(m, x), maxulp=2)
+
+
+def test_lw_gas_optics_matches_oracle(dev, orc, rfmip, models):
+    from rrtmgpnn import api, data
+    prob = subset(rfmip, np.arange(0, 1800, 7))
+    ncol, nlay = prob["ncol"], prob["nlay"]
+    ref = orc.lw_gas_optics(prob, [models["lw_abs"], models["lw_pfrac"]], data.load_kdist("lw"))
+    kd = api.GasOpticsRRTMGP()
+    api.stop_on_err(kd.load("lw"))
+    nets = [api.RrtmgpNetwork(0).load_netcdf(data.path("lw_abs")), api.RrtmgpNetwork(0).load_netcdf(data.path("lw_pfrac"))]
+    gc = api.GasConcs()
+    api.stop_on_err(gc.init(list(prob["gases"])))
+    for k, v in prob["gases"].items():
+        api.stop_on_err(gc.set_vmr(k, T(v, dev)))
+    op = api.OpticalProps1scl()
+    api.stop_on_err(op.alloc_1scl(ncol, nlay, kd))
+    src = api.SourceFuncLW()
+    api.stop_on_err(src.alloc(ncol, nlay, kd))
+    api.stop_on_err(kd.gas_optics(T(prob["play"], dev), T(prob["plev"], dev), T(prob["tlay"], dev),
+                                  T(prob["tsfc"], dev), gc, op, src, tlev=T(prob["tlev"], dev), neural_nets=nets))
+    np.testing.assert_allclose(op.tau.cpu().numpy(), ref["tau"], rtol=2e-5, atol=1e-30)
+    np.testing.assert_allclose(src.lay_source.cpu().numpy(), ref["lay_source"], rtol=2e-5, atol=1e-12)
+    np.testing.assert_allclose(src.lev_source.cpu().numpy(), ref["lev_source"], rtol=2e-5, atol=1e-12)
+    np.testing.assert_allclose(src.sfc_source.cpu().numpy(), ref["sfc_source"], rtol=2e-5, atol=1e-12)
+    np.testing.assert_allclose(src.sfc_source_Jac.cpu().numpy(), ref["sfc_source_Jac"], rtol=2e-5, atol=1e-12)
+
+
+def test_sw_gas_optics_matches_oracle(dev, orc, rfmip, models):
+    from rrtmgpnn import api, data
+    prob = subset(rfmip, np.arange(3, 1800, 11))
+    ncol, nlay = prob["ncol"], prob["nlay"]
+    ref = orc.sw_gas_optics(prob, [models["sw_abs"], models["sw_ray"]])
+    kd = api.GasOpticsRRTMGP()
+    api.stop_on_err(kd.load("sw"))
+    nets = [api.RrtmgpNetwork(0).load_netcdf(data.path("sw_abs")), api.RrtmgpNetwork(0).load_netcdf(data.path("sw_ray"))]
+    gc = api.GasConcs()
+    api.stop_on_err(gc.init(["h2o", "o3", "co2", "n2o", "ch4"]))
+    for k in ["h2o", "o3", "co2", "n2o", "ch4"]:
+        api.stop_on_err(gc.set_vmr(k, T(prob["gases"][k], dev)))
+    op = api.OpticalProps2str()
+    api.stop_on_err(op.alloc_2str(ncol, nlay, kd))
+    op.g.fill_(7.0)  # must be zero-filled by gas_optics (mo_gas_optics_rrtmgp.F90:560-567)
+    toa = torch.empty((ncol, kd.get_ngpt()), device=dev)
+    api.stop_on_err(kd.gas_optics(T(prob["play"], dev), T(prob["plev"], dev), T(prob["tlay"], dev), gc, op, toa,
+                                  neural_nets=nets))
+    np.testing.assert_allclose(op.tau.cpu().numpy(), ref["tau"], rtol=2e-5, atol=1e-30)
+    np.testing.assert_allclose(op.ssa.cpu().numpy(), ref["ssa"], rtol=2e-5, atol=1e-30)
+    assert float(op.g.abs().max()) == 0.0
+    np.testing.assert_allclose(toa.cpu().numpy()[0], kd.solar_source, rtol=0)
+
+
+@pytest.mark.parametrize("nmus", [1, 2, 3, 4])
+@pytest.mark.parametrize("top_at_1", [True, False])
+def test_lw_solver_matches_oracle(dev, orc, nmus, top_at_1):
+    from rrtmgpnn import api, rbin
+    import os
+    g = rbin.read(os.path.join(os.path.dirname(__file__), "golden", "rfmip8_reference.rbin"))
+    sl = (slice(None), slice(None)) if top_at_1 else (slice(None), slice(None, None, -1))
+    tau, lay, lev = g["lw_tau"][sl], g["lw_lay_source"][sl], g["lw_lev_source"][sl]
+    ncol, nlay, ngpt = tau.shape
+    emis = np.repeat(g["lw_sfc_emis_band"][:, :1], ngpt, axis=1)
+    inc = np.full((ncol, ngpt), 0.05, np.float32) if nmus == 2 else None
+    up_o, dn_o = orc.lw_solver(tau, lay, lev, emis, g["lw_sfc_source"], top_at_1, nmus, inc_flux=inc)
+    kd = api.GasOpticsRRTMGP()
+    api.stop_on_err(kd.load("lw"))
+    op = api.OpticalProps1scl()
+    api.stop_on_err(op.alloc_1scl(ncol, nlay, kd))
+    op.tau.copy_(T(tau, dev))
+    src = api.SourceFuncLW()
+    api.stop_on_err(src.alloc(ncol, nlay, kd))
+    src.lay_source.copy_(T(lay, dev))
+    src.lev_source.copy_(T(lev, dev))
+    src.sfc_source.copy_(T(g["lw_sfc_source"], dev))
+    fl = api.FluxesBroadband(torch.empty((ncol, nlay + 1), device=dev), torch.empty((ncol, nlay + 1), device=dev),
+                             flux_net=torch.empty((ncol, nlay + 1), device=dev))
+    api.stop_on_err(api.rte_lw(op, top_at_1, src, T(g["lw_sfc_emis_band"], dev), fl,
+                               inc_flux=None if inc is None else T(inc, dev), n_gauss_angles=nmus))
+    assert_flux(fl.flux_up.cpu().numpy(), up_o, "lw up")
+    assert_flux(fl.flux_dn.cpu().numpy(), dn_o, "lw dn")
+    np.testing.assert_allclose(fl.flux_net.cpu().numpy(), (fl.flux_dn - fl.flux_up).cpu().numpy(), rtol=0, atol=0)
+    if nmus in (1, 3) and top_at_1:  # and directly against the REFERENCE's rte_lw outputs
+        assert_flux(fl.flux_up.cpu().numpy(), g["lw_flux_up_nmu%d" % nmus], "lw up vs reference")
+        assert_flux(fl.flux_dn.cpu().numpy(), g["lw_flux_dn_nmu%d" % nmus], "lw dn vs reference")
+    if nmus == 1 and not top_at_1:
+        assert_flux(fl.flux_up.cpu().numpy(), g["lw_flux_up_flip"], "lw up (flipped) vs reference")
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_sw_solver_matches_reference_fixture(dev, flip):
+    from rrtmgpnn import api, rbin
+    import os
+    g = rbin.read(os.path.join(os.path.dirname(__file__), "golden", "rfmip8_reference.rbin"))
+    sl = (slice(None), slice(None, None, -1)) if flip else (slice(None), slice(None))
+    ncol, nlay, ngpt = g["sw_tau"].shape
+    kd = api.GasOpticsRRTMGP()
+    api.stop_on_err(kd.load("sw"))
+    op = api.OpticalProps2str()
+    api.stop_on_err(op.alloc_2str(ncol, nlay, kd))
+    op.tau.copy_(T(g["sw_tau"][sl], dev))
+    op.ssa.copy_(T(g["sw_ssa"][sl], dev))
+    op.g.copy_(T(g["sw_g"][sl], dev))
+    f = lambda: torch.empty((ncol, nlay + 1), device=dev)  # noqa: E731
+    fl = api.FluxesBroadband(f(), f(), f())
+    api.stop_on_err(api.rte_sw(op, not flip, T(g["sw_mu0"], dev), T(g["sw_toa"], dev), T(g["sw_alb"], dev),
+                               T(g["sw_alb"], dev), fl))
+    suf = "_flip" if flip else ""
+    assert_flux(fl.flux_up.cpu().numpy(), g["sw_flux_up" + suf], "sw up")
+    assert_flux(fl.flux_dn.cpu().numpy(), g["sw_flux_dn" + suf], "sw dn")
+    assert_flux(fl.flux_dn_dir.cpu().numpy(), g["sw_flux_dir" + suf], "sw dir")
+
+
+def test_sw_solver_with_scattering_and_diffuse_inc(dev, orc):
+    """g != 0 and a diffuse incident flux exercise branches the clear-sky NN path never reaches."""
+    from rrtmgpnn import api
+    rng = np.random.default_rng(5)
+    ncol, nlay, ngpt = 37, 23, 224
+    tau = rng.lognormal(-2, 2, size=(ncol, nlay, ngpt)).astype(np.float32)
+    ssa = rng.uniform(0, 1, size=tau.shape).astype(np.float32)
+    gg = rng.uniform(0, 0.9, size=tau.shape).astype(np.float32)
+    mu0 = rng.uniform(0.05, 1, size=ncol).astype(np.float32)
+    inc = rng.uniform(0, 10, size=(ncol, ngpt)).astype(np.float32)
+    dif = rng.uniform(0, 1, size=(ncol, ngpt)).astype(np.float32)
+    ad = rng.uniform(0, 1, size=(ncol, ngpt)).astype(np.float32)
+    af = rng.uniform(0, 1, size=(ncol, ngpt)).astype(np.float32)
+    up_o, dn_o, dr_o = orc.sw_solver(tau, ssa, gg, mu0, inc, ad, af, True, inc_flux_dif=dif)
+    kd = api.GasOpticsRRTMGP()
+    api.stop_on_err(kd.load("sw"))
+    op = api.OpticalProps2str()
+    api.stop_on_err(op.alloc_2str(ncol, nlay, kd))
+    op.tau.copy_(T(tau, dev))
+    op.ssa.copy_(T(ssa, dev))
+    op.g.copy_(T(gg, dev))
+    f = lambda: torch.empty((ncol, nlay + 1), device=dev)  # noqa: E731
+    fl = api.FluxesBroadband(f(), f(), f())
+    api.stop_on_err(api.rte_sw(op, True, T(mu0, dev), T(inc, dev), T(ad, dev), T(af, dev), fl, inc_flux_dif=T(dif, dev)))
+    assert_flux(fl.flux_up.cpu().numpy(), up_o, "sw up")
+    assert_flux(fl.flux_dn.cpu().numpy(), dn_o, "sw dn")
+    assert_flux(fl.flux_dn_dir.cpu().numpy(), dr_o, "sw dir")
+
+
+def _oracle_fluxes(orc, prob, models):
+    from rrtmgpnn import data
+    lu, ld, _ = orc.clear_sky_lw(prob, [models["lw_abs"], models["lw_pfrac"]], data.load_kdist("lw"))
+    su, sd, sr, _ = orc.clear_sky_sw(prob, [models["sw_abs"], models["sw_ray"]], data.load_kdist("sw"))
+    return {"lw_up": lu, "lw_dn": ld, "sw_up": su, "sw_dn": sd, "sw_dir": sr}
+
+
+def _check_pipeline(got, ref, usecol):
+    m = ~usecol
+    for k in ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir"):
+        g = got[k].copy()
+        r = ref[k]
+        if k in ("sw_up", "sw_dn"):
+            g[m] = 0.0
+        if k == "sw_dir":
+            g, r = g[~m], r[~m]
+        assert_flux(g, r, k)
+
+
+def test_full_rfmip_clear_sky_lw_sw(dev, orc, rfmip, models):
+    """C3 (all 1800 RFMIP columns): the benchmarked step vs the oracle, plus heating-rate agreement."""
+    from rrtmgpnn.pipeline import ClearSkyStep
+    step = ClearSkyStep(rfmip, device=0)
+    step.step()
+    torch.cuda.synchronize()
+    got = step.fluxes()
+    ref = _oracle_fluxes(orc, rfmip, models)
+    _check_pipeline(got, ref, rfmip["usecol"])
+    # heating rate (examples/rrtmgp-nn-training/rrtmgp_lw_eval_nn_rfmip.F90:624-653), K/day
+    dp = np.diff(rfmip["plev"], axis=1)
+
+    def hr(up, dn):
+        return -(86400.0 * 9.80665 / 1004.0) * np.diff(dn - up, axis=1) / dp
+    assert np.max(np.abs(hr(got["lw_up"], got["lw_dn"]) - hr(ref["lw_up"], ref["lw_dn"]))[:, 5:]) < 1e-3
+
+
+def test_graph_replay_is_bitwise_identical_to_eager(dev, rfmip):
+    from rrtmgpnn.pipeline import ClearSkyStep
+    step = ClearSkyStep(subset(rfmip, np.arange(0, 1800, 5)), device=0)
+    step.step()
+    torch.cuda.synchronize()
+    a = step.fluxes()
+    step.capture()
+    for t in (step.lw_up, step.lw_dn, step.sw_up, step.sw_dn, step.sw_dir):
+        t.fill_(float("nan"))
+    step.replay()
+    torch.cuda.synchronize()
+    b = step.fluxes()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_column_subset_invariance_bitwise(dev, rfmip):
+    """tests/verification.py column subsetting: a column's fluxes do not depend on its neighbours."""
+    from rrtmgpnn.pipeline import ClearSkyStep
+    full = ClearSkyStep(rfmip, device=0)
+    full.step()
+    idx = np.arange(901, 1800)
+    half = ClearSkyStep(subset(rfmip, idx), device=0)
+    half.step()
+    torch.cuda.synchronize()
+    a, b = full.fluxes(), half.fluxes()
+    for k in a:
+        np.testing.assert_array_equal(a[k][idx], b[k])
+
+
+def test_sw_tsi_linearity(dev, rfmip):
+    """tests/verification.py sw_clear_sky_tsi: fluxes scale linearly with the incident flux."""
+    from rrtmgpnn.pipeline import ClearSkyStep
+    step = ClearSkyStep(subset(rfmip, np.arange(0, 1800, 9)), device=0)
+    step.step()
+    torch.cuda.synchronize()
+    a = step.fluxes()
+    step.toa.mul_(0.5)
+    step.step()
+    torch.cuda.synchronize()
+    b = step.fluxes()
+    for k in ("sw_up", "sw_dn", "sw_dir"):
+        np.testing.assert_allclose(b[k], 0.5 * a[k], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("nlay,ncol", [(2, 3), (137, 50), (60, 1)])
+def test_pipeline_shapes_vs_oracle(dev, orc, models, nlay, ncol):
+    from rrtmgpnn import data
+    from rrtmgpnn.pipeline import ClearSkyStep
+    if nlay == 60:
+        prob = subset(data.rfmip_problem(), [1234])
+    else:
+        prob = data.synthetic_problem(ncol, nlay, seed=nlay)
+    step = ClearSkyStep(prob, device=0)
+    step.step()
+    torch.cuda.synchronize()
+    _check_pipeline(step.fluxes(), _oracle_fluxes(orc, prob, models), prob["usecol"])
+
+
+def test_api_error_messages(dev):
+    from rrtmgpnn import api
+    kd = api.GasOpticsRRTMGP()
+    api.stop_on_err(kd.load("lw"))
+    op = api.OpticalProps1scl()
+    api.stop_on_err(op.alloc_1scl(4, 5, kd))
+    src = api.SourceFuncLW()
+    api.stop_on_err(src.alloc(4, 5, kd))
+    assert api.rte_lw(op, True, src, torch.ones((4, 16), device=dev), api.FluxesBroadband()) == \
+        "rte_lw: no space allocated for fluxes"
+    fl = api.FluxesBroadband(torch.empty((4, 6), device=dev))
+    assert "sfc_emis inconsistently sized" in api.rte_lw(op, True, src, torch.ones((4, 3), device=dev), fl)
+    assert "too many quadrature points" in api.rte_lw(op, True, src, torch.ones((4, 16), device=dev), fl,
+                                                      n_gauss_angles=5)
+    assert op.alloc_1scl(0, 5) != ""

@@ -1,0 +1,131 @@
+"""CPU tests of the host side: data files, problem builders, the C-ABI library's exports, and the
+column sharding used by the multi-GPU driver (gloo, world_size 2)."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rbin_roundtrip(tmp_path):
+    from rrtmgpnn import rbin
+    a = {"x": np.arange(12, dtype=np.float32).reshape(3, 4), "i": np.array([1, 2], np.int32),
+         "c": rbin.chars(["h2o", "o3"])}
+    p = str(tmp_path / "t.rbin")
+    rbin.write(p, a)
+    b = rbin.read(p)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    assert rbin.unchars(b["c"]) == ["h2o", "o3"]
+
+
+def test_models_have_reference_shapes():
+    from rrtmgpnn import data
+    shapes = {"lw_abs": [18, 58, 58, 256], "lw_pfrac": [18, 16, 16, 256], "sw_abs": [7, 16, 16, 224],
+              "sw_ray": [7, 16, 16, 224], "lw_g128_both": [18, 64, 64, 256]}
+    for k, dims in shapes.items():
+        m = data.load_model(k)
+        assert list(m["dims"]) == dims
+        assert list(m["activation"]) == [1, 1, 0]  # softsign, softsign, linear
+        for n in range(3):
+            assert m["w%d" % (n + 1)].shape == (dims[n], dims[n + 1])
+    assert "output_mean" not in data.load_model("lw_pfrac")
+
+
+def test_surrogate_planck_table_integrates_to_sigma_t4():
+    from rrtmgpnn import data
+    kd = data.load_kdist("lw")
+    T = 300.0
+    i = int(round((T - 160.0) / float(kd["totplnk_delta"])))
+    total = np.pi * kd["totplnk"][:, i].sum()
+    assert abs(total / (5.670374419e-8 * T ** 4) - 1.0) < 2e-3  # bands cover 10-3250 cm-1
+    assert kd["nPlanckTemp"] == 196 and kd["ngpt"] == 256 and kd["nband"] == 16
+    kds = data.load_kdist("sw")
+    assert kds["ngpt"] == 224 and kds["nband"] == 14
+
+
+def test_rfmip_problem_matches_driver_preprocessing(rfmip):
+    from rrtmgpnn import data
+    p = rfmip
+    assert p["ncol"] == 1800 and p["nlay"] == 60 and p["top_at_1"]
+    pmin = np.float32(data.load_kdist("lw")["press_ref_min"][0])
+    assert np.all(p["plev"][:, 0] == pmin + data.F32_EPS)            # rrtmgp_rfmip_lw.F90:300-305
+    assert np.all(p["play"] >= pmin)                                  # :287
+    assert np.all((p["mu0"] > 0) & (p["mu0"] <= 1))
+    assert p["usecol"].sum() == 918
+    toa = data.toa_flux(p, data.load_kdist("sw"))
+    np.testing.assert_allclose(toa.sum(1), p["tsi"], rtol=1e-5)         # rrtmgp_rfmip_sw.F90:408-427
+
+
+def test_synthetic_problem_ranges():
+    from rrtmgpnn import data
+    s = data.synthetic_problem(300, 137, seed=3)
+    assert s["play"].shape == (300, 137) and s["plev"].shape == (300, 138)
+    assert np.all(np.diff(s["plev"], axis=1) > 0)
+    assert s["tlay"].min() >= 160 and s["tlay"].max() <= 320.5
+    s2 = data.synthetic_problem(300, 137, seed=3)
+    np.testing.assert_array_equal(s["tlay"], s2["tlay"])  # seeded
+
+
+def _header_symbols():
+    with open(os.path.join(ROOT, "include", "rrtmgpnn.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"\b(rrtmgpnn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_c_abi_exports_every_header_symbol():
+    import ctypes
+    from rrtmgpnn import _lib
+    h = ctypes.CDLL(_lib.LIB_PATH)
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(h, s)]
+    assert not missing, missing
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes table out of sync with include/rrtmgpnn.h"
+
+
+def test_c_abi_errors_are_reported_not_crashed():
+    from rrtmgpnn import _lib
+    L = _lib.lib()
+    assert L.rrtmgpnn_version() == 1
+    h = _lib.c_vp()
+    rc = L.rrtmgpnn_context_create(-1, None, h)
+    assert rc != 0 and L.rrtmgpnn_last_error()
+    assert L.rrtmgpnn_lw_solver_noscat(None, 256, 60, 1, 1, 1, None, None, None, None, None, None, None, None, None,
+                                       None) != 0
+    assert b"null context" in L.rrtmgpnn_last_error()
+
+
+def _shard_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from rrtmgpnn import shard
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    ncol = 1001
+    lo, hi = shard.column_range(ncol, rank, world)
+    local = torch.arange(lo, hi, dtype=torch.float32)[:, None].repeat(1, 3)
+    full = shard.gather_columns(local, ncol, world)
+    q.put((rank, lo, hi, bool(torch.equal(full[:, 0], torch.arange(ncol, dtype=torch.float32)))))
+    dist.destroy_process_group()
+
+
+def test_column_sharding_gloo_world2():
+    import socket
+
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 1001
+    assert res[0][3] and res[1][3]
