@@ -44,7 +44,8 @@ typedef struct rrtmgpnn_network rrtmgpnn_network;
 /* ---- runtime ------------------------------------------------------------------------------ */
 int         rrtmgpnn_version(void);
 const char *rrtmgpnn_last_error(void);
-/* Creates a context on `device`; hip_stream may be NULL (a private non-blocking stream is made). */
+/* Creates a context on `device` that enqueues on `hip_stream` (a hipStream_t; NULL = the legacy default
+ * stream, ordered with every other default-stream operation). */
 int rrtmgpnn_context_create(int device, void *hip_stream, rrtmgpnn_context **ctx);
 int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream);

@@ -160,16 +160,7 @@ int rrtmgpnn_context_create(int device, void *hip_stream, rrtmgpnn_context **ctx
   c->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
-  if (hip_stream) {
-    c->stream = (hipStream_t)hip_stream;
-  } else {
-    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-      delete c;
-      return fail(RRTMGPNN_ERR_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
-    }
-    c->own_stream = true;
-  }
+  c->stream = (hipStream_t)hip_stream;  // NULL = the device's default (null) stream
   *ctx = c;
   return RRTMGPNN_OK;
 }

@@ -27,6 +27,7 @@
 //   layer feeds unit 16m + 4t + q from lane group q, i.e. every dot product is accumulated in
 //   ascending k order -- bit-identical to a sequential fmaf chain (the oracle's order).
 #include "internal.hpp"
+#include "libm_ref.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -52,7 +53,7 @@ __global__ void nn_inputs_kernel(int ncol, int nlay, int nx, const float *__rest
   int ilay = (int)(s % nlay);
   float *o = out + (size_t)nx * s;
   o[0] = (tlay[s] - sc.mn[0]) / (sc.mx[0] - sc.mn[0]);
-  o[1] = (logf(play[s]) - sc.mn[1]) / (sc.mx[1] - sc.mn[1]);
+  o[1] = (ref_logf(play[s]) - sc.mn[1]) / (sc.mx[1] - sc.mn[1]);
   o[2] = (sqrtf(sqrtf(gas.p[2][s])) - sc.mn[2]) / (sc.mx[2] - sc.mn[2]);
   o[3] = (sqrtf(sqrtf(gas.p[3][s])) - sc.mn[3]) / (sc.mx[3] - sc.mn[3]);
   for (int k = 4; k < nx; k++) {
@@ -142,10 +143,10 @@ __device__ __forceinline__ float activate(int act, float x)
   switch (act) {
   case RRTMGPNN_ACT_SOFTSIGN: return x / (fabsf(x) + 1.0f);
   case RRTMGPNN_ACT_RELU: return fmaxf(0.0f, x);
-  case RRTMGPNN_ACT_SIGMOID: return 1.0f / (1.0f + expf(-x));
+  case RRTMGPNN_ACT_SIGMOID: return 1.0f / (1.0f + ref_expf(-x));
   case RRTMGPNN_ACT_HARD_SIGMOID: return fmaxf(0.0f, fminf(1.0f, 0.2f * x + 0.5f));
   case 5: return tanhf(x);
-  case 6: return expf(-x * x);
+  case 6: return ref_expf(-x * x);
   default: return x;
   }
 }

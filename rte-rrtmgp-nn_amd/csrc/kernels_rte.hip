@@ -9,6 +9,7 @@
 //  * lw_noscat_kernel     : lw_solver_noscat[_GaussQuad] (rte/kernels/mo_rte_solver_kernels.F90:119-415)
 //  * sw_2stream kernels   : sw_solver_2stream + sw_two_stream_source + adding (:541-692, :1366-1637)
 #include "internal.hpp"
+#include "libm_ref.hpp"
 
 #include <algorithm>
 #include <cfloat>
@@ -89,11 +90,47 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 }
 
 // ------------------------------------------------------------------------------------------
-// LW no-scattering solver.  block = one column, lane = g-point.  Down pass stores nothing: the up
-// pass re-reads tau/lay/lev for its layer (L2/MALL-hot) and recomputes trans and the source, which
-// are bitwise identical to the down pass' values.  Source indexing follows lw_source_noscat
+// Ordered broadband reduction.  The reference sums g-points into 4 interleaved partial sums,
+// partial j accumulating g = j, j+4, j+8, ... in increasing g, then ((p0+p1)+p2)+p3
+// (rte/kernels/mo_rte_solver_kernels.F90:296-318 LW, :643-686 SW).  A float32 tree reduction
+// differs from that by several ulp of the broadband flux (~1e-3 W/m2 at SW magnitudes), so the
+// kernels reproduce the reference's order exactly: each level's per-g values are staged in an
+// LDS ring of kRing levels; when it fills, 4*kRing*NQ threads each walk one (quantity, level,
+// partial) sequentially.  Deterministic and order-identical to the reference.
+// ------------------------------------------------------------------------------------------
+static constexpr int kRing = 8;
+
+// Flush `nfill` staged levels.  ring: [nq][kRing][ngpt]; part: [nq][nlev][4]; slot_lev[c] = level.
+// dn_mode (SW): quantity 1 is accumulated as (s + ring1) + ring2, i.e. sums_dn + radn_dn + radn_dir.
+__device__ __forceinline__ void ring_flush(const float *ring, float *part, const int *slot_lev, int nq, int nfill,
+                                           int ngpt, int nlev, bool accumulate, bool dn_mode)
+{
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < nq * nfill * 4) {
+    const int q = t / (nfill * 4), c = (t >> 2) % nfill, j = t & 3;
+    const float *r = ring + ((size_t)q * kRing + c) * ngpt;
+    const float *r2 = ring + ((size_t)2 * kRing + c) * ngpt;
+    float s = 0.0f;
+    if (dn_mode && q == 1) {
+      for (int i = j; i < ngpt; i += 4) s = (s + r[i]) + r2[i];
+    } else {
+      for (int i = j; i < ngpt; i += 4) s = s + r[i];
+    }
+    float *p = part + ((size_t)q * nlev + slot_lev[c]) * 4 + j;
+    *p = accumulate ? *p + s : s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]) + p[2]) + p[3]; }
+
+// ------------------------------------------------------------------------------------------
+// LW no-scattering solver.  block = one column, lane = g-point.  The down pass stores nothing: the
+// up pass re-reads tau/lay/lev for its layer (L2/MALL-hot) and recomputes trans and the source,
+// bitwise identical to the down pass' values.  Source indexing follows lw_source_noscat
 // (:742-776): source_dn uses lev(l+1), source_up uses lev(l) for EVERY orientation (quirk B-1).
-// LDS: part[wave][2][nlay+1] per-wave partial sums.
+// LDS: ring [kRing][ngpt], part [2][nlev][4], slot_lev [kRing].
 // ------------------------------------------------------------------------------------------
 struct LwAngles {
   float D[4], w[4];
@@ -106,76 +143,76 @@ __global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwA
                                  const float *__restrict__ emis, const float *__restrict__ sfc,
                                  float *__restrict__ flux_up, float *__restrict__ flux_dn)
 {
-  extern __shared__ float part[];
-  const int icol = blockIdx.x, g = threadIdx.x, lane = g & 63, wave = g >> 6, nw = blockDim.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
   const int nlev = nlay + 1;
+  float *ring = smem;                            // [kRing][ngpt]
+  float *part = ring + (size_t)kRing * ngpt;     // [2][nlev][4]: 0 = dn, 1 = up
+  int *slot_lev = (int *)(part + (size_t)2 * nlev * 4);
   const float tau_thresh = sqrtf(FLT_EPSILON);
   const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
-  float *pd = part + (size_t)wave * 2 * nlev, *pu = pd + nlev;
-  for (int l = lane; l < nlev; l += 64) { pd[l] = 0.0f; pu[l] = 0.0f; }
   const float e = on ? emis[g + (size_t)ngpt * icol] : 0.0f;
   const float ss = on ? sfc[g + (size_t)ngpt * icol] : 0.0f;
   const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
+  int nfill = 0;
+  auto stage = [&](float v, int level, float *pq, bool acc) {
+    if (on) ring[(size_t)nfill * ngpt + g] = v;
+    if (g == 0) slot_lev[nfill] = level;
+    if (++nfill == kRing) {
+      ring_flush(ring, pq, slot_lev, 1, nfill, ngpt, nlev, acc, false);
+      nfill = 0;
+    }
+  };
+  auto drain = [&](float *pq, bool acc) {
+    if (nfill) ring_flush(ring, pq, slot_lev, 1, nfill, ngpt, nlev, acc, false);
+    nfill = 0;
+  };
+  float *pdn = part, *pup = part + (size_t)nlev * 4;
 
   for (int imu = 0; imu < ang.nmus; imu++) {
     const float D = ang.D[imu], fac = 2.0f * kPi * ang.w[imu];
+    const bool acc = imu > 0;
     float I = inc / (2.0f * kPi * ang.w[imu]);
-    {
-      float s = wave_sum(on ? fac * I : 0.0f);
-      if (lane == 0) pd[top] += s;
-    }
+    stage(fac * I, top, pdn, acc);
     // downward: lw_transport_noscat_dn (:982-1009)
     for (int j = 0; j < nlay; j++) {
       const int l = top_at_1 ? j : nlay - 1 - j;
-      float Inext = 0.0f;
       if (on) {
         const size_t i = (size_t)g + (size_t)ngpt * l;
         float t = tau[cl + i] * D;
-        float T = expf(-t);
+        float T = ref_expf(-t);
         float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
         float lvdn = lev[cv + i + ngpt], ly = lay[cl + i];
         float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
-        Inext = T * I + S;
+        I = T * I + S;
       }
-      I = Inext;
-      float s = wave_sum(on ? fac * I : 0.0f);
-      if (lane == 0) pd[top_at_1 ? l + 1 : l] += s;
+      stage(fac * I, top_at_1 ? l + 1 : l, pdn, acc);
     }
+    drain(pdn, acc);
     // surface reflection and emission (:269)
     float U = I * (1.0f - e) + e * ss;
-    {
-      float s = wave_sum(on ? fac * U : 0.0f);
-      if (lane == 0) pu[sfcl] += s;
-    }
+    stage(fac * U, sfcl, pup, acc);
     // upward: lw_transport_noscat_up (:950-980)
     for (int j = 0; j < nlay; j++) {
       const int l = top_at_1 ? nlay - 1 - j : j;
-      float Unext = 0.0f;
       if (on) {
         const size_t i = (size_t)g + (size_t)ngpt * l;
         float t = tau[cl + i] * D;
-        float T = expf(-t);
+        float T = ref_expf(-t);
         float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
         float lvup = lev[cv + i], ly = lay[cl + i];
         float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
-        Unext = T * U + S;
+        U = T * U + S;
       }
-      U = Unext;
-      float s = wave_sum(on ? fac * U : 0.0f);
-      if (lane == 0) pu[top_at_1 ? l : l + 1] += s;
+      stage(fac * U, top_at_1 ? l : l + 1, pup, acc);
     }
+    drain(pup, acc);
   }
-  __syncthreads();
   for (int l = g; l < nlev; l += blockDim.x) {
-    float su = 0.0f, sd = 0.0f;
-    for (int w = 0; w < nw; w++) {
-      sd += part[(size_t)w * 2 * nlev + l];
-      su += part[(size_t)w * 2 * nlev + nlev + l];
-    }
-    flux_up[l + (size_t)nlev * icol] = su;
-    flux_dn[l + (size_t)nlev * icol] = sd;
+    flux_dn[l + (size_t)nlev * icol] = combine4(pdn + 4 * l);
+    flux_up[l + (size_t)nlev * icol] = combine4(pup + 4 * l);
   }
 }
 
@@ -191,7 +228,7 @@ int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
   a.nmus = nmus;
   for (int i = 0; i < nmus; i++) { a.D[i] = Ds[i]; a.w[i] = wts[i]; }
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * (size_t)(threads / 64) * 2 * (nlay + 1);
+  size_t lds = sizeof(float) * ((size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4) + sizeof(int) * kRing;
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many layers for LDS partials");
   hipLaunchKernelGGL(lw_noscat_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a,
                      inc_flux, tau, lay_source, lev_source, sfc_emis, sfc_source, flux_up, flux_dn);
@@ -201,13 +238,14 @@ int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
 
 // ------------------------------------------------------------------------------------------
 // SW two-stream solver.  block = one column, lane = g-point.
-//   pass 1 (top->bottom): direct beam F_dir per level (stored), Sum_g F_dir -> flux_dir
+//   pass 1 (top->bottom): direct beam F_dir per level -> workspace
 //   pass 2 (bottom->top): sw_two_stream_source coefficients (Tnoscat recomputed bit-identically
 //          from tau and mu0), adding's albedo/src/denom (Shonk & Hogan Eqs 9-11); stores per level
-//          alpha, src and the downward recurrence coefficients a_l = Tdif*denom,
-//          b_l = (Rdif*src(below) + S_dn)*denom
-//   pass 3 (top->bottom): flux_dn(next) = a*flux_dn + b (Eq 13), flux_up = flux_dn*alpha + src (Eq 12)
-// Workspace ws: 4 arrays (ngpt, nlay+1, ncol): [F_dir -> alpha], src, a, b.
+//          alpha and src only
+//   pass 3 (top->bottom): recomputes the layer coefficients (same bits as pass 2: memory traffic is
+//          the bound, arithmetic is spare) and runs Eqs 12-13 with the reference's exact expression
+//          order; direct beam recomputed; ordered broadband sums of up, dif+dir, dir.
+// Workspace ws: 2 arrays (ngpt, nlay+1, ncol): [F_dir -> alpha], src.
 // ------------------------------------------------------------------------------------------
 struct SwCoef {
   float Rdif, Tdif, Sup, Sdn, Tnoscat;
@@ -217,7 +255,7 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
 {
   const float k_min = 1.e-4f, eps = FLT_EPSILON;
   SwCoef c;
-  float Tnoscat = expf(-tau * mu0_inv);
+  float Tnoscat = ref_expf(-tau * mu0_inv);
   float gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
   float gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
   float gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
@@ -225,7 +263,7 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
   float k = sqrtf(fmaxf((gamma1 - gamma2) * (gamma1 + gamma2), k_min));
-  float emk = expf(-tau * k);
+  float emk = ref_expf(-tau * k);
   float em2k = emk * emk;
   float k2e = 2.0f * k * emk;
   float RT = 1.0f / (k * (1.0f + em2k) + gamma1 * (1.0f - em2k));
@@ -253,36 +291,33 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
                                   const float *__restrict__ alb_dif, float *__restrict__ ws,
                                   float *__restrict__ flux_up, float *__restrict__ flux_dn, float *__restrict__ flux_dir)
 {
-  extern __shared__ float part[];
-  const int icol = blockIdx.x, g = threadIdx.x, lane = g & 63, wave = g >> 6, nw = blockDim.x >> 6;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
   const int nlev = nlay + 1;
+  float *ring = smem;                              // [3][kRing][ngpt]: up, dif, dir
+  float *part = ring + (size_t)3 * kRing * ngpt;   // [3][nlev][4]: up, dn, dir
+  int *slot_lev = (int *)(part + (size_t)3 * nlev * 4);
   const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
   const size_t plane = (size_t)ngpt * nlev * ncol;
-  float *wA = ws + cv, *wS = ws + plane + cv, *wa = ws + 2 * plane + cv, *wb = ws + 3 * plane + cv;
-  float *pu = part + (size_t)wave * 3 * nlev, *pd = pu + nlev, *pr = pd + nlev;
+  float *wA = ws + cv, *wS = ws + plane + cv;
   const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
-  // level index helpers: "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
+  // "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
   auto lev_above = [&](int l) { return top_at_1 ? l : l + 1; };
   auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
+  const float Ftop = on ? inc_flux[g + (size_t)ngpt * icol] * mu0 : 0.0f;
 
   // ---- pass 1: direct beam ----
-  float Fd = on ? inc_flux[g + (size_t)ngpt * icol] * mu0 : 0.0f;
-  if (on) wA[(size_t)g + (size_t)ngpt * top] = Fd;
-  {
-    float s = wave_sum(Fd);
-    if (lane == 0) pr[top] = s;
-  }
-  for (int j = 0; j < nlay; j++) {
-    const int l = top_at_1 ? j : nlay - 1 - j;
-    if (on) {
-      float Tn = expf(-tau[cl + (size_t)g + (size_t)ngpt * l] * mu0_inv);
+  float Fd = Ftop;
+  if (on) {
+    wA[(size_t)g + (size_t)ngpt * top] = Fd;
+    for (int j = 0; j < nlay; j++) {
+      const int l = top_at_1 ? j : nlay - 1 - j;
+      float Tn = ref_expf(-tau[cl + (size_t)g + (size_t)ngpt * l] * mu0_inv);
       Fd = Tn * Fd;
       wA[(size_t)g + (size_t)ngpt * lev_below(l)] = Fd;
     }
-    float s = wave_sum(on ? Fd : 0.0f);
-    if (lane == 0) pr[lev_below(l)] = s;
   }
   // ---- pass 2: bottom -> top adding (albedo, src) ----
   float alb_b = on ? alb_dif[g + (size_t)ngpt * icol] : 0.0f;  // albedo at the level below
@@ -290,55 +325,59 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
   if (on) {
     wA[(size_t)g + (size_t)ngpt * sfcl] = alb_b;
     wS[(size_t)g + (size_t)ngpt * sfcl] = src_b;
+    for (int j = 0; j < nlay; j++) {
+      const int l = top_at_1 ? nlay - 1 - j : j;
+      const size_t i = (size_t)g + (size_t)ngpt * l;
+      const size_t ia = (size_t)g + (size_t)ngpt * lev_above(l);
+      float Fin = wA[ia];
+      SwCoef c = sw_two_stream(tau[cl + i], ssa[cl + i], gg[cl + i], mu0, mu0_inv, Fin);
+      float denom = 1.0f / (1.0f - c.Rdif * alb_b);
+      float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
+      float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+      wA[ia] = alb;
+      wS[ia] = src;
+      alb_b = alb;
+      src_b = src;
+    }
   }
-  for (int j = 0; j < nlay; j++) {
-    const int l = top_at_1 ? nlay - 1 - j : j;
-    if (!on) continue;
-    const size_t i = (size_t)g + (size_t)ngpt * l;
-    const size_t ia = (size_t)g + (size_t)ngpt * lev_above(l);
-    float Fin = wA[ia];
-    SwCoef c = sw_two_stream(tau[cl + i], ssa[cl + i], gg[cl + i], mu0, mu0_inv, Fin);
-    float denom = 1.0f / (1.0f - c.Rdif * alb_b);
-    float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
-    float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
-    // coefficients of flux_dn(below) = a * flux_dn(above) + b  (Eq 13)
-    wa[(size_t)g + (size_t)ngpt * l] = c.Tdif * denom;
-    wb[(size_t)g + (size_t)ngpt * l] = (c.Rdif * src_b + c.Sdn) * denom;
-    wA[ia] = alb;
-    wS[ia] = src;
-    alb_b = alb;
-    src_b = src;
-  }
-  // ---- pass 3: top -> bottom fluxes ----
+  // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
+  int nfill = 0;
+  auto stage = [&](float up, float dif, float dir, int level) {
+    if (on) {
+      ring[(size_t)nfill * ngpt + g] = up;
+      ring[((size_t)kRing + nfill) * ngpt + g] = dif;
+      ring[((size_t)2 * kRing + nfill) * ngpt + g] = dir;
+    }
+    if (g == 0) slot_lev[nfill] = level;
+    if (++nfill == kRing) {
+      ring_flush(ring, part, slot_lev, 3, nfill, ngpt, nlev, false, true);
+      nfill = 0;
+    }
+  };
   float Fdn = (on && inc_dif) ? inc_dif[g + (size_t)ngpt * icol] : 0.0f;
-  {
-    float up = on ? Fdn * alb_b + src_b : 0.0f;  // alb_b/src_b now hold the top level's values
-    float su = wave_sum(up), sd = wave_sum(on ? Fdn : 0.0f);
-    if (lane == 0) { pu[top] = su; pd[top] = sd; }
-  }
+  Fd = Ftop;
+  stage(Fdn * alb_b + src_b, Fdn, Fd, top);  // Eq 12 at the top; alb_b/src_b hold the top level's values
   for (int j = 0; j < nlay; j++) {
     const int l = top_at_1 ? j : nlay - 1 - j;
     float up = 0.0f;
     if (on) {
+      // recompute the layer's coefficients exactly as pass 2 did (same inputs, same F_dir -> same bits)
+      const size_t i = (size_t)g + (size_t)ngpt * l;
       const size_t ib = (size_t)g + (size_t)ngpt * lev_below(l);
-      Fdn = wa[(size_t)g + (size_t)ngpt * l] * Fdn + wb[(size_t)g + (size_t)ngpt * l];
-      up = Fdn * wA[ib] + wS[ib];
+      SwCoef c = sw_two_stream(tau[cl + i], ssa[cl + i], gg[cl + i], mu0, mu0_inv, Fd);
+      const float alb = wA[ib], src = wS[ib];
+      const float denom = 1.0f / (1.0f - c.Rdif * alb);
+      Fdn = (c.Tdif * Fdn + c.Rdif * src + c.Sdn) * denom;  // Eq 13 (adding :1583-1591)
+      up = Fdn * alb + src;                                  // Eq 12
+      Fd = c.Tnoscat * Fd;
     }
-    float su = wave_sum(up), sd = wave_sum(on ? Fdn : 0.0f);
-    if (lane == 0) { pu[lev_below(l)] = su; pd[lev_below(l)] = sd; }
+    stage(up, Fdn, Fd, lev_below(l));
   }
-  __syncthreads();
+  if (nfill) ring_flush(ring, part, slot_lev, 3, nfill, ngpt, nlev, false, true);
   for (int l = g; l < nlev; l += blockDim.x) {
-    float su = 0.0f, sd = 0.0f, sr = 0.0f;
-    for (int w = 0; w < nw; w++) {
-      const float *p = part + (size_t)w * 3 * nlev;
-      su += p[l];
-      sd += p[nlev + l];
-      sr += p[2 * nlev + l];
-    }
-    flux_up[l + (size_t)nlev * icol] = su;
-    flux_dn[l + (size_t)nlev * icol] = sd + sr;  // total = diffuse + direct
-    flux_dir[l + (size_t)nlev * icol] = sr;
+    flux_up[l + (size_t)nlev * icol] = combine4(part + 4 * l);
+    flux_dn[l + (size_t)nlev * icol] = combine4(part + (size_t)nlev * 4 + 4 * l);
+    flux_dir[l + (size_t)nlev * icol] = combine4(part + (size_t)2 * nlev * 4 + 4 * l);
   }
 }
 
@@ -349,10 +388,10 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: ngpt > 1024");
   void *ws = nullptr;
-  int rc = ctx->workspace(sizeof(float) * 4 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
+  int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
   if (rc) return rc;
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * (size_t)(threads / 64) * 3 * (nlay + 1);
+  size_t lds = sizeof(float) * ((size_t)3 * kRing * ngpt + (size_t)3 * (nlay + 1) * 4) + sizeof(int) * kRing;
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
   hipLaunchKernelGGL(sw_2stream_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1,
                      inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, (float *)ws, flux_up, flux_dn,
