@@ -19,6 +19,14 @@ namespace rrtmgpnn {
 
 static constexpr float kPi = 3.14159265358979323846f;
 
+// Ablation switches for tools/ablate_solvers.sh (never set in the product build): they break parity
+// on purpose to attribute solver time.  RRTMGPNN_ABL_NATIVE_EXP: device expf instead of ref_expf;
+// RRTMGPNN_ABL_NO_REDUCE: skip the ordered broadband reduction (barriers kept);
+// RRTMGPNN_ABL_NO_BARRIER: skip staging and flushing entirely.
+#ifdef RRTMGPNN_ABL_NATIVE_EXP
+#define ref_expf_tab(x, t) __expf(x)
+#endif
+
 __device__ __forceinline__ float wave_sum(float v)
 {
 #pragma unroll
@@ -48,30 +56,42 @@ __device__ __forceinline__ int band_of(const BandArgs &b, int g)
   return 0;
 }
 
+constexpr int kPlanckLayers = 4;  // layers per block: independent loads in flight per lane
+
 __global__ void planck_source_kernel(int ncol, int nlay, int ngpt, int ntemp, const float *__restrict__ tlay,
                                      const float *__restrict__ tlev, const float *__restrict__ tsfc, int sfc_lay,
                                      BandArgs bands, float tmin, float tdelta, const float *__restrict__ totplnk,
                                      float *__restrict__ sfc_src, float *__restrict__ sfc_jac, float *__restrict__ pfrac,
                                      float *__restrict__ lev_src)
 {
-  const int ilay = blockIdx.x, icol = blockIdx.y, g = threadIdx.x;
+  const int l0 = blockIdx.x * kPlanckLayers, icol = blockIdx.y, g = threadIdx.x;
   if (g >= ngpt) return;
   const int b = band_of(bands, g);
   const float *tab = totplnk + (size_t)ntemp * b;
-  const size_t il = (size_t)g + (size_t)ngpt * (ilay + (size_t)nlay * icol);
-  const size_t iv = (size_t)g + (size_t)ngpt * (ilay + (size_t)(nlay + 1) * icol);
-  const float pf = pfrac[il];
   const float *tl = tlev + (size_t)(nlay + 1) * icol;
-  lev_src[iv] = pf * interp1d(tl[ilay], tmin, tdelta, ntemp, tab);
-  if (ilay == nlay - 1) lev_src[iv + ngpt] = pf * interp1d(tl[nlay], tmin, tdelta, ntemp, tab);
-  if (ilay == sfc_lay - 1) {
-    float ts = tsfc[icol];
-    float ps = interp1d(ts, tmin, tdelta, ntemp, tab);
-    float pj = interp1d(ts + 1.0f, tmin, tdelta, ntemp, tab);
-    sfc_src[g + (size_t)ngpt * icol] = pf * ps;
-    sfc_jac[g + (size_t)ngpt * icol] = pf * (pj - ps);
+  float pf[kPlanckLayers];
+#pragma unroll
+  for (int k = 0; k < kPlanckLayers; k++) {
+    const int ilay = min(l0 + k, nlay - 1);
+    pf[k] = pfrac[(size_t)g + (size_t)ngpt * (ilay + (size_t)nlay * icol)];
   }
-  pfrac[il] = pf * interp1d(tlay[ilay + (size_t)nlay * icol], tmin, tdelta, ntemp, tab);
+#pragma unroll
+  for (int k = 0; k < kPlanckLayers; k++) {
+    const int ilay = l0 + k;
+    if (ilay >= nlay) break;
+    const size_t il = (size_t)g + (size_t)ngpt * (ilay + (size_t)nlay * icol);
+    const size_t iv = (size_t)g + (size_t)ngpt * (ilay + (size_t)(nlay + 1) * icol);
+    lev_src[iv] = pf[k] * interp1d(tl[ilay], tmin, tdelta, ntemp, tab);
+    if (ilay == nlay - 1) lev_src[iv + ngpt] = pf[k] * interp1d(tl[nlay], tmin, tdelta, ntemp, tab);
+    if (ilay == sfc_lay - 1) {
+      float ts = tsfc[icol];
+      float ps = interp1d(ts, tmin, tdelta, ntemp, tab);
+      float pj = interp1d(ts + 1.0f, tmin, tdelta, ntemp, tab);
+      sfc_src[g + (size_t)ngpt * icol] = pf[k] * ps;
+      sfc_jac[g + (size_t)ngpt * icol] = pf[k] * (pj - ps);
+    }
+    pfrac[il] = pf[k] * interp1d(tlay[ilay + (size_t)nlay * icol], tmin, tdelta, ntemp, tab);
+  }
 }
 
 int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ntemp, const float *tlay,
@@ -82,7 +102,7 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
   if (ncol == 0 || nlay == 0) return RRTMGPNN_OK;
   if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "planck source: ngpt > 1024");
   int threads = (ngpt + 63) / 64 * 64;
-  hipLaunchKernelGGL(planck_source_kernel, dim3(nlay, ncol), dim3(threads), 0, ctx->stream, ncol, nlay, ngpt, ntemp,
+  hipLaunchKernelGGL(planck_source_kernel, dim3((nlay + kPlanckLayers - 1) / kPlanckLayers, ncol), dim3(threads), 0, ctx->stream, ncol, nlay, ngpt, ntemp,
                      tlay, tlev, tsfc, sfc_lay, bands, temp_ref_min, totplnk_delta, totplnk, sfc_source,
                      sfc_source_Jac, pfrac, lev_source);
   RRTMGPNN_LAUNCH_CHECK("planck_source_kernel");
@@ -99,26 +119,52 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 // partial) sequentially.  Deterministic and order-identical to the reference.
 // ------------------------------------------------------------------------------------------
 static constexpr int kRing = 8;
+static constexpr int kPF = 4;
+static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS  // layers of inputs kept in flight per lane (software prefetch)
 
 // Flush `nfill` staged levels.  ring: [nq][kRing][ngpt]; part: [nq][nlev][4]; slot_lev[c] = level.
+// One thread per (quantity, level) walks the level's g-points with 16-byte LDS reads: element k of
+// the float4 at m is g = 4m + k, so the 4 interleaved partials advance together, each in g order.
 // dn_mode (SW): quantity 1 is accumulated as (s + ring1) + ring2, i.e. sums_dn + radn_dn + radn_dir.
+// ngpt % 4 != 0: the reference uses sum(radn, 1) instead (one sequential sum, kept in partial 0).
 __device__ __forceinline__ void ring_flush(const float *ring, float *part, const int *slot_lev, int nq, int nfill,
                                            int ngpt, int nlev, bool accumulate, bool dn_mode)
 {
   __syncthreads();
   const int t = threadIdx.x;
-  if (t < nq * nfill * 4) {
-    const int q = t / (nfill * 4), c = (t >> 2) % nfill, j = t & 3;
+#ifdef RRTMGPNN_ABL_NO_REDUCE
+  if (false) {
+#else
+  if (t < nq * nfill) {
+#endif
+    const int q = t / nfill, c = t % nfill;
     const float *r = ring + ((size_t)q * kRing + c) * ngpt;
     const float *r2 = ring + ((size_t)2 * kRing + c) * ngpt;
-    float s = 0.0f;
-    if (dn_mode && q == 1) {
-      for (int i = j; i < ngpt; i += 4) s = (s + r[i]) + r2[i];
+    const bool dn = dn_mode && q == 1;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    if ((ngpt & 3) == 0) {
+      const float4 *r4 = (const float4 *)r, *q4 = (const float4 *)r2;
+      const int n4 = ngpt >> 2;
+      if (dn) {
+#pragma unroll 4
+        for (int m = 0; m < n4; m++) {
+          const float4 a = r4[m], b = q4[m];
+          s0 = (s0 + a.x) + b.x; s1 = (s1 + a.y) + b.y; s2 = (s2 + a.z) + b.z; s3 = (s3 + a.w) + b.w;
+        }
+      } else {
+#pragma unroll 4
+        for (int m = 0; m < n4; m++) {
+          const float4 a = r4[m];
+          s0 = s0 + a.x; s1 = s1 + a.y; s2 = s2 + a.z; s3 = s3 + a.w;
+        }
+      }
     } else {
-      for (int i = j; i < ngpt; i += 4) s = s + r[i];
+      if (dn) for (int i = 0; i < ngpt; i++) s0 = s0 + (r[i] + r2[i]);  // radn_dn = radn_dn + radn_dir; sum
+      else    for (int i = 0; i < ngpt; i++) s0 = s0 + r[i];
     }
-    float *p = part + ((size_t)q * nlev + slot_lev[c]) * 4 + j;
-    *p = accumulate ? *p + s : s;
+    float *p = part + ((size_t)q * nlev + slot_lev[c]) * 4;
+    if (accumulate) { p[0] += s0; p[1] += s1; p[2] += s2; p[3] += s3; }
+    else { p[0] = s0; p[1] = s1; p[2] = s2; p[3] = s3; }
   }
   __syncthreads();
 }
@@ -141,15 +187,23 @@ __global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwA
                                  const float *__restrict__ inc_flux, const float *__restrict__ tau,
                                  const float *__restrict__ lay, const float *__restrict__ lev,
                                  const float *__restrict__ emis, const float *__restrict__ sfc,
-                                 float *__restrict__ flux_up, float *__restrict__ flux_dn)
+                                 float *__restrict__ ws, float *__restrict__ flux_up, float *__restrict__ flux_dn)
 {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
+  const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
   const int nlev = nlay + 1;
-  float *ring = smem;                            // [kRing][ngpt]
+  // nmus > 1 (lw_solver_noscat_GaussQuad :383-412): g-point fluxes are summed over angles first, then
+  // reduced with sum_broadband's plain sequential sum; ws holds the per-g accumulators (2, nlev, ngpt).
+  const bool multi = ang.nmus > 1;
+  float *wcol = multi ? ws + (size_t)2 * nlev * ngpt * icol : nullptr;
+  float *ring = smem + kExpTabFloats;            // [kRing][ngpt]
   float *part = ring + (size_t)kRing * ngpt;     // [2][nlev][4]: 0 = dn, 1 = up
   int *slot_lev = (int *)(part + (size_t)2 * nlev * 4);
+  uint64_t *etab = (uint64_t *)(smem + kExpTabOff);  // 16-byte aligned slot at the front
+  load_exp_table(etab);
+  __syncthreads();
   const float tau_thresh = sqrtf(FLT_EPSILON);
   const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
   const float e = on ? emis[g + (size_t)ngpt * icol] : 0.0f;
@@ -158,57 +212,115 @@ __global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwA
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   int nfill = 0;
   auto stage = [&](float v, int level, float *pq, bool acc) {
+    if (multi) {
+      if (on) {
+        float *w = wcol + (size_t)(pq == part ? 0 : nlev) * ngpt + (size_t)level * ngpt + g;
+        *w = acc ? *w + v : v;
+      }
+      return;
+    }
     if (on) ring[(size_t)nfill * ngpt + g] = v;
     if (g == 0) slot_lev[nfill] = level;
+#ifdef RRTMGPNN_ABL_NO_BARRIER
+    return;
+#endif
     if (++nfill == kRing) {
       ring_flush(ring, pq, slot_lev, 1, nfill, ngpt, nlev, acc, false);
       nfill = 0;
     }
   };
   auto drain = [&](float *pq, bool acc) {
+    if (multi) return;
     if (nfill) ring_flush(ring, pq, slot_lev, 1, nfill, ngpt, nlev, acc, false);
     nfill = 0;
   };
   float *pdn = part, *pup = part + (size_t)nlev * 4;
 
   for (int imu = 0; imu < ang.nmus; imu++) {
-    const float D = ang.D[imu], fac = 2.0f * kPi * ang.w[imu];
+    const float D = ang.D[imu];
+    // radiance -> flux factor inside the broadband sum; with nmus == 1 and ngpt % 4 != 0 the reference
+    // sums plain radiances (quirk B-5, mo_rte_solver_kernels.F90:287-320)
+    const float fac = (multi || (ngpt & 3) == 0) ? 2.0f * kPi * ang.w[imu] : 1.0f;
     const bool acc = imu > 0;
     float I = inc / (2.0f * kPi * ang.w[imu]);
     stage(fac * I, top, pdn, acc);
-    // downward: lw_transport_noscat_dn (:982-1009)
-    for (int j = 0; j < nlay; j++) {
-      const int l = top_at_1 ? j : nlay - 1 - j;
-      if (on) {
-        const size_t i = (size_t)g + (size_t)ngpt * l;
-        float t = tau[cl + i] * D;
-        float T = ref_expf(-t);
-        float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
-        float lvdn = lev[cv + i + ngpt], ly = lay[cl + i];
-        float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
-        I = T * I + S;
+    // downward: lw_transport_noscat_dn (:982-1009).  Inputs of layer step j+kPF are loaded while step
+    // j computes (loads are unconditional on clamped indices: no branch around a load).
+    {
+      float pt[kPF], py[kPF], pv[kPF];
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int l = top_at_1 ? min(p, nlay - 1) : max(nlay - 1 - p, 0);
+        const size_t i = (size_t)gc + (size_t)ngpt * l;
+        pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i + ngpt];
       }
-      stage(fac * I, top_at_1 ? l + 1 : l, pdn, acc);
+      for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+        for (int p = 0; p < kPF; p++) {
+          const int j = j0 + p;
+          if (j < nlay) {
+            const int l = top_at_1 ? j : nlay - 1 - j;
+            const float t = pt[p] * D, ly = py[p], lvdn = pv[p];
+            {
+              const int jn = min(j + kPF, nlay - 1), ln = top_at_1 ? jn : nlay - 1 - jn;
+              const size_t i = (size_t)gc + (size_t)ngpt * ln;
+              pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i + ngpt];
+            }
+            float T = ref_expf_tab(-t, etab);
+            float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+            float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
+            I = T * I + S;
+            stage(fac * I, top_at_1 ? l + 1 : l, pdn, acc);
+          }
+        }
+      }
     }
     drain(pdn, acc);
     // surface reflection and emission (:269)
     float U = I * (1.0f - e) + e * ss;
     stage(fac * U, sfcl, pup, acc);
     // upward: lw_transport_noscat_up (:950-980)
-    for (int j = 0; j < nlay; j++) {
-      const int l = top_at_1 ? nlay - 1 - j : j;
-      if (on) {
-        const size_t i = (size_t)g + (size_t)ngpt * l;
-        float t = tau[cl + i] * D;
-        float T = ref_expf(-t);
-        float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
-        float lvup = lev[cv + i], ly = lay[cl + i];
-        float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
-        U = T * U + S;
+    {
+      float pt[kPF], py[kPF], pv[kPF];
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int l = top_at_1 ? max(nlay - 1 - p, 0) : min(p, nlay - 1);
+        const size_t i = (size_t)gc + (size_t)ngpt * l;
+        pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i];
       }
-      stage(fac * U, top_at_1 ? l : l + 1, pup, acc);
+      for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+        for (int p = 0; p < kPF; p++) {
+          const int j = j0 + p;
+          if (j < nlay) {
+            const int l = top_at_1 ? nlay - 1 - j : j;
+            const float t = pt[p] * D, ly = py[p], lvup = pv[p];
+            {
+              const int jn = min(j + kPF, nlay - 1), ln = top_at_1 ? nlay - 1 - jn : jn;
+              const size_t i = (size_t)gc + (size_t)ngpt * ln;
+              pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i];
+            }
+            float T = ref_expf_tab(-t, etab);
+            float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+            float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
+            U = T * U + S;
+            stage(fac * U, top_at_1 ? l : l + 1, pup, acc);
+          }
+        }
+      }
     }
     drain(pup, acc);
+  }
+  if (multi) {
+    __syncthreads();
+    for (int t = g; t < 2 * nlev; t += blockDim.x) {
+      const float *w = wcol + (size_t)t * ngpt;
+      float s = 0.0f;
+      for (int i = 0; i < ngpt; i++) s = s + w[i];  // sum_broadband: sequential over g
+      const int l = t % nlev;
+      (t < nlev ? flux_dn : flux_up)[l + (size_t)nlev * icol] = s;
+    }
+    return;
   }
   for (int l = g; l < nlev; l += blockDim.x) {
     flux_dn[l + (size_t)nlev * icol] = combine4(pdn + 4 * l);
@@ -228,10 +340,15 @@ int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
   a.nmus = nmus;
   for (int i = 0; i < nmus; i++) { a.D[i] = Ds[i]; a.w[i] = wts[i]; }
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * ((size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4) + sizeof(int) * kRing;
+  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4) + sizeof(int) * kRing;
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many layers for LDS partials");
+  void *ws = nullptr;
+  if (nmus > 1) {
+    int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
+    if (rc) return rc;
+  }
   hipLaunchKernelGGL(lw_noscat_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a,
-                     inc_flux, tau, lay_source, lev_source, sfc_emis, sfc_source, flux_up, flux_dn);
+                     inc_flux, tau, lay_source, lev_source, sfc_emis, sfc_source, (float *)ws, flux_up, flux_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_noscat_kernel");
   return RRTMGPNN_OK;
 }
@@ -251,11 +368,12 @@ struct SwCoef {
   float Rdif, Tdif, Sup, Sdn, Tnoscat;
 };
 
-__device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, float mu0, float mu0_inv, float dir_inc)
+__device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, float mu0, float mu0_inv, float dir_inc,
+                                               const uint64_t *etab)
 {
   const float k_min = 1.e-4f, eps = FLT_EPSILON;
   SwCoef c;
-  float Tnoscat = ref_expf(-tau * mu0_inv);
+  float Tnoscat = ref_expf_tab(-tau * mu0_inv, etab);
   float gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
   float gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
   float gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
@@ -263,7 +381,7 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
   float k = sqrtf(fmaxf((gamma1 - gamma2) * (gamma1 + gamma2), k_min));
-  float emk = ref_expf(-tau * k);
+  float emk = ref_expf_tab(-tau * k, etab);
   float em2k = emk * emk;
   float k2e = 2.0f * k * emk;
   float RT = 1.0f / (k * (1.0f + em2k) + gamma1 * (1.0f - em2k));
@@ -295,7 +413,10 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
   const int nlev = nlay + 1;
-  float *ring = smem;                              // [3][kRing][ngpt]: up, dif, dir
+  float *ring = smem + kExpTabFloats;              // [3][kRing][ngpt]: up, dif, dir
+  uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
+  load_exp_table(etab);
+  __syncthreads();
   float *part = ring + (size_t)3 * kRing * ngpt;   // [3][nlev][4]: up, dn, dir
   int *slot_lev = (int *)(part + (size_t)3 * nlev * 4);
   const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
@@ -305,18 +426,31 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
   // "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
   auto lev_above = [&](int l) { return top_at_1 ? l : l + 1; };
   auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
+  auto lay_of_down = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };  // j-th layer from the top
+  auto lay_of_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };    // j-th layer from the surface
+  const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   const float Ftop = on ? inc_flux[g + (size_t)ngpt * icol] * mu0 : 0.0f;
 
-  // ---- pass 1: direct beam ----
+  // ---- pass 1: direct beam (only tau is read) ----
   float Fd = Ftop;
-  if (on) {
-    wA[(size_t)g + (size_t)ngpt * top] = Fd;
-    for (int j = 0; j < nlay; j++) {
-      const int l = top_at_1 ? j : nlay - 1 - j;
-      float Tn = ref_expf(-tau[cl + (size_t)g + (size_t)ngpt * l] * mu0_inv);
-      Fd = Tn * Fd;
-      wA[(size_t)g + (size_t)ngpt * lev_below(l)] = Fd;
+  if (on) wA[(size_t)g + (size_t)ngpt * top] = Fd;
+  {
+    float pt[kPF];
+#pragma unroll
+    for (int p = 0; p < kPF; p++) pt[p] = tau[cl + (size_t)gc + (size_t)ngpt * lay_of_down(min(p, nlay - 1))];
+    for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int j = j0 + p;
+        if (j < nlay) {
+          const int l = lay_of_down(j);
+          const float t = pt[p];
+          pt[p] = tau[cl + (size_t)gc + (size_t)ngpt * lay_of_down(min(j + kPF, nlay - 1))];
+          Fd = ref_expf_tab(-t * mu0_inv, etab) * Fd;
+          if (on) wA[(size_t)g + (size_t)ngpt * lev_below(l)] = Fd;
+        }
+      }
     }
   }
   // ---- pass 2: bottom -> top adding (albedo, src) ----
@@ -325,19 +459,39 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
   if (on) {
     wA[(size_t)g + (size_t)ngpt * sfcl] = alb_b;
     wS[(size_t)g + (size_t)ngpt * sfcl] = src_b;
-    for (int j = 0; j < nlay; j++) {
-      const int l = top_at_1 ? nlay - 1 - j : j;
-      const size_t i = (size_t)g + (size_t)ngpt * l;
-      const size_t ia = (size_t)g + (size_t)ngpt * lev_above(l);
-      float Fin = wA[ia];
-      SwCoef c = sw_two_stream(tau[cl + i], ssa[cl + i], gg[cl + i], mu0, mu0_inv, Fin);
-      float denom = 1.0f / (1.0f - c.Rdif * alb_b);
-      float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
-      float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
-      wA[ia] = alb;
-      wS[ia] = src;
-      alb_b = alb;
-      src_b = src;
+  }
+  {
+    float pt[kPF], pw[kPF], pg[kPF];
+#pragma unroll
+    for (int p = 0; p < kPF; p++) {
+      const size_t i = cl + (size_t)gc + (size_t)ngpt * lay_of_up(min(p, nlay - 1));
+      pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i];
+    }
+    for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int j = j0 + p;
+        if (j < nlay) {
+          const int l = lay_of_up(j);
+          const float t = pt[p], w0 = pw[p], g0 = pg[p];
+          {
+            const size_t i = cl + (size_t)gc + (size_t)ngpt * lay_of_up(min(j + kPF, nlay - 1));
+            pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i];
+          }
+          const size_t ia = (size_t)gc + (size_t)ngpt * lev_above(l);
+          const float Fin = wA[ia];
+          SwCoef c = sw_two_stream(t, w0, g0, mu0, mu0_inv, Fin, etab);
+          float denom = 1.0f / (1.0f - c.Rdif * alb_b);
+          float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
+          float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+          if (on) {
+            wA[ia] = alb;
+            wS[ia] = src;
+          }
+          alb_b = alb;
+          src_b = src;
+        }
+      }
     }
   }
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
@@ -349,6 +503,9 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
       ring[((size_t)2 * kRing + nfill) * ngpt + g] = dir;
     }
     if (g == 0) slot_lev[nfill] = level;
+#ifdef RRTMGPNN_ABL_NO_BARRIER
+    return;
+#endif
     if (++nfill == kRing) {
       ring_flush(ring, part, slot_lev, 3, nfill, ngpt, nlev, false, true);
       nfill = 0;
@@ -357,21 +514,36 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
   float Fdn = (on && inc_dif) ? inc_dif[g + (size_t)ngpt * icol] : 0.0f;
   Fd = Ftop;
   stage(Fdn * alb_b + src_b, Fdn, Fd, top);  // Eq 12 at the top; alb_b/src_b hold the top level's values
-  for (int j = 0; j < nlay; j++) {
-    const int l = top_at_1 ? j : nlay - 1 - j;
-    float up = 0.0f;
-    if (on) {
-      // recompute the layer's coefficients exactly as pass 2 did (same inputs, same F_dir -> same bits)
-      const size_t i = (size_t)g + (size_t)ngpt * l;
-      const size_t ib = (size_t)g + (size_t)ngpt * lev_below(l);
-      SwCoef c = sw_two_stream(tau[cl + i], ssa[cl + i], gg[cl + i], mu0, mu0_inv, Fd);
-      const float alb = wA[ib], src = wS[ib];
-      const float denom = 1.0f / (1.0f - c.Rdif * alb);
-      Fdn = (c.Tdif * Fdn + c.Rdif * src + c.Sdn) * denom;  // Eq 13 (adding :1583-1591)
-      up = Fdn * alb + src;                                  // Eq 12
-      Fd = c.Tnoscat * Fd;
+  {
+    float pt[kPF], pw[kPF], pg[kPF], pa[kPF], ps[kPF];
+#pragma unroll
+    for (int p = 0; p < kPF; p++) {
+      const int l = lay_of_down(min(p, nlay - 1));
+      const size_t i = cl + (size_t)gc + (size_t)ngpt * l, ib = (size_t)gc + (size_t)ngpt * lev_below(l);
+      pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i]; pa[p] = wA[ib]; ps[p] = wS[ib];
     }
-    stage(up, Fdn, Fd, lev_below(l));
+    for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int j = j0 + p;
+        if (j < nlay) {
+          const int l = lay_of_down(j);
+          const float t = pt[p], w0 = pw[p], g0 = pg[p], alb = pa[p], src = ps[p];
+          {
+            const int ln = lay_of_down(min(j + kPF, nlay - 1));
+            const size_t i = cl + (size_t)gc + (size_t)ngpt * ln, ib = (size_t)gc + (size_t)ngpt * lev_below(ln);
+            pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i]; pa[p] = wA[ib]; ps[p] = wS[ib];
+          }
+          // recompute the layer's coefficients exactly as pass 2 did (same inputs, same F_dir -> same bits)
+          SwCoef c = sw_two_stream(t, w0, g0, mu0, mu0_inv, Fd, etab);
+          const float denom = 1.0f / (1.0f - c.Rdif * alb);
+          Fdn = (c.Tdif * Fdn + c.Rdif * src + c.Sdn) * denom;  // Eq 13 (adding :1583-1591)
+          const float up = Fdn * alb + src;                      // Eq 12
+          Fd = c.Tnoscat * Fd;
+          stage(up, Fdn, Fd, lev_below(l));
+        }
+      }
+    }
   }
   if (nfill) ring_flush(ring, part, slot_lev, 3, nfill, ngpt, nlev, false, true);
   for (int l = g; l < nlev; l += blockDim.x) {
@@ -391,7 +563,7 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
   if (rc) return rc;
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * ((size_t)3 * kRing * ngpt + (size_t)3 * (nlay + 1) * 4) + sizeof(int) * kRing;
+  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRing * ngpt + (size_t)3 * (nlay + 1) * 4) + sizeof(int) * kRing;
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
   hipLaunchKernelGGL(sw_2stream_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1,
                      inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, (float *)ws, flux_up, flux_dn,

@@ -28,7 +28,9 @@ __device__ __constant__ static const uint64_t kExpTab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
-__device__ __forceinline__ float ref_expf(float x)
+// tab: the 32-entry table, in LDS in the hot kernels (a per-lane gather from __constant__ memory is a
+// vector memory load with L1/L2 latency; from LDS it is a ds_read_b64).
+__device__ __forceinline__ float ref_expf_tab(float x, const uint64_t *tab)
 {
   const double InvLn2N = 0x1.71547652b82fep+0 * 32, SHIFT = 0x1.8p+52;
   const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
@@ -46,11 +48,19 @@ __device__ __forceinline__ float ref_expf(float x)
   const uint64_t ki = f64_as_u64(kd);
   kd -= SHIFT;
   const double r = __fma_rn(InvLn2N, xd, -kd);
-  const double s = u64_as_f64(kExpTab[ki % 32] + (ki << 47));
+  const double s = u64_as_f64(tab[ki % 32] + (ki << 47));
   const double z = __fma_rn(C0, r, C1), r2 = r * r;
   double y = __fma_rn(C2, r, 1.0);
   y = __fma_rn(z, r2, y);
   return (float)(y * s);
+}
+
+__device__ __forceinline__ float ref_expf(float x) { return ref_expf_tab(x, kExpTab); }
+
+// Copy the exp table into LDS (call with all threads of the block; a __syncthreads() must follow).
+__device__ __forceinline__ void load_exp_table(uint64_t *lds_tab)
+{
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) lds_tab[i] = kExpTab[i];
 }
 
 struct LogTab {

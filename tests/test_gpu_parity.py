@@ -1,10 +1,13 @@
 """GPU parity: the HIP kernels (through the C ABI) against the oracle on the same inputs.
 
-Tolerances (float32 throughout, north star: <= 1e-3 W/m2 RMS flux error):
-  * MLP raw outputs: <= 2 ulp (the MFMA kernel accumulates every dot product in the oracle's k order)
-  * optical depths / sources: relative 2e-5 (libm vs device expf/logf/sqrtf differ by <= 1-2 ulp,
-    amplified 8x by the (.)^8 post-processing)
-  * broadband fluxes: RMS <= 1e-3 W/m2 and max abs <= 1e-2 W/m2
+Bar (float32 throughout): BIT-IDENTICAL to the oracle, which is itself bit-identical to the reference
+Fortran (rte_lw, rte_sw, MLP) -- see tests/test_oracle.py.  This holds because
+  * the MFMA MLP accumulates every dot product in the oracle's ascending-k fmaf order,
+  * device expf/logf reproduce glibc's algorithms exactly (csrc/libm_ref.hpp),
+  * broadband sums reproduce the reference's 4-way interleaved summation order,
+  * kernels and oracle are compiled with -ffp-contract=off.
+The north star's own bar (<= 1e-3 W/m2 RMS flux error) is asserted as well, as a floor that would still
+hold if a future libm or compiler changed the last bits.
 """
 import numpy as np
 import pytest
@@ -37,11 +40,13 @@ def rms(a, b):
     return float(np.sqrt(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2)))
 
 
-def assert_flux(got, ref, what):
+def assert_flux(got, ref, what, exact=True):
     if np.size(got) == 0 and np.size(ref) == 0:
         return
     r, m = rms(got, ref), float(np.max(np.abs(got - ref)))
     assert r <= 1e-3 and m <= 1e-2, "%s: RMS %.3g, max %.3g W/m2" % (what, r, m)
+    if exact:
+        np.testing.assert_array_equal(got, ref, err_msg=what + ": not bit-identical")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -54,7 +59,7 @@ def test_mlp_forward_matches_oracle(dev, orc, models, name, nbatch):
     x = rng.uniform(-0.2, 1.2, size=(nbatch, int(m["dims"][0]))).astype(np.float32)
     net = api.RrtmgpNetwork(0).load_netcdf(data.path(name))
     y = net.output_sgemm_flat(T(x, dev)).cpu().numpy()
-    np.testing.assert_array_max_ulp(y, orc.mlp(m, x), maxulp=2)
+    np.testing.assert_array_equal(y, orc.mlp(m, x))  # bit-identical MFMA chain
 
 
 def test_lw_gas_optics_matches_oracle(dev, orc, rfmip, models):
@@ -75,13 +80,11 @@ def test_lw_gas_optics_matches_oracle(dev, orc, rfmip, models):
     api.stop_on_err(src.alloc(ncol, nlay, kd))
     api.stop_on_err(kd.gas_optics(T(prob["play"], dev), T(prob["plev"], dev), T(prob["tlay"], dev),
                                   T(prob["tsfc"], dev), gc, op, src, tlev=T(prob["tlev"], dev), neural_nets=nets))
-    # |dtau| <= 2e-5 |tau| + 1e-6: device logf/sqrtf in compute_nn_inputs may differ by 1 ulp from glibc, and
-    # (std*y + mean) cancels for a few tiny-tau g-points; 1e-6 of optical depth is far below flux resolution
-    np.testing.assert_allclose(op.tau.cpu().numpy(), ref["tau"], rtol=2e-5, atol=1e-6)
-    np.testing.assert_allclose(src.lay_source.cpu().numpy(), ref["lay_source"], rtol=2e-5, atol=1e-12)
-    np.testing.assert_allclose(src.lev_source.cpu().numpy(), ref["lev_source"], rtol=2e-5, atol=1e-12)
-    np.testing.assert_allclose(src.sfc_source.cpu().numpy(), ref["sfc_source"], rtol=2e-5, atol=1e-12)
-    np.testing.assert_allclose(src.sfc_source_Jac.cpu().numpy(), ref["sfc_source_Jac"], rtol=2e-5, atol=1e-12)
+    np.testing.assert_array_equal(op.tau.cpu().numpy(), ref["tau"])
+    np.testing.assert_array_equal(src.lay_source.cpu().numpy(), ref["lay_source"])
+    np.testing.assert_array_equal(src.lev_source.cpu().numpy(), ref["lev_source"])
+    np.testing.assert_array_equal(src.sfc_source.cpu().numpy(), ref["sfc_source"])
+    np.testing.assert_array_equal(src.sfc_source_Jac.cpu().numpy(), ref["sfc_source_Jac"])
 
 
 def test_sw_gas_optics_matches_oracle(dev, orc, rfmip, models):
@@ -102,8 +105,8 @@ def test_sw_gas_optics_matches_oracle(dev, orc, rfmip, models):
     toa = torch.empty((ncol, kd.get_ngpt()), device=dev)
     api.stop_on_err(kd.gas_optics(T(prob["play"], dev), T(prob["plev"], dev), T(prob["tlay"], dev), gc, op, toa,
                                   neural_nets=nets))
-    np.testing.assert_allclose(op.tau.cpu().numpy(), ref["tau"], rtol=2e-5, atol=1e-30)
-    np.testing.assert_allclose(op.ssa.cpu().numpy(), ref["ssa"], rtol=2e-5, atol=1e-30)
+    np.testing.assert_array_equal(op.tau.cpu().numpy(), ref["tau"])
+    np.testing.assert_array_equal(op.ssa.cpu().numpy(), ref["ssa"])
     assert float(op.g.abs().max()) == 0.0
     np.testing.assert_allclose(toa.cpu().numpy()[0], kd.solar_source, rtol=0)
 
