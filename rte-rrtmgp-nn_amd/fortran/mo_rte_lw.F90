@@ -1,0 +1,139 @@
+! mo_rte_lw -- drop-in for rte/mo_rte_lw.F90 (rte_lw, :60-424) in the fork's configuration
+! (no-scattering solver, compute_Jac = .false., rte/mo_rte_rrtmgp_config.F90:28).
+! Inputs are staged to the device, expand(sfc_emis) and lw_solver_noscat_GaussQuad run as HIP kernels
+! with the broadband reduction fused into the solver, and the broadband fluxes come back into the
+! caller's flux_up / flux_dn / flux_net.  g-point fluxes, the two-stream / rescaled paths, lw_Ds and the
+! Jacobians return an error string, as the reference does for unsupported combinations.
+module mo_rte_lw
+  use, intrinsic :: iso_c_binding
+  use mo_rte_kind,         only: wp
+  use mo_optical_props,    only: ty_optical_props_arry, ty_optical_props_1scl
+  use mo_source_functions, only: ty_source_func_lw
+  use mo_fluxes,           only: ty_fluxes_flexible
+  use mo_rte_rrtmgp_config, only: check_values
+  use mo_rrtmgpnn_c
+  implicit none
+  private
+  public :: rte_lw
+
+  integer,  parameter :: max_gauss_pts = 4
+  ! Diffusivity angle (nmus = 1) and Gauss-Jacobi-5 quadrature (mo_rte_lw.F90:113-125)
+  real(c_float), parameter, dimension(max_gauss_pts, max_gauss_pts) :: &
+    gauss_Ds  = reshape([1.66_wp,         0._wp,           0._wp,           0._wp, &
+                         1.18350343_wp,   2.81649655_wp,   0._wp,           0._wp, &
+                         1.09719858_wp,   1.69338507_wp,   4.70941630_wp,   0._wp, &
+                         1.06056257_wp,   1.38282560_wp,   2.40148179_wp,   7.15513024_wp], [4, 4]), &
+    gauss_wts = reshape([0.5_wp,          0._wp,           0._wp,           0._wp, &
+                         0.3180413817_wp, 0.1819586183_wp, 0._wp,           0._wp, &
+                         0.2009319137_wp, 0.2292411064_wp, 0.0698269799_wp, 0._wp, &
+                         0.1355069134_wp, 0.2034645680_wp, 0.1298475476_wp, 0.0311809710_wp], [4, 4])
+
+contains
+
+  function rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux, n_gauss_angles, use_2stream, &
+                  lw_Ds, flux_up_Jac, flux_dn_Jac) result(error_msg)
+    class(ty_optical_props_arry), intent(in) :: optical_props
+    logical,                      intent(in) :: top_at_1
+    type(ty_source_func_lw),      intent(in) :: sources
+    real(wp), dimension(:,:),     intent(in) :: sfc_emis        ! (nband, ncol)
+    class(ty_fluxes_flexible), intent(inout) :: fluxes
+    real(wp), dimension(:,:), contiguous, target, optional, intent(in) :: inc_flux   ! (ngpt, ncol)
+    integer,  optional, intent(in) :: n_gauss_angles
+    logical,  optional, intent(in) :: use_2stream
+    real(wp), dimension(:,:), optional, intent(in) :: lw_Ds
+    real(wp), dimension(:,:), target, optional, intent(inout) :: flux_up_Jac, flux_dn_Jac
+    character(len=128) :: error_msg
+    integer :: ncol, nlay, ngpt, nband, nmus
+    integer(c_int), allocatable :: lims(:,:)
+    type(c_ptr) :: d_tau, d_lay, d_lev, d_sfc, d_emis, d_emis_gpt, d_inc, d_up, d_dn
+    real(wp), allocatable :: up(:,:), dn(:,:)
+    character(len=128) :: e
+
+    ncol  = optical_props%get_ncol()
+    nlay  = optical_props%get_nlay()
+    ngpt  = optical_props%get_ngpt()
+    nband = optical_props%get_nband()
+    error_msg = ""
+    if (.not. fluxes%are_desired()) then
+      error_msg = "rte_lw: no space allocated for fluxes"; return
+    end if
+    if (fluxes%are_desired_gpt()) then
+      error_msg = "rte_lw: g-point fluxes are not produced by this build (broadband only)"; return
+    end if
+    if (any([sources%get_ncol(), sources%get_nlay(), sources%get_ngpt()] /= [ncol, nlay, ngpt])) then
+      error_msg = "rte_lw: sources and optical properties inconsistently sized"; return
+    end if
+    if (any(shape(sfc_emis) /= [nband, ncol])) then
+      error_msg = "rte_lw: sfc_emis inconsistently sized"; return
+    end if
+    if (check_values .and. any(sfc_emis < 0._wp .or. sfc_emis > 1._wp)) then
+      error_msg = "rte_lw: sfc_emis has values < 0 or > 1"; return
+    end if
+    if (present(inc_flux)) then
+      if (any(shape(inc_flux) /= [ngpt, ncol])) then
+        error_msg = "rte_lw: inc_flux inconsistently sized"; return
+      end if
+      if (check_values .and. any(inc_flux < 0._wp)) then
+        error_msg = "rte_lw: inc_flux has values < 0"; return
+      end if
+    end if
+    nmus = 1
+    if (present(n_gauss_angles)) then
+      if (n_gauss_angles > max_gauss_pts) then
+        error_msg = "rte_lw: asking for too many quadrature points for no-scattering calculation"; return
+      end if
+      if (n_gauss_angles < 1) then
+        error_msg = "rte_lw: have to ask for at least one quadrature point for no-scattering calculation"; return
+      end if
+      nmus = n_gauss_angles
+    end if
+    if (present(lw_Ds)) then
+      error_msg = "rte_lw: lw_Ds (column-dependent diffusivity) is not implemented"; return
+    end if
+    if (present(flux_up_Jac) .or. present(flux_dn_Jac)) then
+      error_msg = "rte_lw: compute_Jac is .false. in this configuration (mo_rte_rrtmgp_config.F90:28)"; return
+    end if
+    select type (optical_props)
+    type is (ty_optical_props_1scl)
+      if (present(use_2stream)) then
+        if (use_2stream) then
+          error_msg = "rte_lw: can't use two-stream methods with only absorption optical depth"; return
+        end if
+      end if
+    class default
+      error_msg = "rte_lw: two-stream / rescaled longwave solvers are not implemented (1scl only)"; return
+    end select
+
+    lims = optical_props%get_band_lims_gpoint()
+    d_tau = dev_upload(optical_props%tau, ngpt * nlay * ncol)
+    d_lay = dev_upload(sources%lay_source, ngpt * nlay * ncol)
+    d_lev = dev_upload(sources%lev_source, ngpt * (nlay + 1) * ncol)
+    d_sfc = dev_upload(sources%sfc_source, ngpt * ncol)
+    d_emis = dev_upload(sfc_emis, nband * ncol)
+    d_emis_gpt = dev_alloc(ngpt * ncol)
+    d_inc = c_null_ptr
+    if (present(inc_flux)) d_inc = dev_upload(inc_flux, ngpt * ncol)
+    d_up = dev_alloc((nlay + 1) * ncol)
+    d_dn = dev_alloc((nlay + 1) * ncol)
+    ! sfc_emis expanded to g-points (:429-447), then lw_solver_noscat_GaussQuad (:332-415)
+    error_msg = rrtmgpnn_check(c_rrtmgpnn_expand_band_to_gpt(rrtmgpnn_ctx(), nband, ngpt, ncol, lims, d_emis, &
+                                                             d_emis_gpt), "rte_lw: expand")
+    if (error_msg == '') &
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                 merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
+                                 gauss_wts(1:nmus, nmus), d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, d_up, d_dn), &
+                                 "rte_lw: lw_solver_noscat")
+    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "rte_lw")
+    if (error_msg == '') error_msg = e
+    if (error_msg == '') then
+      allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol))
+      call dev_download(up, d_up, (nlay + 1) * ncol)
+      call dev_download(dn, d_dn, (nlay + 1) * ncol)
+      if (associated(fluxes%flux_up)) fluxes%flux_up = up
+      if (associated(fluxes%flux_dn)) fluxes%flux_dn = dn
+      if (associated(fluxes%flux_net)) fluxes%flux_net = dn - up
+    end if
+    call dev_free(d_tau); call dev_free(d_lay); call dev_free(d_lev); call dev_free(d_sfc)
+    call dev_free(d_emis); call dev_free(d_emis_gpt); call dev_free(d_inc); call dev_free(d_up); call dev_free(d_dn)
+  end function rte_lw
+end module mo_rte_lw

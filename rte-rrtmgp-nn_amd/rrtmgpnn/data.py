@@ -55,10 +55,15 @@ def spacing(x):
     return np.float32(np.nextafter(x, np.float32(np.inf)) - x)
 
 
+def seqsum(a, axis=-1):
+    """float32 sum accumulated strictly in index order, like a Fortran DO loop / SUM (numpy's .sum is pairwise)."""
+    return np.take(np.cumsum(np.asarray(a, np.float32), axis=axis, dtype=np.float32), -1, axis=axis)
+
+
 def set_tsi(solar_source, tsi):
     """ty_gas_optics_rrtmgp%set_tsi (rrtmgp/mo_gas_optics_rrtmgp.F90:1097-1120), float32."""
     s = np.asarray(solar_source, np.float32)
-    norm = np.float32(1.0) / np.float32(s.sum(dtype=np.float32))
+    norm = np.float32(1.0) / seqsum(s)[()]
     return (s * np.float32(tsi) * norm).astype(np.float32)
 
 
@@ -177,5 +182,6 @@ def toa_flux(problem, kd_sw, tsi_default=1361.0):
     sol = set_tsi(kd_sw["solar_source"], tsi_default)
     ncol = problem["ncol"]
     toa = np.broadcast_to(sol, (ncol, sol.size)).astype(np.float32)
-    def_tsi = toa.sum(axis=1, dtype=np.float32)
-    return (toa * (problem["tsi"] / def_tsi)[:, None]).astype(np.float32)
+    def_tsi = seqsum(toa, axis=1)
+    # toa_flux * total_solar_irradiance / def_tsi, evaluated left to right as the driver does (:423)
+    return ((toa * np.asarray(problem["tsi"], np.float32)[:, None]) / def_tsi[:, None]).astype(np.float32)

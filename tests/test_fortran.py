@@ -1,0 +1,102 @@
+"""The Fortran drop-in class layer (rte-rrtmgp-nn_amd/fortran): modules with the reference's names
+(mo_gas_optics_rrtmgp, mo_rte_lw, mo_rte_sw, mod_network_rrtmgp, ...) over the C ABI.
+
+CPU: the layer and the example host program build; every C symbol it binds is declared in
+include/rrtmgpnn.h; the RBIN reader/writer and ty_gas_concs round-trip data.
+GPU: the example RFMIP host program (blocked, ragged last block) reproduces the oracle bit for bit.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, subset
+
+FDIR = os.path.join(ROOT, "rte-rrtmgp-nn_amd", "fortran")
+FBUILD = os.path.join(FDIR, "build")
+EXE = os.path.join(FBUILD, "rrtmgpnn_rfmip_clear_sky")
+FC = os.environ.get("FC_RRTMGPNN", "/opt/rocm/lib/llvm/bin/amdflang")
+
+needs_fc = pytest.mark.skipif(not os.path.exists(FC), reason="amdflang not available")
+
+
+def _make():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "rte-rrtmgp-nn_amd")], check=True, capture_output=True)
+    r = subprocess.run(["make", "-C", FDIR], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def write_problem(prob, path, n_gauss_angles=1):
+    from rrtmgpnn import rbin
+    names = sorted(prob["gases"])
+    arrays = {k: np.asarray(prob[k], np.float32) for k in ("play", "plev", "tlay", "tlev", "tsfc", "sfc_emis",
+                                                             "sfc_alb", "mu0", "tsi")}
+    arrays["usecol"] = np.asarray(prob["usecol"], np.float32)
+    arrays["top_at_1"] = np.array([1.0 if prob["top_at_1"] else 0.0], np.float32)
+    arrays["n_gauss_angles"] = np.array([n_gauss_angles], np.float32)
+    arrays["gas_names"] = rbin.chars(names, 32)
+    for g in names:
+        arrays["vmr_" + g] = np.broadcast_to(np.asarray(prob["gases"][g], np.float32),
+                                             prob["play"].shape).copy()
+    rbin.write(path, arrays)
+    return names
+
+
+@needs_fc
+def test_fortran_layer_builds_and_binds_only_header_symbols():
+    _make()
+    assert os.path.exists(EXE)
+    header = open(os.path.join(ROOT, "include", "rrtmgpnn.h")).read()
+    declared = set(re.findall(r"\b(rrtmgpnn_\w+)\s*\(", header))
+    nm = subprocess.run(["nm", "-u", os.path.join(FBUILD, "librrtmgpnn_fortran.a")], capture_output=True,
+                        text=True, check=True).stdout
+    bound = set(re.findall(r"\b(rrtmgpnn_\w+)\b", nm))
+    assert bound, "the Fortran layer binds no C entry point"
+    assert bound <= declared, "bound but not declared: %s" % sorted(bound - declared)
+
+
+@needs_fc
+def test_fortran_rbin_roundtrip_and_gas_concs(tmp_path, rfmip):
+    from rrtmgpnn import rbin
+    _make()
+    exe = str(tmp_path / "rbin_roundtrip")
+    subprocess.run([FC, "-O1", "-I", FBUILD, os.path.join(ROOT, "tests", "fortran", "rbin_roundtrip.F90"), "-o", exe,
+                    os.path.join(FBUILD, "librrtmgpnn_fortran.a")], check=True, capture_output=True)
+    prob = subset(rfmip, np.arange(0, 1800, 97))
+    fin, fout = str(tmp_path / "in.rbin"), str(tmp_path / "out.rbin")
+    write_problem(prob, fin)
+    subprocess.run([exe, fin, fout], check=True, capture_output=True)
+    out = rbin.read(fout)
+    np.testing.assert_array_equal(out["play"], prob["play"])
+    np.testing.assert_array_equal(out["tsfc"], prob["tsfc"])
+    np.testing.assert_array_equal(out["h2o"], prob["gases"]["h2o"])
+
+
+@pytest.mark.gpu
+@needs_fc
+def test_fortran_rfmip_driver_matches_oracle(tmp_path, orc, rfmip):
+    """The reference-shaped host program, blocked (64 columns, ragged last block), vs the oracle."""
+    from rrtmgpnn import data, rbin
+    if not os.path.exists(EXE):
+        _make()
+    prob = subset(rfmip, np.arange(0, 1800, 9))
+    fin, fout = str(tmp_path / "prob.rbin"), str(tmp_path / "flux.rbin")
+    write_problem(prob, fin)
+    r = subprocess.run(["timeout", "-k", "10", "300", EXE, fin, fout, data.DATA_DIR, "64"], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = rbin.read(fout)
+    lu, ld, _ = orc.clear_sky_lw(prob, [data.load_model("lw_abs"), data.load_model("lw_pfrac")],
+                                 data.load_kdist("lw"))
+    su, sd, sr, _ = orc.clear_sky_sw(prob, [data.load_model("sw_abs"), data.load_model("sw_ray")],
+                                     data.load_kdist("sw"))
+    use = prob["usecol"]
+    for k, ref, g in (("lw_up", lu, got["lw_flux_up"]), ("lw_dn", ld, got["lw_flux_dn"]),
+                      ("sw_up", su, got["sw_flux_up"]), ("sw_dn", sd, got["sw_flux_dn"]),
+                      ("sw_dir", sr[use], got["sw_flux_dir"][use])):
+        err = float(np.sqrt(np.mean((g.astype(np.float64) - ref) ** 2)))
+        assert err <= 1e-3, "%s: RMS %.3g W/m2" % (k, err)
+        np.testing.assert_array_equal(g, ref, err_msg=k + ": not bit-identical")
