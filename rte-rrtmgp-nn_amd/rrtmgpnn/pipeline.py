@@ -144,6 +144,12 @@ class ClearSkyStep:
     def replay(self):
         self.graph.replay()
 
+    def io_tensors(self):
+        """(inputs, outputs): the device tensors a host-resident caller would upload / download per step."""
+        ins = [self.play, self.plev, self.tlay, self.tlev, self.tsfc, *self.gases.values(), self.sfc_emis, self.mu0,
+               self.toa, self.alb]
+        return ins, [self.lw_up, self.lw_dn, self.sw_up, self.sw_dn, self.sw_dir]
+
     def fluxes(self):
         """Host copies of the broadband fluxes, with SW zeroed where sza >= 90 is applied by the caller."""
         return {k: getattr(self, k).cpu().numpy() for k in ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir")}
