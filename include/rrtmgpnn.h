@@ -123,7 +123,20 @@ int rrtmgpnn_lw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int nco
                               const float *tau, const float *lay_source, const float *lev_source,
                               const float *sfc_emis_gpt, const float *sfc_source,
                               float *flux_up, float *flux_dn);
-/* sw_solver_2stream (:541-692).  inc_flux_dif may be NULL (zero, rte/mo_rte_sw.F90:197-210). */
+/* Fused clear-sky LW entry: compute_Planck_source_nn (rrtmgp/kernels/mo_gas_optics_kernels.F90:615-683)
+ * + lw_solver_noscat_GaussQuad in one kernel.  Takes the Planck fraction (what predict_nn_lw writes into
+ * lay_source) instead of lay/lev/sfc sources, forms every source in-kernel with the same products as
+ * rrtmgpnn_compute_planck_source_nn, and never stores them: fluxes are bit-identical to
+ * compute_planck_source_nn followed by lw_solver_noscat.  band_lims_gpt HOST (2,nbnd); totplnk DEVICE. */
+int rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                     const float *Ds, const float *weights, const float *inc_flux, const float *tau,
+                                     const float *pfrac, int nbnd, int nPlanckTemp, const float *tlay,
+                                     const float *tlev, const float *tsfc, int sfc_lay, const int *band_lims_gpt,
+                                     float temp_ref_min, float totplnk_delta, const float *totplnk,
+                                     const float *sfc_emis_gpt, float *flux_up, float *flux_dn);
+/* sw_solver_2stream (:541-692).  inc_flux_dif may be NULL (zero, rte/mo_rte_sw.F90:197-210).
+ * g may be NULL: asymmetry parameter identically zero, as gas_optics_ext's NN branch produces
+ * (mo_gas_optics_rrtmgp.F90:560-567) -- same fluxes as passing a zero-filled array. */
 int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
                                const float *inc_flux, const float *inc_flux_dif,
                                const float *tau, const float *ssa, const float *g, const float *mu0,

@@ -99,6 +99,11 @@ int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
                      const float *wts, const float *inc_flux, const float *tau, const float *lay_source,
                      const float *lev_source, const float *sfc_emis, const float *sfc_source, float *flux_up,
                      float *flux_dn);
+int launch_lw_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                            const float *Ds, const float *wts, const float *inc_flux, const float *tau,
+                            const float *pfrac, int ntemp, const float *tlay, const float *tlev, const float *tsfc,
+                            int sfc_lay, const BandArgs &bands, float temp_ref_min, float totplnk_delta,
+                            const float *totplnk, const float *sfc_emis, float *flux_up, float *flux_dn);
 int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                       const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                       const float *mu0, const float *alb_dir, const float *alb_dif, float *flux_up,

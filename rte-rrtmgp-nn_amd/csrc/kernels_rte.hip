@@ -118,28 +118,66 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 // LDS ring of kRing levels; when it fills, 4*kRing*NQ threads each walk one (quantity, level,
 // partial) sequentially.  Deterministic and order-identical to the reference.
 // ------------------------------------------------------------------------------------------
-static constexpr int kRing = 8;
-static constexpr int kPF = 4;
-static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS  // layers of inputs kept in flight per lane (software prefetch)
+// Tuning knobs (overridable with -D for tools/solver_variants.sh):
+//   kRing : levels staged in LDS per ordered flush;
+//   *_PF  : layers of inputs kept in flight per lane (software prefetch) -- LW, fused LW, SW;
+//   *_WAVES : __launch_bounds__ minimum waves per SIMD (0 = none; > 0 caps blocks at 256 threads).
+#ifndef RRTMGPNN_RING
+#define RRTMGPNN_RING 8
+#endif
+#ifndef RRTMGPNN_SW_RING
+#define RRTMGPNN_SW_RING 6
+#endif
+#ifndef RRTMGPNN_LW_PF
+#define RRTMGPNN_LW_PF 4
+#endif
+#ifndef RRTMGPNN_LWF_PF
+#define RRTMGPNN_LWF_PF 2
+#endif
+#ifndef RRTMGPNN_SW_PF
+#define RRTMGPNN_SW_PF 2
+#endif
+#ifndef RRTMGPNN_LW_WAVES
+#define RRTMGPNN_LW_WAVES 8
+#endif
+#ifndef RRTMGPNN_SW_WAVES
+#define RRTMGPNN_SW_WAVES 8
+#endif
+#define BOUNDS_(w) __launch_bounds__(256, w)
+#if RRTMGPNN_LW_WAVES > 0
+#define LW_BOUNDS BOUNDS_(RRTMGPNN_LW_WAVES)
+#else
+#define LW_BOUNDS
+#endif
+#if RRTMGPNN_SW_WAVES > 0
+#define SW_BOUNDS BOUNDS_(RRTMGPNN_SW_WAVES)
+#else
+#define SW_BOUNDS
+#endif
+static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
+static constexpr int kLwMaxG = RRTMGPNN_LW_WAVES > 0 ? 256 : 1024;  // g-points per column block
+static constexpr int kSwMaxG = RRTMGPNN_SW_WAVES > 0 ? 256 : 1024;
+static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS
 
-// Flush `nfill` staged levels.  ring: [nq][kRing][ngpt]; part: [nq][nlev][4]; slot_lev[c] = level.
+// Flush `n` staged levels.  ring: [nq][R][ngpt], slot c holds level lev0 + c*dl; part: [nq][nlev][4].
 // One thread per (quantity, level) walks the level's g-points with 16-byte LDS reads: element k of
 // the float4 at m is g = 4m + k, so the 4 interleaved partials advance together, each in g order.
 // dn_mode (SW): quantity 1 is accumulated as (s + ring1) + ring2, i.e. sums_dn + radn_dn + radn_dir.
 // ngpt % 4 != 0: the reference uses sum(radn, 1) instead (one sequential sum, kept in partial 0).
-__device__ __forceinline__ void ring_flush(const float *ring, float *part, const int *slot_lev, int nq, int nfill,
-                                           int ngpt, int nlev, bool accumulate, bool dn_mode)
+template <int R>
+__device__ __forceinline__ void ring_flush(const float *ring, float *part, int nq, int n, int lev0, int dl, int ngpt,
+                                           int nlev, bool dn_mode)
 {
   __syncthreads();
   const int t = threadIdx.x;
 #ifdef RRTMGPNN_ABL_NO_REDUCE
   if (false) {
 #else
-  if (t < nq * nfill) {
+  if (t < nq * n) {
 #endif
-    const int q = t / nfill, c = t % nfill;
-    const float *r = ring + ((size_t)q * kRing + c) * ngpt;
-    const float *r2 = ring + ((size_t)2 * kRing + c) * ngpt;
+    const int q = t / n, c = t - q * n;
+    const float *r = ring + ((size_t)q * R + c) * ngpt;
+    const float *r2 = ring + ((size_t)2 * R + c) * ngpt;
     const bool dn = dn_mode && q == 1;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
     if ((ngpt & 3) == 0) {
@@ -162,9 +200,8 @@ __device__ __forceinline__ void ring_flush(const float *ring, float *part, const
       if (dn) for (int i = 0; i < ngpt; i++) s0 = s0 + (r[i] + r2[i]);  // radn_dn = radn_dn + radn_dir; sum
       else    for (int i = 0; i < ngpt; i++) s0 = s0 + r[i];
     }
-    float *p = part + ((size_t)q * nlev + slot_lev[c]) * 4;
-    if (accumulate) { p[0] += s0; p[1] += s1; p[2] += s2; p[3] += s3; }
-    else { p[0] = s0; p[1] = s1; p[2] = s2; p[3] = s3; }
+    float4 *p = (float4 *)(part + ((size_t)q * nlev + lev0 + c * dl) * 4);
+    *p = make_float4(s0, s1, s2, s3);
   }
   __syncthreads();
 }
@@ -172,69 +209,134 @@ __device__ __forceinline__ void ring_flush(const float *ring, float *part, const
 __device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]) + p[2]) + p[3]; }
 
 // ------------------------------------------------------------------------------------------
+// Column-local addressing.  Every solver array is (ngpt, n, ncol) with the column block uniform per
+// workgroup, so each array gets a per-column buffer descriptor built from wave-uniform values: a
+// load is `buffer_load v, voff=g*4, s_rsrc, soff=layer*ngpt*4` -- no per-lane 64-bit address math,
+// the layer offset lives in an SGPR.
+// ------------------------------------------------------------------------------------------
+struct ColArr {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ ColArr() = default;
+  __device__ __forceinline__ ColArr(const float *base, size_t col_off, uint32_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void *)(base + col_off), 0, (int)bytes, 0x00020000)) {}
+  __device__ __forceinline__ float ld(uint32_t voff, uint32_t soff) const
+  {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  }
+  __device__ __forceinline__ void st(float v, uint32_t voff, uint32_t soff) const
+  {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+  }
+};
+
+// ------------------------------------------------------------------------------------------
 // LW no-scattering solver.  block = one column, lane = g-point.  The down pass stores nothing: the
-// up pass re-reads tau/lay/lev for its layer (L2/MALL-hot) and recomputes trans and the source,
-// bitwise identical to the down pass' values.  Source indexing follows lw_source_noscat
-// (:742-776): source_dn uses lev(l+1), source_up uses lev(l) for EVERY orientation (quirk B-1).
-// LDS: ring [kRing][ngpt], part [2][nlev][4], slot_lev [kRing].
+// up pass re-reads its layer's inputs (L2/MALL-hot) and recomputes trans and the source, bitwise
+// identical to the down pass' values.  Source indexing follows lw_source_noscat (:742-776):
+// source_dn uses lev(l+1), source_up uses lev(l) for EVERY orientation (quirk B-1).
+//
+// Layers are walked in chunks of kRing: each chunk's levels are staged in LDS slots with static
+// indices (the chunk loop is unrolled) and reduced by one ring_flush at the chunk end, so the
+// recurrence never branches around a flush.  Inputs run kPF layers ahead of the recurrence.
+//
+// kFused: the Planck sources are not read from lay_source/lev_source but formed in-kernel from the
+// Planck fraction exactly as compute_Planck_source_nn (mo_gas_optics_kernels.F90:615-683) forms
+// them -- lay(g,l) = pfrac(g,l)*B_b(tlay(l)), lev(g,l) = pfrac(g,min(l,nlay-1))*B_b(tlev(l)),
+// sfc(g) = pfrac(g,sfc_lay)*B_b(tsfc) -- with the band Planck values B_b interpolated once per
+// column into LDS.  Same products, same bits; the source arrays never touch HBM.
+// LDS: etab | [fused: B [nbnd][2*nlay+1], Bsfc[nbnd]] | ring [kRing][ngpt] | part [2][nlev][4]
 // ------------------------------------------------------------------------------------------
 struct LwAngles {
   float D[4], w[4];
   int nmus;
 };
 
-__global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwAngles ang,
-                                 const float *__restrict__ inc_flux, const float *__restrict__ tau,
-                                 const float *__restrict__ lay, const float *__restrict__ lev,
-                                 const float *__restrict__ emis, const float *__restrict__ sfc,
-                                 float *__restrict__ ws, float *__restrict__ flux_up, float *__restrict__ flux_dn)
+struct LwPlanck {
+  const float *tlay, *tlev, *tsfc, *totplnk;
+  int ntemp, sfc_lay;
+  float tmin, tdelta;
+};
+
+// fused Planck table size in floats, padded so the ring that follows stays 16-byte aligned
+__host__ __device__ constexpr size_t lw_btab_floats(int nbnd, int nlay) { return ((size_t)nbnd * (2 * nlay + 2) + 3) & ~(size_t)3; }
+
+template <bool kFused, int kPF>
+__global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwAngles ang,
+                                           const float *__restrict__ inc_flux, const float *__restrict__ tau,
+                                           const float *__restrict__ lay, const float *__restrict__ lev,
+                                           const float *__restrict__ emis, const float *__restrict__ sfc,
+                                           LwPlanck pl, BandArgs bands, float *__restrict__ ws,
+                                           float *__restrict__ flux_up, float *__restrict__ flux_dn)
 {
+  static_assert(kRing % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
   const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
   const int nlev = nlay + 1;
+  const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
   // nmus > 1 (lw_solver_noscat_GaussQuad :383-412): g-point fluxes are summed over angles first, then
   // reduced with sum_broadband's plain sequential sum; ws holds the per-g accumulators (2, nlev, ngpt).
   const bool multi = ang.nmus > 1;
   float *wcol = multi ? ws + (size_t)2 * nlev * ngpt * icol : nullptr;
-  float *ring = smem + kExpTabFloats;            // [kRing][ngpt]
-  float *part = ring + (size_t)kRing * ngpt;     // [2][nlev][4]: 0 = dn, 1 = up
-  int *slot_lev = (int *)(part + (size_t)2 * nlev * 4);
-  uint64_t *etab = (uint64_t *)(smem + kExpTabOff);  // 16-byte aligned slot at the front
+  uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
+  float *btab = smem + kExpTabFloats;                        // fused: [nbnd][2*nlay+1] + [nbnd]
+  const int brow = 2 * nlay + 1;
+  float *ring = btab + (kFused ? lw_btab_floats(bands.nbnd, nlay) : 0);  // [kRing][ngpt]
+  float *part = ring + (size_t)kRing * ngpt;                 // [2][nlev][4]: 0 = dn, 1 = up
   load_exp_table(etab);
-  __syncthreads();
+  const ColArr Ttau(tau, (size_t)ngpt * nlay * icol, row * nlay);
+  const ColArr Tlay(lay, (size_t)ngpt * nlay * icol, row * nlay);  // lay_source, or pfrac when fused
+  const ColArr Tlev(lev, (size_t)ngpt * nlev * icol, row * nlev);
+  const float *bl = btab;  // this lane's band row
+  float ss;
+  if constexpr (kFused) {
+    // band Planck values for this column: B_b(tlay(l)) at [b][l], B_b(tlev(l)) at [b][nlay+l], B_b(tsfc) at
+    // [nbnd*brow + b]; interpolate1D of compute_Planck_source_nn
+    const float *tl = pl.tlay + (size_t)nlay * icol, *tv = pl.tlev + (size_t)nlev * icol;
+    for (int i = threadIdx.x; i < bands.nbnd * (brow + 1); i += blockDim.x) {
+      const int b = i < bands.nbnd * brow ? i / brow : i - bands.nbnd * brow;
+      const int k = i < bands.nbnd * brow ? i - b * brow : -1;
+      const float T = k < 0 ? pl.tsfc[icol] : (k < nlay ? tl[k] : tv[k - nlay]);
+      btab[i] = interp1d(T, pl.tmin, pl.tdelta, pl.ntemp, pl.totplnk + (size_t)pl.ntemp * b);
+    }
+    const int b = band_of(bands, gc);
+    bl = btab + (size_t)b * brow;
+    __syncthreads();
+    ss = Tlay.ld(vg, row * (uint32_t)(pl.sfc_lay - 1)) * btab[(size_t)bands.nbnd * brow + b];
+  } else {
+    __syncthreads();
+    ss = on ? sfc[g + (size_t)ngpt * icol] : 0.0f;
+  }
   const float tau_thresh = sqrtf(FLT_EPSILON);
-  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
   const float e = on ? emis[g + (size_t)ngpt * icol] : 0.0f;
-  const float ss = on ? sfc[g + (size_t)ngpt * icol] : 0.0f;
   const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
-  int nfill = 0;
-  auto stage = [&](float v, int level, float *pq, bool acc) {
+  // stage one level's value: slot r of the ring, or (nmus > 1) the per-g accumulator of plane q
+  auto put = [&](float v, int r, int q, int level, bool acc) {
     if (multi) {
       if (on) {
-        float *w = wcol + (size_t)(pq == part ? 0 : nlev) * ngpt + (size_t)level * ngpt + g;
+        float *w = wcol + ((size_t)q * nlev + level) * ngpt + g;
         *w = acc ? *w + v : v;
       }
-      return;
-    }
-    if (on) ring[(size_t)nfill * ngpt + g] = v;
-    if (g == 0) slot_lev[nfill] = level;
-#ifdef RRTMGPNN_ABL_NO_BARRIER
-    return;
-#endif
-    if (++nfill == kRing) {
-      ring_flush(ring, pq, slot_lev, 1, nfill, ngpt, nlev, acc, false);
-      nfill = 0;
+    } else if (on) {
+      ring[(size_t)r * ngpt + g] = v;
     }
   };
-  auto drain = [&](float *pq, bool acc) {
-    if (multi) return;
-    if (nfill) ring_flush(ring, pq, slot_lev, 1, nfill, ngpt, nlev, acc, false);
-    nfill = 0;
+  auto flush = [&](float *pq, int n, int lev0, int dl) {
+#ifndef RRTMGPNN_ABL_NO_BARRIER
+    if (!multi) ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
+#endif
+  };
+  // layer source and the level source on the side given by `li` (lev index, 0..nlay)
+  auto lay_src = [&](float y, int l) { return kFused ? y * bl[l] : y; };
+  auto lev_src = [&](float v, int li) { return kFused ? v * bl[nlay + li] : v; };
+  // the value to load for lev index li: lev_source(li), or pfrac(min(li, nlay-1)) when fused
+  auto lev_ld = [&](int li) {
+    return kFused ? Tlay.ld(vg, row * (uint32_t)min(li, nlay - 1)) : Tlev.ld(vg, row * (uint32_t)li);
   };
   float *pdn = part, *pup = part + (size_t)nlev * 4;
+  const int dl_dn = top_at_1 ? 1 : -1;  // level index step going down
 
   for (int imu = 0; imu < ang.nmus; imu++) {
     const float D = ang.D[imu];
@@ -243,73 +345,75 @@ __global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwA
     const float fac = (multi || (ngpt & 3) == 0) ? 2.0f * kPi * ang.w[imu] : 1.0f;
     const bool acc = imu > 0;
     float I = inc / (2.0f * kPi * ang.w[imu]);
-    stage(fac * I, top, pdn, acc);
-    // downward: lw_transport_noscat_dn (:982-1009).  Inputs of layer step j+kPF are loaded while step
-    // j computes (loads are unconditional on clamped indices: no branch around a load).
+    put(fac * I, 0, 0, top, acc);
+    flush(pdn, 1, top, 1);
+    // downward: lw_transport_noscat_dn (:982-1009); j-th layer from the top is l = lay_dn(j)
+    auto lay_dn = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
     {
       float pt[kPF], py[kPF], pv[kPF];
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
-        const int l = top_at_1 ? min(p, nlay - 1) : max(nlay - 1 - p, 0);
-        const size_t i = (size_t)gc + (size_t)ngpt * l;
-        pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i + ngpt];
+        const int l = lay_dn(min(p, nlay - 1));
+        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pv[p] = lev_ld(l + 1);
       }
-      for (int j0 = 0; j0 < nlay; j0 += kPF) {
+      for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
-        for (int p = 0; p < kPF; p++) {
-          const int j = j0 + p;
+        for (int r = 0; r < kRing; r++) {
+          const int j = j0 + r, p = r % kPF;
           if (j < nlay) {
-            const int l = top_at_1 ? j : nlay - 1 - j;
-            const float t = pt[p] * D, ly = py[p], lvdn = pv[p];
+            const int l = lay_dn(j);
+            const float t = pt[p] * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
             {
-              const int jn = min(j + kPF, nlay - 1), ln = top_at_1 ? jn : nlay - 1 - jn;
-              const size_t i = (size_t)gc + (size_t)ngpt * ln;
-              pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i + ngpt];
+              const int ln = lay_dn(min(j + kPF, nlay - 1));
+              pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
             }
-            float T = ref_expf_tab(-t, etab);
-            float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
-            float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
+            const float T = ref_expf_nb(-t, etab);
+            const float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+            const float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
             I = T * I + S;
-            stage(fac * I, top_at_1 ? l + 1 : l, pdn, acc);
+            put(fac * I, r, 0, top_at_1 ? l + 1 : l, acc);
           }
         }
+        flush(pdn, min(kRing, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     }
-    drain(pdn, acc);
     // surface reflection and emission (:269)
     float U = I * (1.0f - e) + e * ss;
-    stage(fac * U, sfcl, pup, acc);
-    // upward: lw_transport_noscat_up (:950-980)
+    put(fac * U, 0, 1, sfcl, acc);
+    flush(pup, 1, sfcl, 1);
+    // upward: lw_transport_noscat_up (:950-980); j-th layer from the surface is l = lay_up(j)
+    auto lay_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
     {
       float pt[kPF], py[kPF], pv[kPF];
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
-        const int l = top_at_1 ? max(nlay - 1 - p, 0) : min(p, nlay - 1);
-        const size_t i = (size_t)gc + (size_t)ngpt * l;
-        pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i];
+        const int l = lay_up(min(p, nlay - 1));
+        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l);
+        if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * l);
       }
-      for (int j0 = 0; j0 < nlay; j0 += kPF) {
+      for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
-        for (int p = 0; p < kPF; p++) {
-          const int j = j0 + p;
+        for (int r = 0; r < kRing; r++) {
+          const int j = j0 + r, p = r % kPF;
           if (j < nlay) {
-            const int l = top_at_1 ? nlay - 1 - j : j;
-            const float t = pt[p] * D, ly = py[p], lvup = pv[p];
+            const int l = lay_up(j);
+            // fused: lev(l) = pfrac(l) * B(tlev(l)) (l < nlay), from the layer's own pfrac
+            const float t = pt[p] * D, ly = lay_src(py[p], l), lvup = lev_src(kFused ? py[p] : pv[p], l);
             {
-              const int jn = min(j + kPF, nlay - 1), ln = top_at_1 ? nlay - 1 - jn : jn;
-              const size_t i = (size_t)gc + (size_t)ngpt * ln;
-              pt[p] = tau[cl + i]; py[p] = lay[cl + i]; pv[p] = lev[cv + i];
+              const int ln = lay_up(min(j + kPF, nlay - 1));
+              pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln);
+              if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * ln);
             }
-            float T = ref_expf_tab(-t, etab);
-            float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
-            float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
+            const float T = ref_expf_nb(-t, etab);
+            const float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+            const float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
             U = T * U + S;
-            stage(fac * U, top_at_1 ? l : l + 1, pup, acc);
+            put(fac * U, r, 1, top_at_1 ? l : l + 1, acc);
           }
         }
+        flush(pup, min(kRing, nlay - j0), sfcl - dl_dn * (j0 + 1), -dl_dn);
       }
     }
-    drain(pup, acc);
   }
   if (multi) {
     __syncthreads();
@@ -328,42 +432,95 @@ __global__ void lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwA
   }
 }
 
-int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
-                     const float *wts, const float *inc_flux, const float *tau, const float *lay_source,
-                     const float *lev_source, const float *sfc_emis, const float *sfc_source, float *flux_up,
-                     float *flux_dn)
+template <bool kFused>
+static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                          const float *Ds, const float *wts, const float *inc_flux, const float *tau,
+                          const float *lay_or_pfrac, const float *lev_source, const float *sfc_emis,
+                          const float *sfc_source, const LwPlanck &pl, const BandArgs &bands, float *flux_up,
+                          float *flux_dn)
 {
   if (ncol == 0) return RRTMGPNN_OK;
   if (nmus < 1 || nmus > 4) return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: nmus must be 1..4");
-  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: ngpt > 1024");
+  if (ngpt > kLwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many g-points");
   LwAngles a{};
   a.nmus = nmus;
   for (int i = 0; i < nmus; i++) { a.D[i] = Ds[i]; a.w[i] = wts[i]; }
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4) + sizeof(int) * kRing;
+  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4);
+  if (kFused) lds += sizeof(float) * lw_btab_floats(bands.nbnd, nlay);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many layers for LDS partials");
   void *ws = nullptr;
   if (nmus > 1) {
     int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL(lw_noscat_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a,
-                     inc_flux, tau, lay_source, lev_source, sfc_emis, sfc_source, (float *)ws, flux_up, flux_dn);
+  hipLaunchKernelGGL((lw_noscat_kernel<kFused, kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF>), dim3(ncol),
+                     dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac,
+                     kFused ? lay_or_pfrac : lev_source, sfc_emis, sfc_source, pl, bands, (float *)ws, flux_up,
+                     flux_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_noscat_kernel");
   return RRTMGPNN_OK;
 }
 
+int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
+                     const float *wts, const float *inc_flux, const float *tau, const float *lay_source,
+                     const float *lev_source, const float *sfc_emis, const float *sfc_source, float *flux_up,
+                     float *flux_dn)
+{
+  LwPlanck pl{};
+  BandArgs b{};
+  return launch_lw_impl<false>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, lay_source, lev_source,
+                               sfc_emis, sfc_source, pl, b, flux_up, flux_dn);
+}
+
+int launch_lw_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                            const float *Ds, const float *wts, const float *inc_flux, const float *tau,
+                            const float *pfrac, int ntemp, const float *tlay, const float *tlev, const float *tsfc,
+                            int sfc_lay, const BandArgs &bands, float temp_ref_min, float totplnk_delta,
+                            const float *totplnk, const float *sfc_emis, float *flux_up, float *flux_dn)
+{
+  LwPlanck pl{tlay, tlev, tsfc, totplnk, ntemp, sfc_lay, temp_ref_min, totplnk_delta};
+  return launch_lw_impl<true>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, pfrac, nullptr, sfc_emis,
+                              nullptr, pl, bands, flux_up, flux_dn);
+}
+
 // ------------------------------------------------------------------------------------------
 // SW two-stream solver.  block = one column, lane = g-point.
-//   pass 1 (top->bottom): direct beam F_dir per level -> workspace
+//   pass 1 (top->bottom): direct beam F_dir per level -> WA
 //   pass 2 (bottom->top): sw_two_stream_source coefficients (Tnoscat recomputed bit-identically
-//          from tau and mu0), adding's albedo/src/denom (Shonk & Hogan Eqs 9-11); stores per level
-//          alpha and src only
-//   pass 3 (top->bottom): recomputes the layer coefficients (same bits as pass 2: memory traffic is
-//          the bound, arithmetic is spare) and runs Eqs 12-13 with the reference's exact expression
-//          order; direct beam recomputed; ordered broadband sums of up, dif+dir, dir.
-// Workspace ws: 2 arrays (ngpt, nlay+1, ncol): [F_dir -> alpha], src.
+//          from tau and mu0) and adding's albedo/src (Shonk & Hogan Eqs 9-11) -> WB, WS per level;
+//          the layer's direct-beam source S_dn -> WD
+//   pass 3 (top->bottom): Eqs 12-13 with the reference's exact expression order.  Only R_dif and
+//          T_dif are recomputed (same expressions, same bits as pass 2); S_dn, albedo, src and the
+//          direct beam are read back.  Ordered broadband sums of up, dif+dir, dir, staged per chunk
+//          of kRingSw levels as in the LW solver.
+// The split between recomputing and storing balances the kernel's two bounds: recomputing all of
+// sw_two_stream in pass 3 made it VALU-bound (~400 VALU ops per layer and g-point), storing every
+// coefficient would make it HBM-bound; this form is ~250 ops and 4 workspace planes.
+// Workspace ws: 4 arrays (ngpt, nlay+1, ncol): WA = F_dir, WB = albedo, WS = src, WD = S_dn.
+// kHasG = false: g == NULL means g == 0 everywhere (the NN path zero-fills g, quirk B-6); the
+// coefficient expressions then evaluate with a literal 0 -- identical bits, one array less to read.
 // ------------------------------------------------------------------------------------------
+struct SwDif {
+  float gamma1, gamma2, k, emk, em2k, RT, Rdif, Tdif;
+};
+
+// diffuse reflectance/transmittance of sw_two_stream (mo_rte_solver_kernels.F90:1366-1480)
+__device__ __forceinline__ SwDif sw_dif(float tau, float w0, float g, const uint64_t *etab)
+{
+  const float k_min = 1.e-4f;
+  SwDif d;
+  d.gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
+  d.gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
+  d.k = sqrt_rn_normal(fmaxf((d.gamma1 - d.gamma2) * (d.gamma1 + d.gamma2), k_min));
+  d.emk = ref_expf_nb(-tau * d.k, etab);
+  d.em2k = d.emk * d.emk;
+  d.RT = rcp_rn_normal(d.k * (1.0f + d.em2k) + d.gamma1 * (1.0f - d.em2k));
+  d.Rdif = d.RT * d.gamma2 * (1.0f - d.em2k);
+  d.Tdif = d.RT * 2.0f * d.k * d.emk;
+  return d;
+}
+
 struct SwCoef {
   float Rdif, Tdif, Sup, Sdn, Tnoscat;
 };
@@ -371,25 +528,21 @@ struct SwCoef {
 __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, float mu0, float mu0_inv, float dir_inc,
                                                const uint64_t *etab)
 {
-  const float k_min = 1.e-4f, eps = FLT_EPSILON;
+  const float eps = FLT_EPSILON;
   SwCoef c;
-  float Tnoscat = ref_expf_tab(-tau * mu0_inv, etab);
-  float gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
-  float gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
+  const SwDif d = sw_dif(tau, w0, g, etab);
+  const float gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
+  float Tnoscat = ref_expf_nb(-tau * mu0_inv, etab);
   float gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
   float gamma4 = 1.0f - gamma3;
   float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
-  float k = sqrtf(fmaxf((gamma1 - gamma2) * (gamma1 + gamma2), k_min));
-  float emk = ref_expf_tab(-tau * k, etab);
-  float em2k = emk * emk;
   float k2e = 2.0f * k * emk;
-  float RT = 1.0f / (k * (1.0f + em2k) + gamma1 * (1.0f - em2k));
-  c.Rdif = RT * gamma2 * (1.0f - em2k);
-  c.Tdif = RT * 2.0f * k * emk;
+  c.Rdif = d.Rdif;
+  c.Tdif = d.Tdif;
   float k_mu = k * mu0, k_mu2 = k_mu * k_mu, k_g3 = k * gamma3, k_g4 = k * gamma4;
   float dd = (fabsf(1.0f - k_mu2) >= eps) ? (1.0f - k_mu2) : eps;
-  RT = w0 * RT / dd;
+  float RT = w0 * d.RT / dd;
   float Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
                      k2e * (gamma3 - alpha2 * mu0) * Tnoscat);
   float Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
@@ -402,43 +555,48 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   return c;
 }
 
-__global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, const float *__restrict__ inc_flux,
-                                  const float *__restrict__ inc_dif, const float *__restrict__ tau,
-                                  const float *__restrict__ ssa, const float *__restrict__ gg,
-                                  const float *__restrict__ mu0p, const float *__restrict__ alb_dir,
-                                  const float *__restrict__ alb_dif, float *__restrict__ ws,
-                                  float *__restrict__ flux_up, float *__restrict__ flux_dn, float *__restrict__ flux_dir)
+template <bool kHasG, int kPF>
+__global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1,
+                                            const float *__restrict__ inc_flux, const float *__restrict__ inc_dif,
+                                            const float *__restrict__ tau, const float *__restrict__ ssa,
+                                            const float *__restrict__ gg, const float *__restrict__ mu0p,
+                                            const float *__restrict__ alb_dir, const float *__restrict__ alb_dif,
+                                            float *__restrict__ ws, float *__restrict__ flux_up,
+                                            float *__restrict__ flux_dn, float *__restrict__ flux_dir)
 {
+  static_assert(kRingSw % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
   const int nlev = nlay + 1;
-  float *ring = smem + kExpTabFloats;              // [3][kRing][ngpt]: up, dif, dir
+  float *ring = smem + kExpTabFloats;                // [3][kRingSw][ngpt]: up, dif, dir
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   load_exp_table(etab);
   __syncthreads();
-  float *part = ring + (size_t)3 * kRing * ngpt;   // [3][nlev][4]: up, dn, dir
-  int *slot_lev = (int *)(part + (size_t)3 * nlev * 4);
-  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol;
-  const size_t plane = (size_t)ngpt * nlev * ncol;
-  float *wA = ws + cv, *wS = ws + plane + cv;
+  float *part = ring + (size_t)3 * kRingSw * ngpt;   // [3][nlev][4]: up, dn, dir
+  const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
+  const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
+  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol, plane = (size_t)ngpt * nlev * ncol;
+  const ColArr Ttau(tau, cl, row * nlay), Tssa(ssa, cl, row * nlay), Tg(kHasG ? gg : tau, cl, row * nlay);
+  const ColArr WA(ws, cv, row * nlev), WB(ws + plane, cv, row * nlev), WS(ws + 2 * plane, cv, row * nlev),
+      WD(ws + 3 * plane, cv, row * nlev);
   const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
   // "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
   auto lev_above = [&](int l) { return top_at_1 ? l : l + 1; };
   auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
   auto lay_of_down = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };  // j-th layer from the top
   auto lay_of_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };    // j-th layer from the surface
-  const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
+  auto ld_g = [&](uint32_t soff) { return kHasG ? Tg.ld(vg, soff) : 0.0f; };
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   const float Ftop = on ? inc_flux[g + (size_t)ngpt * icol] * mu0 : 0.0f;
 
   // ---- pass 1: direct beam (only tau is read) ----
   float Fd = Ftop;
-  if (on) wA[(size_t)g + (size_t)ngpt * top] = Fd;
+  if (on) WA.st(Fd, vg, row * top);
   {
     float pt[kPF];
 #pragma unroll
-    for (int p = 0; p < kPF; p++) pt[p] = tau[cl + (size_t)gc + (size_t)ngpt * lay_of_down(min(p, nlay - 1))];
+    for (int p = 0; p < kPF; p++) pt[p] = Ttau.ld(vg, row * lay_of_down(min(p, nlay - 1)));
     for (int j0 = 0; j0 < nlay; j0 += kPF) {
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
@@ -446,9 +604,9 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
         if (j < nlay) {
           const int l = lay_of_down(j);
           const float t = pt[p];
-          pt[p] = tau[cl + (size_t)gc + (size_t)ngpt * lay_of_down(min(j + kPF, nlay - 1))];
-          Fd = ref_expf_tab(-t * mu0_inv, etab) * Fd;
-          if (on) wA[(size_t)g + (size_t)ngpt * lev_below(l)] = Fd;
+          pt[p] = Ttau.ld(vg, row * lay_of_down(min(j + kPF, nlay - 1)));
+          Fd = ref_expf_nb(-t * mu0_inv, etab) * Fd;
+          if (on) WA.st(Fd, vg, row * lev_below(l));
         }
       }
     }
@@ -457,15 +615,16 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
   float alb_b = on ? alb_dif[g + (size_t)ngpt * icol] : 0.0f;  // albedo at the level below
   float src_b = on ? Fd * alb_dir[g + (size_t)ngpt * icol] : 0.0f;
   if (on) {
-    wA[(size_t)g + (size_t)ngpt * sfcl] = alb_b;
-    wS[(size_t)g + (size_t)ngpt * sfcl] = src_b;
+    WB.st(alb_b, vg, row * sfcl);
+    WS.st(src_b, vg, row * sfcl);
   }
   {
-    float pt[kPF], pw[kPF], pg[kPF];
+    float pt[kPF], pw[kPF], pg[kPF], pf[kPF];
 #pragma unroll
     for (int p = 0; p < kPF; p++) {
-      const size_t i = cl + (size_t)gc + (size_t)ngpt * lay_of_up(min(p, nlay - 1));
-      pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i];
+      const int l = lay_of_up(min(p, nlay - 1));
+      const uint32_t s = row * l;
+      pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(l));
     }
     for (int j0 = 0; j0 < nlay; j0 += kPF) {
 #pragma unroll
@@ -473,20 +632,21 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
         const int j = j0 + p;
         if (j < nlay) {
           const int l = lay_of_up(j);
-          const float t = pt[p], w0 = pw[p], g0 = pg[p];
+          const float t = pt[p], w0 = pw[p], g0 = pg[p], Fin = pf[p];
           {
-            const size_t i = cl + (size_t)gc + (size_t)ngpt * lay_of_up(min(j + kPF, nlay - 1));
-            pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i];
+            const int ln = lay_of_up(min(j + kPF, nlay - 1));
+            const uint32_t s = row * ln;
+            pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(ln));
           }
-          const size_t ia = (size_t)gc + (size_t)ngpt * lev_above(l);
-          const float Fin = wA[ia];
-          SwCoef c = sw_two_stream(t, w0, g0, mu0, mu0_inv, Fin, etab);
-          float denom = 1.0f / (1.0f - c.Rdif * alb_b);
-          float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
-          float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+          SwCoef c = sw_two_stream(t, w0, kHasG ? g0 : 0.0f, mu0, mu0_inv, Fin, etab);
+          const float denom = rcp_rn_normal(1.0f - c.Rdif * alb_b);
+          const float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
+          const float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
           if (on) {
-            wA[ia] = alb;
-            wS[ia] = src;
+            const uint32_t sa = row * lev_above(l);
+            WB.st(alb, vg, sa);
+            WS.st(src, vg, sa);
+            WD.st(c.Sdn, vg, row * l);
           }
           alb_b = alb;
           src_b = src;
@@ -495,57 +655,49 @@ __global__ void sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1, co
     }
   }
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
-  int nfill = 0;
-  auto stage = [&](float up, float dif, float dir, int level) {
+  auto put = [&](float up, float dif, float dir, int r) {
     if (on) {
-      ring[(size_t)nfill * ngpt + g] = up;
-      ring[((size_t)kRing + nfill) * ngpt + g] = dif;
-      ring[((size_t)2 * kRing + nfill) * ngpt + g] = dir;
-    }
-    if (g == 0) slot_lev[nfill] = level;
-#ifdef RRTMGPNN_ABL_NO_BARRIER
-    return;
-#endif
-    if (++nfill == kRing) {
-      ring_flush(ring, part, slot_lev, 3, nfill, ngpt, nlev, false, true);
-      nfill = 0;
+      ring[(size_t)r * ngpt + g] = up;
+      ring[((size_t)kRingSw + r) * ngpt + g] = dif;
+      ring[((size_t)2 * kRingSw + r) * ngpt + g] = dir;
     }
   };
+  auto flush = [&](int n, int lev0, int dl) {
+#ifndef RRTMGPNN_ABL_NO_BARRIER
+    ring_flush<kRingSw>(ring, part, 3, n, lev0, dl, ngpt, nlev, true);
+#endif
+  };
+  const int dl_dn = top_at_1 ? 1 : -1;
   float Fdn = (on && inc_dif) ? inc_dif[g + (size_t)ngpt * icol] : 0.0f;
-  Fd = Ftop;
-  stage(Fdn * alb_b + src_b, Fdn, Fd, top);  // Eq 12 at the top; alb_b/src_b hold the top level's values
+  put(Fdn * alb_b + src_b, Fdn, Ftop, 0);  // Eq 12 at the top; alb_b/src_b hold the top level's values
+  flush(1, top, 1);
   {
-    float pt[kPF], pw[kPF], pg[kPF], pa[kPF], ps[kPF];
+    float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF];
+    auto load = [&](int p, int l) {
+      const uint32_t s = row * l, sb = row * lev_below(l);
+      pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pd[p] = WD.ld(vg, s);
+      pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb); pf[p] = WA.ld(vg, sb);
+    };
 #pragma unroll
-    for (int p = 0; p < kPF; p++) {
-      const int l = lay_of_down(min(p, nlay - 1));
-      const size_t i = cl + (size_t)gc + (size_t)ngpt * l, ib = (size_t)gc + (size_t)ngpt * lev_below(l);
-      pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i]; pa[p] = wA[ib]; ps[p] = wS[ib];
-    }
-    for (int j0 = 0; j0 < nlay; j0 += kPF) {
+    for (int p = 0; p < kPF; p++) load(p, lay_of_down(min(p, nlay - 1)));
+    for (int j0 = 0; j0 < nlay; j0 += kRingSw) {
 #pragma unroll
-      for (int p = 0; p < kPF; p++) {
-        const int j = j0 + p;
+      for (int r = 0; r < kRingSw; r++) {
+        const int j = j0 + r, p = r % kPF;
         if (j < nlay) {
-          const int l = lay_of_down(j);
-          const float t = pt[p], w0 = pw[p], g0 = pg[p], alb = pa[p], src = ps[p];
-          {
-            const int ln = lay_of_down(min(j + kPF, nlay - 1));
-            const size_t i = cl + (size_t)gc + (size_t)ngpt * ln, ib = (size_t)gc + (size_t)ngpt * lev_below(ln);
-            pt[p] = tau[i]; pw[p] = ssa[i]; pg[p] = gg[i]; pa[p] = wA[ib]; ps[p] = wS[ib];
-          }
-          // recompute the layer's coefficients exactly as pass 2 did (same inputs, same F_dir -> same bits)
-          SwCoef c = sw_two_stream(t, w0, g0, mu0, mu0_inv, Fd, etab);
-          const float denom = 1.0f / (1.0f - c.Rdif * alb);
-          Fdn = (c.Tdif * Fdn + c.Rdif * src + c.Sdn) * denom;  // Eq 13 (adding :1583-1591)
-          const float up = Fdn * alb + src;                      // Eq 12
-          Fd = c.Tnoscat * Fd;
-          stage(up, Fdn, Fd, lev_below(l));
+          const float t = pt[p], w0 = pw[p], g0 = pg[p], Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
+          load(p, lay_of_down(min(j + kPF, nlay - 1)));
+          // R_dif, T_dif exactly as pass 2 computed them (same inputs, same expressions -> same bits)
+          const SwDif d = sw_dif(t, w0, kHasG ? g0 : 0.0f, etab);
+          const float denom = rcp_rn_normal(1.0f - d.Rdif * alb);
+          Fdn = (d.Tdif * Fdn + d.Rdif * src + Sdn) * denom;  // Eq 13 (adding :1583-1591)
+          const float up = Fdn * alb + src;                    // Eq 12
+          put(up, Fdn, Fdir, r);
         }
       }
+      flush(min(kRingSw, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
     }
   }
-  if (nfill) ring_flush(ring, part, slot_lev, 3, nfill, ngpt, nlev, false, true);
   for (int l = g; l < nlev; l += blockDim.x) {
     flux_up[l + (size_t)nlev * icol] = combine4(part + 4 * l);
     flux_dn[l + (size_t)nlev * icol] = combine4(part + (size_t)nlev * 4 + 4 * l);
@@ -558,16 +710,21 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
                       const float *alb_dir, const float *alb_dif, float *flux_up, float *flux_dn, float *flux_dir)
 {
   if (ncol == 0) return RRTMGPNN_OK;
-  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: ngpt > 1024");
+  if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
   void *ws = nullptr;
-  int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
+  int rc = ctx->workspace(sizeof(float) * 4 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
   if (rc) return rc;
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRing * ngpt + (size_t)3 * (nlay + 1) * 4) + sizeof(int) * kRing;
+  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRingSw * ngpt + (size_t)3 * (nlay + 1) * 4);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
-  hipLaunchKernelGGL(sw_2stream_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1,
-                     inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, (float *)ws, flux_up, flux_dn,
-                     flux_dir);
+  if (g)
+    hipLaunchKernelGGL((sw_2stream_kernel<true, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
+                       nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, (float *)ws,
+                       flux_up, flux_dn, flux_dir);
+  else
+    hipLaunchKernelGGL((sw_2stream_kernel<false, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream,
+                       ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif,
+                       (float *)ws, flux_up, flux_dn, flux_dir);
   RRTMGPNN_LAUNCH_CHECK("sw_2stream_kernel");
   return RRTMGPNN_OK;
 }

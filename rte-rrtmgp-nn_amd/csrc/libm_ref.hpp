@@ -57,6 +57,56 @@ __device__ __forceinline__ float ref_expf_tab(float x, const uint64_t *tab)
 
 __device__ __forceinline__ float ref_expf(float x) { return ref_expf_tab(x, kExpTab); }
 
+// Branch-free form for the solvers' inner loops: the main path is evaluated for every x and glibc's
+// over/underflow cases are applied by selection afterwards (x < -0x1.9fe368p6: 0, including -inf;
+// x > 0x1.62e42ep6: +inf).  A nan propagates through the main path (glibc returns x + x: also a nan).
+// For every other x, including the |x| >= 88 band glibc also sends through the main path, the
+// arithmetic is the same as ref_expf_tab's.  No divergent branch, so the scheduler interleaves
+// consecutive exps with the surrounding arithmetic.
+__device__ __forceinline__ float ref_expf_nb(float x, const uint64_t *tab)
+{
+  const double InvLn2N = 0x1.71547652b82fep+0 * 32, SHIFT = 0x1.8p+52;
+  const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+               C2 = 0x1.62e42ff0c52d6p-1 / 32;
+  const double xd = (double)x;
+  double kd = __fma_rn(InvLn2N, xd, SHIFT);
+  const uint64_t ki = f64_as_u64(kd);
+  kd -= SHIFT;
+  const double r = __fma_rn(InvLn2N, xd, -kd);
+  const double s = u64_as_f64(tab[ki % 32] + (ki << 47));
+  const double z = __fma_rn(C0, r, C1), r2 = r * r;
+  double y = __fma_rn(C2, r, 1.0);
+  y = __fma_rn(z, r2, y);
+  float res = (float)(y * s);
+  res = (x < -0x1.9fe368p6f) ? 0.0f : res;
+  res = (x > 0x1.62e42ep6f) ? __int_as_float(0x7f800000) : res;
+  return res;
+}
+
+// Correctly rounded sqrtf for normal positive x (the solvers call it on max(., 1e-4)): the hardware
+// estimate corrected by one ulp either way, the same steps the compiler emits for sqrtf minus the
+// denormal pre-scaling and the zero/inf class test, which never fire in that range.
+__device__ __forceinline__ float sqrt_rn_normal(float x)
+{
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float em = fmaf(-sm, s, x), ep = fmaf(-sp, s, x);
+  float r = (em <= 0.0f) ? sm : s;
+  return (ep > 0.0f) ? sp : r;
+}
+
+// Correctly rounded 1/b for b in [2^-60, 2^60] (the solvers' denominators: k(1+e^-2k tau)+... and
+// 1 - R_dif*albedo): the compiler's IEEE division sequence minus v_div_scale / v_div_fixup, which
+// leave the operands and the result untouched in that range, so the bits are those of 1.0f / b.
+__device__ __forceinline__ float rcp_rn_normal(float b)
+{
+  float r = __builtin_amdgcn_rcpf(b);
+  r = fmaf(fmaf(-b, r, 1.0f), r, r);
+  float q = r;                       // 1 * r
+  q = fmaf(fmaf(-b, q, 1.0f), r, q);
+  return fmaf(fmaf(-b, q, 1.0f), r, q);
+}
+
 // Copy the exp table into LDS (call with all threads of the block; a __syncthreads() must follow).
 __device__ __forceinline__ void load_exp_table(uint64_t *lds_tab)
 {

@@ -6,6 +6,12 @@ One `ClearSkyStep` owns every input and output of one column block in HBM and re
 with the same kernels as the class-level API (api.py), but with all ctypes arguments prepared once
 so the host cost per step is just the launches (or one hipGraph replay).
 
+fused=True (default) keeps intermediates that the flux computation does not need out of HBM: the
+Planck sources are formed inside the LW solver from the Planck fraction
+(rrtmgpnn_lw_solver_noscat_planck: same products, same bits, compute_Planck_source_nn's arrays never
+stored), and the SW asymmetry parameter -- identically zero in the NN path -- is passed as NULL
+instead of being written and re-read.  fused=False issues exactly the class layer's call sequence.
+
 What one step computes is exactly the drivers' per-block work
 (examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:399-441, rrtmgp_rfmip_sw.F90:374-451):
 compute_nn_inputs, get_col_dry, both NN models per stream with post-processing, the Planck sources,
@@ -28,8 +34,9 @@ def _t(a, dev):
 
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
-                 sw_models=("sw_abs", "sw_ray")):
+                 sw_models=("sw_abs", "sw_ray"), fused=True):
         self.dev = torch.device("cuda", device)
+        self.fused = fused
         self.ctx = ctx or Context(device)
         L = self.L = _lib.lib()
         self.kd_lw, self.kd_sw = data.load_kdist("lw"), data.load_kdist("sw")
@@ -66,9 +73,12 @@ class ClearSkyStep:
         self.col_dry = f(ncol, nlay)
         self.x_lw, self.x_sw = f(ncol, nlay, self.nx_lw), f(ncol, nlay, self.nx_sw)
         self.tau_lw, self.lay_src = f(ncol, nlay, self.ng_lw), f(ncol, nlay, self.ng_lw)
-        self.lev_src = f(ncol, nlay + 1, self.ng_lw)
-        self.sfc_src, self.sfc_jac, self.emis_gpt = f(ncol, self.ng_lw), f(ncol, self.ng_lw), f(ncol, self.ng_lw)
-        self.tau_sw, self.ssa_sw, self.g_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
+        self.emis_gpt = f(ncol, self.ng_lw)
+        self.tau_sw, self.ssa_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
+        if not fused:  # arrays the fused step never materialises
+            self.lev_src = f(ncol, nlay + 1, self.ng_lw)
+            self.sfc_src, self.sfc_jac = f(ncol, self.ng_lw), f(ncol, self.ng_lw)
+            self.g_sw = f(ncol, nlay, self.ng_sw)
         self.lw_up, self.lw_dn = f(ncol, nlay + 1), f(ncol, nlay + 1)
         self.sw_up, self.sw_dn, self.sw_dir = f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1)
 
@@ -98,25 +108,46 @@ class ClearSkyStep:
             ("predict_nn_lw", L.rrtmgpnn_predict_nn_lw,
              (c, ncol, nlay, self.ng_lw, self.nx_lw, p(self.x_lw), p(self.col_dry), self._nets_lw, len(self.lw_nets),
               p(self.tau_lw), p(self.lay_src))),
-            ("planck_source", L.rrtmgpnn_compute_planck_source_nn,
-             (c, ncol, nlay, self.nb_lw, self.ng_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev),
-              p(self.tsfc), self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]),
-              float(self.kd_lw["totplnk_delta"]), p(self.totplnk), p(self.sfc_src), p(self.sfc_jac),
-              p(self.lay_src), p(self.lev_src))),
-            ("expand_emis", L.rrtmgpnn_expand_band_to_gpt,
-             (c, self.nb_lw, self.ng_lw, ncol, self._lims_lw, p(self.sfc_emis), p(self.emis_gpt))),
-            ("lw_solver", L.rrtmgpnn_lw_solver_noscat,
-             (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None, p(self.tau_lw),
-              p(self.lay_src), p(self.lev_src), p(self.emis_gpt), p(self.sfc_src), p(self.lw_up), p(self.lw_dn))),
+        ]
+        if fused:
+            # compute_Planck_source_nn fused into the LW solver (sources formed in-kernel from pfrac)
+            lw_calls = [
+                ("expand_emis", L.rrtmgpnn_expand_band_to_gpt,
+                 (c, self.nb_lw, self.ng_lw, ncol, self._lims_lw, p(self.sfc_emis), p(self.emis_gpt))),
+                ("lw_solver", L.rrtmgpnn_lw_solver_noscat_planck,
+                 (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None, p(self.tau_lw),
+                  p(self.lay_src), self.nb_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev), p(self.tsfc),
+                  self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]),
+                  float(self.kd_lw["totplnk_delta"]), p(self.totplnk), p(self.emis_gpt), p(self.lw_up),
+                  p(self.lw_dn))),
+            ]
+        else:
+            lw_calls = [
+                ("planck_source", L.rrtmgpnn_compute_planck_source_nn,
+                 (c, ncol, nlay, self.nb_lw, self.ng_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev),
+                  p(self.tsfc), self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]),
+                  float(self.kd_lw["totplnk_delta"]), p(self.totplnk), p(self.sfc_src), p(self.sfc_jac),
+                  p(self.lay_src), p(self.lev_src))),
+                ("expand_emis", L.rrtmgpnn_expand_band_to_gpt,
+                 (c, self.nb_lw, self.ng_lw, ncol, self._lims_lw, p(self.sfc_emis), p(self.emis_gpt))),
+                ("lw_solver", L.rrtmgpnn_lw_solver_noscat,
+                 (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None, p(self.tau_lw),
+                  p(self.lay_src), p(self.lev_src), p(self.emis_gpt), p(self.sfc_src), p(self.lw_up), p(self.lw_dn))),
+            ]
+        self.calls += lw_calls
+        # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
+        # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
+        g_sw = None if fused else p(self.g_sw)
+        self.calls += [
             ("nn_inputs_sw", L.rrtmgpnn_compute_nn_inputs,
              (c, ncol, nlay, self.nx_sw, p(self.play), p(self.tlay), self._g_sw, self._nd_sw, self.sw_nets[0],
               p(self.x_sw))),
             ("predict_nn_sw", L.rrtmgpnn_predict_nn_sw,
              (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.x_sw), p(self.col_dry), self._nets_sw, p(self.tau_sw),
-              p(self.ssa_sw), p(self.g_sw))),
+              p(self.ssa_sw), g_sw)),
             ("sw_solver", L.rrtmgpnn_sw_solver_2stream,
              (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
-              p(self.g_sw), p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
+              g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
         ]
         self.graph = None
 

@@ -1,0 +1,106 @@
+"""GPU: the fused entry points are bit-identical to the class layer's call sequence.
+
+* rrtmgpnn_lw_solver_noscat_planck (Planck sources formed in-kernel from pfrac) ==
+  compute_planck_source_nn + lw_solver_noscat, and == the oracle, for nmus 1-4 and both orientations;
+* rrtmgpnn_sw_solver_2stream with g == NULL == the same call with a zero-filled g;
+* the fused ClearSkyStep (the benchmarked step) == the unfused one, bit for bit.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import subset
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    torch.cuda.set_device(0)
+    return torch.device("cuda", 0)
+
+
+def T(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
+
+
+def _flip(prob):
+    out = dict(prob)
+    for k in ("play", "plev", "tlay", "tlev"):
+        out[k] = np.ascontiguousarray(prob[k][:, ::-1])
+    out["gases"] = {k: np.ascontiguousarray(v[:, ::-1]) for k, v in prob["gases"].items()}
+    out["top_at_1"] = False
+    return out
+
+
+@pytest.mark.parametrize("nmus", [1, 2, 3, 4])
+@pytest.mark.parametrize("top_at_1", [True, False])
+def test_fused_lw_solver_matches_oracle(dev, orc, rfmip, nmus, top_at_1):
+    from rrtmgpnn import _lib, data
+    from rrtmgpnn._lib import check, float_array, int_array
+    from rrtmgpnn.api import GAUSS_DS, GAUSS_WTS, context
+    prob = subset(rfmip, np.arange(5, 1800, 13))
+    if not top_at_1:
+        prob = _flip(prob)
+    kd = data.load_kdist("lw")
+    go = orc.lw_gas_optics(prob, [data.load_model("lw_abs"), data.load_model("lw_pfrac")], kd)
+    ncol, nlay, ngpt = go["tau"].shape
+    emis = np.repeat(np.asarray(prob["sfc_emis"], np.float32)[:, None], ngpt, axis=1)
+    up_o, dn_o = orc.lw_solver(go["tau"], go["lay_source"], go["lev_source"], emis, go["sfc_source"], top_at_1, nmus)
+    sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
+    up, dn = torch.empty((ncol, nlay + 1), device=dev), torch.empty((ncol, nlay + 1), device=dev)
+    args = [T(go["tau"], dev), T(go["pfrac"], dev), T(prob["tlay"], dev), T(prob["tlev"], dev), T(prob["tsfc"], dev),
+            T(kd["totplnk"], dev), T(emis, dev)]
+    ctx = context(0)
+    check(_lib.lib().rrtmgpnn_lw_solver_noscat_planck(
+        ctx.h, ngpt, nlay, ncol, int(top_at_1), nmus, float_array(GAUSS_DS[nmus]), float_array(GAUSS_WTS[nmus]), None,
+        args[0].data_ptr(), args[1].data_ptr(), kd["nband"], kd["nPlanckTemp"], args[2].data_ptr(),
+        args[3].data_ptr(), args[4].data_ptr(), sfc_lay, int_array(kd["band_lims_gpt"].ravel()),
+        float(kd["temp_ref_min"][0]), float(kd["totplnk_delta"]), args[5].data_ptr(), args[6].data_ptr(),
+        up.data_ptr(), dn.data_ptr()), "lw_solver_noscat_planck")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(up.cpu().numpy(), up_o)
+    np.testing.assert_array_equal(dn.cpu().numpy(), dn_o)
+
+
+@pytest.mark.parametrize("top_at_1", [True, False])
+def test_sw_null_g_equals_zero_g(dev, top_at_1):
+    from rrtmgpnn import _lib
+    from rrtmgpnn._lib import check
+    from rrtmgpnn.api import context
+    rng = np.random.default_rng(11)
+    ncol, nlay, ngpt = 41, 37, 224
+    tau = T(rng.lognormal(-2, 2, size=(ncol, nlay, ngpt)), dev)
+    ssa = T(rng.uniform(0, 1, size=(ncol, nlay, ngpt)), dev)
+    zero = torch.zeros_like(tau)
+    mu0 = T(rng.uniform(0.05, 1, size=ncol), dev)
+    inc = T(rng.uniform(0, 10, size=(ncol, ngpt)), dev)
+    ad, af = T(rng.uniform(0, 1, size=(ncol, ngpt)), dev), T(rng.uniform(0, 1, size=(ncol, ngpt)), dev)
+    outs = []
+    for g in (zero, None):
+        o = [torch.empty((ncol, nlay + 1), device=dev) for _ in range(3)]
+        check(_lib.lib().rrtmgpnn_sw_solver_2stream(
+            context(0).h, ngpt, nlay, ncol, int(top_at_1), inc.data_ptr(), None, tau.data_ptr(), ssa.data_ptr(),
+            None if g is None else g.data_ptr(), mu0.data_ptr(), ad.data_ptr(), af.data_ptr(), *[t.data_ptr() for t in o]),
+            "sw_solver_2stream")
+        torch.cuda.synchronize()
+        outs.append([t.cpu().numpy() for t in o])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_fused_step_equals_class_sequence(dev, rfmip):
+    from rrtmgpnn.pipeline import ClearSkyStep
+    prob = subset(rfmip, np.arange(2, 1800, 3))
+    res = []
+    for fused in (False, True):
+        step = ClearSkyStep(prob, device=0, fused=fused)
+        step.step()
+        torch.cuda.synchronize()
+        res.append(step.fluxes())
+    for k in res[0]:
+        np.testing.assert_array_equal(res[0][k], res[1][k], err_msg=k)
