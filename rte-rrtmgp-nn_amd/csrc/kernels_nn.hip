@@ -151,6 +151,25 @@ __device__ __forceinline__ float activate(int act, float x)
   }
 }
 
+// Compile-time activation sets of the fused kernel: ACTS == 1 is the shipped models' softsign,
+// softsign, linear (Appendix A of SURVEY.md), inlined straight-line; ACTS == 0 dispatches on the
+// runtime codes (any other combination).
+template <int ACTS>
+__device__ __forceinline__ float act_hidden(int act, float x)
+{
+#ifdef RRTMGPNN_ABL_MLP_CHEAP_ACT  // ablation only: breaks parity
+  if constexpr (ACTS == 1) return x * 0.5f;
+#endif
+  if constexpr (ACTS == 1) return x / (fabsf(x) + 1.0f);  // softsign (mod_activation.F90:107-128)
+  else return activate(act, x);
+}
+template <int ACTS>
+__device__ __forceinline__ float act_out(int act, float x)
+{
+  if constexpr (ACTS == 1) return x;  // linear
+  else return activate(act, x);
+}
+
 // ------------------------------------------------------------------------------------------
 // Packed image layout (floats) of a 3-layer network [nx, h1, h2, ny]:
 //   K1S = ceil(nx/4), H1T = ceil(h1/16), H2T = ceil(h2/16), NGT = ceil(ny/16)
@@ -255,7 +274,7 @@ __device__ __forceinline__ float pow8(float t)
 }
 
 // Hidden layers of one network for a 16-sample tile: returns H2 accumulators.
-template <int K1S, int H1T, int H2T>
+template <int K1S, int H1T, int H2T, int ACTS>
 __device__ __forceinline__ void mlp_hidden(const float *__restrict__ img, int NGT, const float (&xv)[K1S], int lane,
                                            int act1, int act2, floatx4 (&h2)[H2T])
 {
@@ -269,7 +288,7 @@ __device__ __forceinline__ void mlp_hidden(const float *__restrict__ img, int NG
     for (int t = 0; t < K1S; t++)
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(img[L.l1 + (mo * K1S + t) * 64 + lane], xv[t], acc, 0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < 4; r++) acc[r] = activate(act1, acc[r] + img[L.b1 + 16 * mo + 4 * q + r]);
+    for (int r = 0; r < 4; r++) acc[r] = act_hidden<ACTS>(act1, acc[r] + img[L.b1 + 16 * mo + 4 * q + r]);
     h1[mo] = acc;
   }
 #pragma unroll
@@ -282,7 +301,7 @@ __device__ __forceinline__ void mlp_hidden(const float *__restrict__ img, int NG
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(img[L.l2 + (mo * 4 * H1T + 4 * m + t) * 64 + lane], h1[m][t], acc,
                                                    0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < 4; r++) acc[r] = activate(act2, acc[r] + img[L.b2 + 16 * mo + 4 * q + r]);
+    for (int r = 0; r < 4; r++) acc[r] = act_hidden<ACTS>(act2, acc[r] + img[L.b2 + 16 * mo + 4 * q + r]);
     h2[mo] = acc;
   }
 }
@@ -301,9 +320,17 @@ __device__ __forceinline__ floatx4 mlp_out_tile(const float *__restrict__ img, i
   return acc;
 }
 
-constexpr int kMlpThreads = 512;
+// Threads per MLP block (tools/solver_variants.sh knob): the weight images live once per block in LDS,
+// so a wider block raises the waves per SIMD that share one copy of them.
+#ifndef RRTMGPNN_MLP_THREADS
+#define RRTMGPNN_MLP_THREADS 512
+#endif
+#ifndef RRTMGPNN_MLP_GO_UNROLL
+#define RRTMGPNN_MLP_GO_UNROLL 1
+#endif
+constexpr int kMlpThreads = RRTMGPNN_MLP_THREADS, kGoUnroll = RRTMGPNN_MLP_GO_UNROLL;
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE>
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS>
 __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -317,7 +344,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
   const float *imgA = lds;
   const float *imgB = lds + a.imgA_floats;
   const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
-  const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;
   const int NGT = a.ngt, nx = a.nx, ngpt = a.ngpt;
   const ImgLayout LA = img_layout(AK, AH1, AH2, NGT);
   const ImgLayout LB = img_layout(BK, BH1, BH2, NGT);
@@ -336,11 +363,11 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
       }
     }
     floatx4 hA[AH2];
-    mlp_hidden<AK, AH1, AH2>(imgA, NGT, xv, lane, a.actA[0], a.actA[1], hA);
+    mlp_hidden<AK, AH1, AH2, ACTS>(imgA, NGT, xv, lane, a.actA[0], a.actA[1], hA);
     floatx4 hB[BH2];
     if constexpr (MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) {
       static_assert(BK == AK, "paired networks share their inputs");
-      mlp_hidden<BK, BH1, BH2>(imgB, NGT, xv, lane, a.actB[0], a.actB[1], hB);
+      mlp_hidden<BK, BH1, BH2, ACTS>(imgB, NGT, xv, lane, a.actB[0], a.actB[1], hB);
     }
     // Per-lane sample rows of the output tile: s = s0 + 4q + r
     float cd[4];
@@ -357,6 +384,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
         cd[r] = s < a.nbatch ? a.col_dry[s] : 0.0f;
       }
     }
+#pragma unroll kGoUnroll
     for (int go = 0; go < NGT; go++) {
       const int g = 16 * go + j;
       floatx4 yA = mlp_out_tile<AH2>(imgA, LA.l3, go, hA, lane);
@@ -366,7 +394,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           long long s = s0 + 4 * q + r;
-          if (s < a.nbatch && g < ny) a.out0[(size_t)s * ny + g] = activate(a.actA[2], yA[r] + bA);
+          if (s < a.nbatch && g < ny) a.out0[(size_t)s * ny + g] = act_out<ACTS>(a.actA[2], yA[r] + bA);
         }
       } else if constexpr (MODE == MLP_LW_BOTH) {
         // single model, outputs [0,ngpt) -> tau, [ngpt, 2 ngpt) -> pfrac (mo_gas_optics_kernels.F90:754-766)
@@ -405,9 +433,15 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
               if (s >= a.nbatch || g >= ngpt) continue;
               float t = sdA * (yA[r] + bA);
               t = t + mnA;
-              a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];  // tau
               float p = yB[r] + bB;
-              a.out1[(size_t)s * ngpt + g] = p * p;  // pfrac
+#ifdef RRTMGPNN_ABL_MLP_NOSTORE  // ablation only: stores skipped unless the value is a nan
+              if (t != t || p != p) {
+#else
+              {
+#endif
+                a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];  // tau
+                a.out1[(size_t)s * ngpt + g] = p * p;            // pfrac
+              }
             }
           } else {  // MLP_SW_PAIR
             const float sdB = imgB[LB.sd + g], mnB = imgB[LB.mn + g];
@@ -433,10 +467,10 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
   }
 }
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE>
-static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS>
+static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
 {
-  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE>;
+  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS>;
   size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
   // Raise the dynamic-LDS limit once per instantiation (kept out of the per-call path so the launch
@@ -456,6 +490,18 @@ static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kMlpThreads), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp_pair_kernel");
   return RRTMGPNN_OK;
+}
+
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE>
+static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
+{
+  const bool pair = MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR;
+  auto std_acts = [](const int *act) {
+    return act[0] == RRTMGPNN_ACT_SOFTSIGN && act[1] == RRTMGPNN_ACT_SOFTSIGN && act[2] == RRTMGPNN_ACT_LINEAR;
+  };
+  if (std_acts(a.actA) && (!pair || std_acts(a.actB)))
+    return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1>(ctx, a);
+  return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 0>(ctx, a);
 }
 
 // Shape dispatch: the shipped models (Appendix A of SURVEY.md).

@@ -1,5 +1,5 @@
-"""Time the LW/SW solver kernels of each variant build (tools/solver_variants.sh) on one config's inputs and
-check every variant's fluxes bit for bit against the first variant."""
+"""Time every stage of the fused step (and the unfused LW/SW solvers) for each variant build
+(tools/solver_variants.sh), checking each variant's fluxes bit for bit against the first variant."""
 import ctypes
 import os
 import sys
@@ -15,48 +15,68 @@ from rrtmgpnn.pipeline import ClearSkyStep  # noqa: E402
 B, config, names = sys.argv[1], sys.argv[2], sys.argv[3:]
 prob = data.rfmip_problem() if config == "c3" else data.synthetic_problem(10000 if config == "c4" else 125000,
                                                                          60 if config == "c4" else 137)
-steps = {"": ClearSkyStep(prob, device=0, fused=False), "fused_": ClearSkyStep(prob, device=0, fused=True)}
-calls, outs = {}, {}
-for tag, step in steps.items():
-    step.step()
-    torch.cuda.synchronize()
-    for n, fn, a in step.calls:
-        if n in ("lw_solver", "sw_solver"):
-            calls[tag + n] = (n, a)
-    outs[tag + "lw_solver"] = (step.lw_up, step.lw_dn)
-    outs[tag + "sw_solver"] = (step.sw_up, step.sw_dn, step.sw_dir)
-first = {}
-for v in names:
-    L = ctypes.CDLL(os.path.join(B, "lib_%s.so" % v))
+steps = {"": ClearSkyStep(prob, device=0, fused=False), "f:": ClearSkyStep(prob, device=0, fused=True)}
+for st in steps.values():
+    st.step()
+torch.cuda.synchronize()
+SHOW = {"": ("lw_solver", "sw_solver"), "f:": ("predict_nn_lw", "lw_solver", "predict_nn_sw", "sw_solver", "nn_inputs_lw")}
+first = None
+
+
+def bind(L):
     for name, (res, args) in _lib.SIGNATURES.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
+
+
+for v in names:
+    L = ctypes.CDLL(os.path.join(B, "lib_%s.so" % v))
+    bind(L)
     h = _lib.c_vp()
     assert L.rrtmgpnn_context_create(0, None, h) == 0
-    line = []
-    fns = {"lw_solver": L.rrtmgpnn_lw_solver_noscat, "fused_lw_solver": L.rrtmgpnn_lw_solver_noscat_planck,
-           "sw_solver": L.rrtmgpnn_sw_solver_2stream, "fused_sw_solver": L.rrtmgpnn_sw_solver_2stream}
-    for name, fn in fns.items():
-        a = list(calls[name][1])
-        a[0] = h
-        for t in outs[name]:
+    line, res = [], []
+    for tag, st in steps.items():
+        # the networks are loaded through the variant library too (its packed MLP images)
+        calls = []
+        for name, fn, a in st.calls:
+            a = list(a)
+            a[0] = h
+            calls.append((name, getattr(L, fn.__name__), a))
+        nets = {}
+        for m in ("lw_abs", "lw_pfrac", "sw_abs", "sw_ray"):
+            hh = _lib.c_vp()
+            assert L.rrtmgpnn_network_load(h, data.path(m).encode(), hh) == 0
+            nets[m] = hh.value
+        keep = []
+        for name, fn, a in calls:
+            if name.startswith("predict_nn"):
+                models = ("lw_abs", "lw_pfrac") if "lw" in name else ("sw_abs", "sw_ray")
+                arr = (ctypes.c_void_p * 2)(*[nets[m] for m in models])
+                keep.append(arr)
+                a[7] = arr
+            elif name.startswith("nn_inputs"):
+                a[8] = ctypes.c_void_p(nets["lw_abs" if "lw" in name else "sw_abs"])
+        for t in (st.lw_up, st.lw_dn, st.sw_up, st.sw_dn, st.sw_dir):
             t.fill_(float("nan"))
-        rc = fn(*a)
+        for name, fn, a in calls:
+            assert fn(*a) == 0, name
         torch.cuda.synchronize()
-        if rc:
-            line.append("%s FAILED rc=%d" % (name, rc))
-            continue
-        res = [t.cpu().numpy().copy() for t in outs[name]]
-        if name not in first:
-            first[name] = res
-            same = "ref"
-        else:
-            same = "bitwise" if all(np.array_equal(x, y) for x, y in zip(res, first[name])) else "DIFFERS"
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(20):
-            fn(*a)
-        e1.record()
-        e1.synchronize()
-        line.append("%s %.4f ms (%s)" % (name, e0.elapsed_time(e1) / 20, same))
-    print("%-14s" % v, " | ".join(line), flush=True)
+        res += [t.cpu().numpy().copy() for t in (st.lw_up, st.lw_dn, st.sw_up, st.sw_dn, st.sw_dir)]
+        for name, fn, a in calls:
+            if name not in SHOW[tag]:
+                continue
+            best = 1e9
+            for _ in range(2):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(20):
+                    fn(*a)
+                e1.record()
+                e1.synchronize()
+                best = min(best, e0.elapsed_time(e1) / 20)
+            line.append("%s%s %.4f" % (tag, name, best))
+    if first is None:
+        first, same = res, "ref"
+    else:
+        same = "bitwise" if all(np.array_equal(x, y) for x, y in zip(res, first)) else "DIFFERS"
+    print("%-10s [%s] " % (v, same) + " | ".join(line), flush=True)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build solver-kernel variants (compile-time knobs of csrc/kernels_rte.hip) and time them on the GPU box
+# Build kernel variants (compile-time knobs of csrc/kernels_rte.hip and csrc/kernels_nn.hip) and time them on the GPU box
 # in one process, checking each variant's fluxes bit for bit against the first one.
 # Usage: bash tools/solver_variants.sh "name1:-DFOO=1 -DBAR=2" "name2:..." ...
 set -e
@@ -8,15 +8,15 @@ PKG=rte-rrtmgp-nn_amd
 B=${TMPDIR:-/tmp}/rrtmgpnn_var
 rm -rf $B; mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off"
-/opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/kernels_nn.hip -o $B/nn.o &
 /opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/api.cpp -o $B/api.o &
 names=()
 for spec in "$@"; do
   n=${spec%%:*}; d=${spec#*:}; names+=($n)
   /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_rte.hip -o $B/rte_$n.o &
+  /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_nn.hip -o $B/nn_$n.o &
 done
 wait
 for n in "${names[@]}"; do
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/api.o $B/nn.o $B/rte_$n.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/api.o $B/nn_$n.o $B/rte_$n.o
 done
 python3 tools/solver_variants.py $B ${CONFIG:-c3} "${names[@]}"
