@@ -61,7 +61,7 @@ def stage_work(name, step):
     N = ncol * nlay
     glw, gsw = step.ng_lw, step.ng_sw
     f4 = 4
-    nsw_out = 2 if step.fused else 3  # tau, ssa (+ g when it is materialised)
+    nsw_out = 2 if (step.fused and not step.allsky) else 3  # tau, ssa (+ g when it is materialised)
     if name == "predict_nn_lw":
         from rrtmgpnn import data
         fl = sum(mlp_flops([int(v) for v in data.load_model(m)["dims"]]) for m in ("lw_abs", "lw_pfrac"))
@@ -79,6 +79,16 @@ def stage_work(name, step):
     if name == "sw_solver":
         # tau, ssa (, g) (G x L) + toa, alb_dir, alb_dif (G) + mu0 read; up/dn/dir written
         return "byte", ncol * ((nsw_out * gsw * nlay + 3 * gsw + 1) * f4 + 3 * (nlay + 1) * f4), None, None
+    if name in ("cloud_optics_lw", "cloud_optics_sw"):
+        # lwp, iwp, rel, rei read; 1 (LW 1scl) or 3 (SW 2str) by-band arrays written
+        nb = step.nb_lw if name.endswith("lw") else step.nb_sw
+        return "byte", N * (4 + (1 if name.endswith("lw") else 3) * nb) * f4, None, None
+    if name == "delta_scale_sw":
+        return "byte", N * 6 * step.nb_sw * f4, None, None
+    if name == "increment_lw":
+        return "byte", N * (2 * glw + step.nb_lw) * f4, None, None
+    if name == "increment_sw":
+        return "byte", N * (6 * gsw + 3 * step.nb_sw) * f4, None, None
     if name == "planck_source":
         # pfrac read, lay (in place) + lev + sfc + sfcJac written
         return "byte", ncol * ((glw * nlay + glw * nlay + glw * (nlay + 1) + 2 * glw) * f4), None, None
@@ -102,19 +112,23 @@ def main():
     from rrtmgpnn import data
     from rrtmgpnn.pipeline import ClearSkyStep
 
+    clouds = None
     if args.config == "c3":
         prob = data.rfmip_problem()
         workload = "C3: RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics (g256 LW + g224 SW)"
         data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
     elif args.config == "c4":
         prob = data.synthetic_problem(10000, 60, seed=20251015 + rank)
-        workload = "C4-shaped clear-sky: 10000 synthetic columns x 60 layers (clouds not yet included)"
-        data_desc = "synthetic columns drawn from RFMIP profiles (PCG64 seed 20251015+rank)"
+        clouds = data.allsky_clouds(prob, data.load_cloud_optics("lw"))
+        workload = ("C4: all-sky LW+SW, 10000 synthetic columns x 60 layers, NN gas optics + cloud_optics (LUT, ice "
+                    "roughness 2; LW 1scl increment, SW delta-scaled 2str increment)")
+        data_desc = ("synthetic columns drawn from RFMIP profiles (PCG64 seed 20251015+rank); clouds by the all-sky "
+                     "example's recipe (rrtmgp_allsky.F90:329-350); the reference's cloud-optics coefficients")
     else:
         prob = data.synthetic_problem(125000, 137, seed=20251015 + rank)
         workload = "C5 shard: 125000 synthetic columns x 137 layers per GPU, clear-sky LW+SW"
         data_desc = "synthetic columns interpolated from RFMIP profiles (PCG64 seed 20251015+rank)"
-    step = ClearSkyStep(prob, device=local, fused=not args.unfused)
+    step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds)
     ncol, nlay = step.ncol, step.nlay
 
     use_graph = not args.no_graph
@@ -246,6 +260,8 @@ def main():
     # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if clouds is not None:
+            prob = dict(prob, **dict(zip(("lwp", "iwp", "rel", "rei"), clouds)))
         cpu = cpu_baseline(prob, args.cpu_seconds, args.cpu_kind)
 
     if rank == 0:
@@ -256,7 +272,8 @@ def main():
             "config": {"workload": workload, "ncol_per_gpu": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
                        "ngpt_sw": step.ng_sw, "parallelism": "column-sharded, 1 process per GPU",
                        "launch": "hipGraph replay" if use_graph else "eager",
-                       "kernels": "fused Planck-in-LW-solver, g=0 elided" if step.fused else "class-layer sequence"},
+                       "kernels": ("class-layer sequence" if not step.fused else "fused Planck-in-LW-solver" +
+                                   ("" if step.allsky else ", g=0 elided"))},
             "column_layers_per_s": round(value * nlay, 1),
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -307,14 +324,23 @@ def cpu_baseline(prob, target_s, kind="auto"):
     models_lw = [data.load_model("lw_abs"), data.load_model("lw_pfrac")]
     models_sw = [data.load_model("sw_abs"), data.load_model("sw_ray")]
     kd, kds = data.load_kdist("lw"), data.load_kdist("sw")
+    allsky = "lwp" in prob
+    co_lw, co_sw = (data.load_cloud_optics(w) for w in ("lw", "sw")) if allsky else (None, None)
+
+    def cl(sub):
+        return tuple(sub[k] for k in ("lwp", "iwp", "rel", "rei"))
 
     if ref is None:
         orc.set_threads(threads)
 
         def run(n):
             sub = _subset(prob, n)
-            orc.clear_sky_lw(sub, models_lw, kd)
-            orc.clear_sky_sw(sub, models_sw, kds)
+            if allsky:
+                orc.all_sky_lw(sub, models_lw, kd, co_lw, cl(sub))
+                orc.all_sky_sw(sub, models_sw, kds, co_sw, cl(sub))
+            else:
+                orc.clear_sky_lw(sub, models_lw, kd)
+                orc.clear_sky_sw(sub, models_sw, kds)
         label, desc = "port", "C restatement (oracle), OpenMP over columns"
     else:
         import threading
@@ -334,6 +360,8 @@ def cpu_baseline(prob, target_s, kind="auto"):
             sfc_lay = 1 if sub["play"][0, 0] > sub["play"][0, nlay - 1] else nlay
             lay, lev, sfc, jac = orc.planck_source(kd, sub["tlay"], sub["tlev"], sub["tsfc"], pf, sfc_lay)
             emis = np.repeat(np.asarray(sub["sfc_emis"], np.float32)[:, None], kd["nband"], axis=1)
+            if allsky:  # rrtmgp_allsky.F90: cloud_optics -> clouds%increment(atmos)
+                (tau,) = ref.increment_bybnd(kd, (tau,), ref.cloud_optics(co_lw, *cl(sub), nstr=1, icergh=2))
             ref.rte_lw(kd, tau, lay, lev, sfc, jac, emis, sub["top_at_1"])
             xs = orc.nn_inputs(sub["play"], sub["tlay"], sub["gases"], models_sw[0]).reshape(-1, int(models_sw[0]["dims"][0]))
             ta = orc.tau_post(models_sw[0], ref.mlp(models_sw[0], xs), cd)
@@ -341,8 +369,11 @@ def cpu_baseline(prob, target_s, kind="auto"):
             ng = ta.shape[-1]
             toa = data.toa_flux(sub, kds)
             alb = np.repeat(np.asarray(sub["sfc_alb"], np.float32)[:, None], ng, axis=1)
-            ref.rte_sw(kds, ta.reshape(ncol, nlay, ng), ssa.reshape(ncol, nlay, ng), np.zeros((ncol, nlay, ng), np.float32),
-                       sub["mu0"], toa, alb, alb, sub["top_at_1"])
+            ta, ssa, g = ta.reshape(ncol, nlay, ng), ssa.reshape(ncol, nlay, ng), np.zeros((ncol, nlay, ng), np.float32)
+            if allsky:  # cloud_optics -> clouds%delta_scale() -> clouds%increment(atmos)
+                c = ref.cloud_optics(co_sw, *cl(sub), nstr=2, icergh=2)
+                ta, ssa, g = ref.increment_bybnd(kds, (ta, ssa, g), ref.delta_scale(kds, *c))
+            ref.rte_sw(kds, ta, ssa, g, sub["mu0"], toa, alb, alb, sub["top_at_1"])
 
         pool = ThreadPoolExecutor(max_workers=threads)
 
@@ -363,7 +394,8 @@ def cpu_baseline(prob, target_s, kind="auto"):
         n = int(min(n * max(2.0, min(8.0, target_s / max(dt, 1e-3) / 2)), prob["ncol"] * 256))
         n = (n + 35) // 36 * 36
     return {"value": round(n / dt, 1), "unit": "columns/s", "cores": threads, "kind": label,
-            "sample": "%d columns of the same workload (LW+SW gas optics + RTE), %.1f s: %s" % (n, dt, desc)}
+            "sample": "%d columns of the same workload (LW+SW gas optics%s + RTE), %.1f s: %s"
+                      % (n, " + cloud optics/increment/delta-scale" if allsky else "", dt, desc)}
 
 
 if __name__ == "__main__":

@@ -40,6 +40,7 @@ extern "C" {
 
 typedef struct rrtmgpnn_context rrtmgpnn_context;
 typedef struct rrtmgpnn_network rrtmgpnn_network;
+typedef struct rrtmgpnn_cloud_optics rrtmgpnn_cloud_optics;
 
 /* ---- runtime ------------------------------------------------------------------------------ */
 int         rrtmgpnn_version(void);
@@ -145,6 +146,50 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
 /* expand (rte/mo_rte_lw.F90:429-447): (nband,ncol) -> (ngpt,ncol).  band_lims_gpt HOST (2,nband). */
 int rrtmgpnn_expand_band_to_gpt(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const int *band_lims_gpt,
                                 const float *arr_in, float *arr_out);
+
+/* ---- all-sky: cloud optics, increment, delta scaling ------------------ */
+/* ty_cloud_optics%load, LUT form (extensions/cloud_optics/mo_cloud_optics.F90:load_lut).  HOST arrays in the
+ * coefficient file's Fortran layout: liquid (nsize_liq, nband), ice (nsize_ice, nband, nrghice).
+ * band_lims_wvn (2, nband) may be NULL.  Ice roughness starts at 1 (set_ice_roughness). */
+int rrtmgpnn_cloud_optics_create_lut(rrtmgpnn_context *ctx, int nband, const float *band_lims_wvn, int nsize_liq,
+                                     int nsize_ice, int nrghice, float radliq_lwr, float radliq_upr,
+                                     float radice_lwr, float radice_upr, const float *lut_extliq,
+                                     const float *lut_ssaliq, const float *lut_asyliq, const float *lut_extice,
+                                     const float *lut_ssaice, const float *lut_asyice, rrtmgpnn_cloud_optics **co);
+/* Pade form (load_pade): coefficients (nband, nsizereg, ncoef[, nrghice]) with ncoef_ext = 6 ([2/3]
+ * approximants) and ncoef_ssa = 5 ([2/2]); size-regime bounds (nsizereg + 1) each; nsizereg must be 3. */
+int rrtmgpnn_cloud_optics_create_pade(rrtmgpnn_context *ctx, int nband, const float *band_lims_wvn, int nsizereg,
+                                      int ncoef_ext, int ncoef_ssa, int nrghice, const float *pade_extliq,
+                                      const float *pade_ssaliq, const float *pade_asyliq, const float *pade_extice,
+                                      const float *pade_ssaice, const float *pade_asyice,
+                                      const float *sizreg_extliq, const float *sizreg_ssaliq,
+                                      const float *sizreg_asyliq, const float *sizreg_extice,
+                                      const float *sizreg_ssaice, const float *sizreg_asyice,
+                                      rrtmgpnn_cloud_optics **co);
+/* Load the RBIN conversion of rrtmgp-cloud-optics-coeffs-{lw,sw}.nc; use_lut selects the method. */
+int rrtmgpnn_cloud_optics_load(rrtmgpnn_context *ctx, const char *path, int use_lut, rrtmgpnn_cloud_optics **co);
+int rrtmgpnn_cloud_optics_set_ice_roughness(rrtmgpnn_cloud_optics *co, int icergh);
+/* host outputs: nband, nrghice, radii = {liq min, liq max, ice min, ice max} (get_min/max_radius_*) */
+int rrtmgpnn_cloud_optics_get(const rrtmgpnn_cloud_optics *co, int *nband, int *nrghice, float radii[4]);
+int rrtmgpnn_cloud_optics_destroy(rrtmgpnn_cloud_optics *co);
+/* cloud_optics (:354-535): clwp, ciwp, reliq, reice (nlay, ncol) -> by band (nband, nlay, ncol).
+ * ssa == NULL: 1scl, tau = absorption optical depth; otherwise 2str (tau, ssa, g; g required). */
+int rrtmgpnn_cloud_optics_compute(rrtmgpnn_context *ctx, const rrtmgpnn_cloud_optics *co, int ncol, int nlay,
+                                  const float *clwp, const float *ciwp, const float *reliq, const float *reice,
+                                  float *tau, float *ssa, float *g);
+/* ty_optical_props_arry%increment of g-point properties (ngpt, nlay, ncol) by band-resolved ones
+ * (nband, nlay, ncol) (rte/mo_optical_props.F90:882-1023, inc_*_bybnd).  ssa_io == NULL: 1scl target;
+ * ssa_in == NULL: 1scl increment.  band_lims_gpt HOST (2, nband). */
+int rrtmgpnn_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int nband, const int *band_lims_gpt,
+                             float *tau_io, float *ssa_io, float *g_io, const float *tau_in, const float *ssa_in,
+                             const float *g_in);
+/* Same-resolution increment (increment_*_by_*, rte/kernels/mo_optical_props_kernels.F90:109-219):
+ * both sets (ngpt, nlay, ncol); NULL ssa as above. */
+int rrtmgpnn_increment(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, float *tau_io, float *ssa_io, float *g_io,
+                       const float *tau_in, const float *ssa_in, const float *g_in);
+/* ty_optical_props_2str%delta_scale([for]) (rte/mo_optical_props.F90:576-604; kernels
+ * rte/kernels/mo_optical_props_kernels.F90:41-92) on n values in place.  fwd == NULL: f = g**2. */
+int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);
 
 #ifdef __cplusplus
 }

@@ -56,6 +56,10 @@ class Oracle:
         L.orc_sw_solver_2stream.argtypes = [c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                             _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_expand.argtypes = [c_int, c_int, c_int, _i32p, _f32p, _f32p]
+        L.orc_cloud_optics.argtypes = ([c_int] * 4 + [c_float] * 4 + [_f32p] * 6 + [c_int] + [_f32p] * 12 +
+                                       [c_int, c_int] + [_f32p] * 4 + [c_int] + [_f32p] * 3)
+        L.orc_increment_bybnd.argtypes = [c_int] * 4 + [_i32p, c_int, _f32p, _f32p, _f32p, c_int, _f32p, _f32p, _f32p]
+        L.orc_delta_scale_2str.argtypes = [c_long, _f32p, _f32p, _f32p, ctypes.c_void_p]
         L.orc_set_num_threads.argtypes = [c_int]
         L.orc_num_threads.restype = c_int
 
@@ -143,6 +147,37 @@ class Oracle:
                                      f32(mu0), f32(alb_dir_gpt), f32(alb_dif_gpt), up, dn, dr)
         return up, dn, dr
 
+    def cloud_optics(self, co, clwp, ciwp, reliq, reice, nstr=2, lut=True, icergh=1):
+        """ty_cloud_optics%cloud_optics (extensions/cloud_optics/mo_cloud_optics.F90:354-535); by band."""
+        t = cloud_tables(co, icergh)
+        ncol, nlay = clwp.shape
+        nb = t["nband"]
+        tau, ssa, g = (np.zeros((ncol, nlay, nb), np.float32) for _ in range(3))
+        self.L.orc_cloud_optics(int(lut), nb, t["nsize_liq"], t["nsize_ice"], *t["rad"], *t["lut"], t["nsizereg"],
+                                *t["pade"], *t["sr"], ncol, nlay, f32(clwp), f32(ciwp), f32(reliq), f32(reice),
+                                nstr, tau, ssa, g)
+        return (tau,) if nstr == 1 else (tau, ssa, g)
+
+    def increment_bybnd(self, band_lims_gpt, io, inc):
+        """ty_optical_props_arry%increment by band (rte/mo_optical_props.F90:882-1023); io/inc = (tau,) or
+        (tau, ssa, g) tuples, io g-point resolved, inc by band.  Returns new io arrays."""
+        io = [f32(a).copy() for a in io]
+        ncol, nlay, ngpt = io[0].shape
+        nb = inc[0].shape[-1]
+        z = np.zeros(1, np.float32)
+        self.L.orc_increment_bybnd(ncol, nlay, ngpt, nb, np.ascontiguousarray(band_lims_gpt, np.int32), len(io) if len(io) == 1 else 2,
+                                   io[0], io[1] if len(io) > 1 else z, io[2] if len(io) > 1 else z,
+                                   1 if len(inc) == 1 else 2, f32(inc[0]), f32(inc[1]) if len(inc) > 1 else z,
+                                   f32(inc[2]) if len(inc) > 1 else z)
+        return tuple(io)
+
+    def delta_scale(self, tau, ssa, g, fwd=None):
+        """delta_scale_2str (rte/kernels/mo_optical_props_kernels.F90:41-92): f = fwd, or g**2 when None."""
+        tau, ssa, g = f32(tau).copy(), f32(ssa).copy(), f32(g).copy()
+        fw = None if fwd is None else f32(fwd)
+        self.L.orc_delta_scale_2str(tau.size, tau, ssa, g, None if fw is None else fw.ctypes.data)
+        return tau, ssa, g
+
     # -- class-level pipelines (gas_optics + rte) -------------------------------------------
     def lw_gas_optics(self, prob, models, kd):
         """gas_optics_int NN branch (rrtmgp/mo_gas_optics_rrtmgp.F90:239-428). models: [abs, pfrac]."""
@@ -176,6 +211,32 @@ class Oracle:
                                 prob["top_at_1"], nmus)
         return up, dn, go
 
+    def all_sky_lw(self, prob, models, kd, co, clouds, nmus=1, icergh=2, lut=True):
+        """examples/all-sky/rrtmgp_allsky.F90:366-404 with NN gas optics: cloud_optics (1scl, by band) ->
+        gas_optics -> clouds%increment(atmos) -> rte_lw.  clouds = (lwp, iwp, rel, rei), each (ncol, nlay)."""
+        go = self.lw_gas_optics(prob, models, kd)
+        cld = self.cloud_optics(co, *clouds, nstr=1, lut=lut, icergh=icergh)
+        (tau,) = self.increment_bybnd(kd["band_lims_gpt"], (go["tau"],), cld)
+        ngpt = tau.shape[-1]
+        emis = np.repeat(f32(prob["sfc_emis"])[:, None], ngpt, axis=1)
+        up, dn = self.lw_solver(tau, go["lay_source"], go["lev_source"], emis, go["sfc_source"], prob["top_at_1"], nmus)
+        return up, dn, dict(go, tau=tau, clouds=cld)
+
+    def all_sky_sw(self, prob, models, kd_sw, co, clouds, icergh=2, lut=True):
+        """rrtmgp_allsky.F90:405-446: cloud_optics (2str) -> gas_optics -> clouds%delta_scale() ->
+        clouds%increment(atmos) -> rte_sw."""
+        go = self.sw_gas_optics(prob, models)
+        cld = self.delta_scale(*self.cloud_optics(co, *clouds, nstr=2, lut=lut, icergh=icergh))
+        tau, ssa, g = self.increment_bybnd(kd_sw["band_lims_gpt"], (go["tau"], go["ssa"], go["g"]), cld)
+        ngpt = tau.shape[-1]
+        toa = data.toa_flux(prob, kd_sw)
+        alb = np.repeat(f32(prob["sfc_alb"])[:, None], ngpt, axis=1)
+        up, dn, dr = self.sw_solver(tau, ssa, g, prob["mu0"], toa, alb, alb, prob["top_at_1"])
+        m = ~prob["usecol"]
+        up[m] = 0.0
+        dn[m] = 0.0
+        return up, dn, dr, dict(go, tau=tau, ssa=ssa, g=g, clouds=cld)
+
     def clear_sky_sw(self, prob, models, kd_sw):
         go = self.sw_gas_optics(prob, models)
         ngpt = go["tau"].shape[-1]
@@ -186,6 +247,22 @@ class Oracle:
         up[m] = 0.0
         dn[m] = 0.0
         return up, dn, dr, go
+
+
+def cloud_tables(co, icergh=1):
+    """Flat argument tuple of a cloud-optics RBIN dict (data.load_cloud_optics) for the C/Fortran entry points:
+    LUT and Pade tables in the file's Fortran layout, the ice tables sliced at roughness icergh (1-based)."""
+    nband = co["bnd_limits_wavenumber"].shape[0]
+    r = icergh - 1
+    lut = (f32(co["lut_extliq"]), f32(co["lut_ssaliq"]), f32(co["lut_asyliq"]),
+           f32(co["lut_extice"][r]), f32(co["lut_ssaice"][r]), f32(co["lut_asyice"][r]))
+    pade = (f32(co["pade_extliq"]), f32(co["pade_ssaliq"]), f32(co["pade_asyliq"]),
+            f32(co["pade_extice"][r]), f32(co["pade_ssaice"][r]), f32(co["pade_asyice"][r]))
+    sr = tuple(f32(co["pade_sizreg_" + k]) for k in ("extliq", "ssaliq", "asyliq", "extice", "ssaice", "asyice"))
+    return {"nband": nband, "nsize_liq": co["lut_extliq"].shape[1], "nsize_ice": co["lut_extice"].shape[2],
+            "nrgh": co["lut_extice"].shape[0], "nsizereg": co["pade_extliq"].shape[1],
+            "rad": tuple(float(co[k][0]) for k in ("radliq_lwr", "radliq_upr", "radice_lwr", "radice_upr")),
+            "lut": lut, "pade": pade, "sr": sr}
 
 
 def gauss(nmus):
@@ -214,6 +291,15 @@ class Reference:
         L.ref_mlp.argtypes = [c_int, _i32p, _i32p, _f32p, _f32p, c_int, _f32p, _f32p]
         L.ref_mlp.restype = c_int
         L.ref_last_error.argtypes = [ctypes.c_char_p, c_int]
+        L.ref_cloud_optics.argtypes = ([c_int, c_int, _f32p, c_int, c_int, c_int] + [c_float] * 4 + [_f32p] * 6 +
+                                       [c_int, c_int, c_int] + [_f32p] * 12 + [c_int, c_int, c_int] + [_f32p] * 4 +
+                                       [c_int] + [_f32p] * 3)
+        L.ref_cloud_optics.restype = c_int
+        L.ref_increment_bybnd.argtypes = [c_int] * 4 + [_i32p, _f32p, c_int, _f32p, _f32p, _f32p, c_int, _f32p, _f32p,
+                                                        _f32p]
+        L.ref_increment_bybnd.restype = c_int
+        L.ref_delta_scale.argtypes = [c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, c_int, _f32p]
+        L.ref_delta_scale.restype = c_int
 
     def _check(self, rc):
         if rc != 0:
@@ -250,3 +336,39 @@ class Reference:
         out = np.zeros((nb, dims[-1]), np.float32)
         self._check(self.L.ref_mlp(nl, dims, np.asarray(model["activation"], np.int32), w_all, b_all, nb, x, out))
         return out
+
+    def cloud_optics(self, co, clwp, ciwp, reliq, reice, nstr=2, lut=True, icergh=1):
+        """The reference's ty_cloud_optics (load_lut / load_pade, set_ice_roughness, cloud_optics)."""
+        t = cloud_tables(co, 1)
+        nb = t["nband"]
+        ncol, nlay = clwp.shape
+        full = lambda k: f32(co[k])  # noqa: E731  (all roughness types; the reference slices itself)
+        tau, ssa, g = (np.zeros((ncol, nlay, nb), np.float32) for _ in range(3))
+        ncx, ncs = co["pade_extliq"].shape[0], co["pade_ssaliq"].shape[0]
+        self._check(self.L.ref_cloud_optics(
+            int(lut), nb, f32(co["bnd_limits_wavenumber"]), t["nsize_liq"], t["nsize_ice"], t["nrgh"], *t["rad"],
+            full("lut_extliq"), full("lut_ssaliq"), full("lut_asyliq"), full("lut_extice"), full("lut_ssaice"),
+            full("lut_asyice"), t["nsizereg"], ncx, ncs, full("pade_extliq"), full("pade_ssaliq"),
+            full("pade_asyliq"), full("pade_extice"), full("pade_ssaice"), full("pade_asyice"), *t["sr"], icergh,
+            ncol, nlay, f32(clwp), f32(ciwp), f32(reliq), f32(reice), nstr, tau, ssa, g))
+        return (tau,) if nstr == 1 else (tau, ssa, g)
+
+    def increment_bybnd(self, kd, io, inc):
+        io = [f32(a).copy() for a in io]
+        ncol, nlay, ngpt = io[0].shape
+        z = np.zeros(io[0].shape, np.float32)
+        zi = np.zeros(inc[0].shape, np.float32)
+        self._check(self.L.ref_increment_bybnd(ncol, nlay, kd["nband"], ngpt, np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                               f32(kd["band_lims_wvn"]), 1 if len(io) == 1 else 2, io[0],
+                                               io[1] if len(io) > 1 else z, io[2] if len(io) > 1 else z,
+                                               1 if len(inc) == 1 else 2, f32(inc[0]),
+                                               f32(inc[1]) if len(inc) > 1 else zi, f32(inc[2]) if len(inc) > 1 else zi))
+        return tuple(io)
+
+    def delta_scale(self, kd, tau, ssa, g, fwd=None):
+        tau, ssa, g = f32(tau).copy(), f32(ssa).copy(), f32(g).copy()
+        ncol, nlay, nb = tau.shape
+        fw = np.zeros_like(tau) if fwd is None else f32(fwd)
+        self._check(self.L.ref_delta_scale(ncol, nlay, nb, f32(kd["band_lims_wvn"]), tau, ssa, g, int(fwd is not None),
+                                           fw))
+        return tau, ssa, g

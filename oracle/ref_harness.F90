@@ -7,6 +7,10 @@
 !   ref_rte_lw   -> rte_lw (rte/mo_rte_lw.F90:60) on ty_optical_props_1scl + ty_source_func_lw
 !   ref_rte_sw   -> rte_sw (rte/mo_rte_sw.F90:48) on ty_optical_props_2str
 !   ref_mlp      -> network_type%output_sgemm_flat (neural/mod_network.F90:273) with MKL sgemm
+!   ref_cloud_optics -> ty_cloud_optics%load (LUT or Pade) + set_ice_roughness + cloud_optics
+!                       (extensions/cloud_optics/mo_cloud_optics.F90) into 1scl or 2str by band
+!   ref_increment_bybnd / ref_delta_scale -> ty_optical_props_arry%increment, %delta_scale
+!                       (rte/mo_optical_props.F90:882-1023, :576-604)
 ! The NN modules that need netcdf (mod_network_rrtmgp, mo_gas_optics_rrtmgp,
 ! mo_gas_optics_kernels) are not built: netcdf-fortran is absent and we do not stub it.
 module ref_harness
@@ -18,6 +22,7 @@ module ref_harness
   use mo_rte_lw,           only: rte_lw
   use mo_rte_sw,           only: rte_sw
   use mod_network,         only: network_type
+  use mo_cloud_optics,     only: ty_cloud_optics
   implicit none
   character(len=128), save :: last_msg = ''
 contains
@@ -131,4 +136,130 @@ contains
       buf(i) = last_msg(i:i)
     end do
   end subroutine ref_last_error
+  ! cloud_optics: LUT (lut != 0) or Pade coefficient arrays in the file's (Fortran) layout.
+  ! nstr = 1 -> ty_optical_props_1scl (absorption tau), 2 -> 2str (tau, ssa, g); outputs (nband, nlay, ncol).
+  integer(c_int) function ref_cloud_optics(lut, nband, band_lims_wvn, nsize_liq, nsize_ice, nrgh, &
+      radliq_lwr, radliq_upr, radice_lwr, radice_upr, extliq, ssaliq, asyliq, extice, ssaice, asyice, &
+      nsizereg, ncoef_ext, ncoef_ssa, p_extliq, p_ssaliq, p_asyliq, p_extice, p_ssaice, p_asyice, &
+      sr_extliq, sr_ssaliq, sr_asyliq, sr_extice, sr_ssaice, sr_asyice, icergh, &
+      ncol, nlay, clwp, ciwp, reliq, reice, nstr, tau, ssa, g) bind(C, name="ref_cloud_optics")
+    integer(c_int), value :: lut, nband, nsize_liq, nsize_ice, nrgh, nsizereg, ncoef_ext, ncoef_ssa, icergh
+    integer(c_int), value :: ncol, nlay, nstr
+    real(c_float),  value :: radliq_lwr, radliq_upr, radice_lwr, radice_upr
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband)
+    real(c_float),  intent(in) :: extliq(nsize_liq, nband), ssaliq(nsize_liq, nband), asyliq(nsize_liq, nband)
+    real(c_float),  intent(in) :: extice(nsize_ice, nband, nrgh), ssaice(nsize_ice, nband, nrgh), &
+                                  asyice(nsize_ice, nband, nrgh)
+    real(c_float),  intent(in) :: p_extliq(nband, nsizereg, ncoef_ext), p_ssaliq(nband, nsizereg, ncoef_ssa), &
+                                  p_asyliq(nband, nsizereg, ncoef_ssa)
+    real(c_float),  intent(in) :: p_extice(nband, nsizereg, ncoef_ext, nrgh), p_ssaice(nband, nsizereg, ncoef_ssa, nrgh), &
+                                  p_asyice(nband, nsizereg, ncoef_ssa, nrgh)
+    real(c_float),  intent(in) :: sr_extliq(nsizereg+1), sr_ssaliq(nsizereg+1), sr_asyliq(nsizereg+1), &
+                                  sr_extice(nsizereg+1), sr_ssaice(nsizereg+1), sr_asyice(nsizereg+1)
+    real(c_float),  intent(in) :: clwp(nlay, ncol), ciwp(nlay, ncol), reliq(nlay, ncol), reice(nlay, ncol)
+    real(c_float),  intent(out) :: tau(nband, nlay, ncol), ssa(nband, nlay, ncol), g(nband, nlay, ncol)
+
+    type(ty_cloud_optics) :: co
+    type(ty_optical_props_1scl) :: o1
+    type(ty_optical_props_2str) :: o2
+    character(len=128) :: err
+
+    ref_cloud_optics = 1
+    if (lut /= 0) then
+      err = co%load(band_lims_wvn, radliq_lwr, radliq_upr, 0._wp, radice_lwr, radice_upr, 0._wp, &
+                    extliq, ssaliq, asyliq, extice, ssaice, asyice)
+    else
+      err = co%load(band_lims_wvn, p_extliq, p_ssaliq, p_asyliq, p_extice, p_ssaice, p_asyice, &
+                    sr_extliq, sr_ssaliq, sr_asyliq, sr_extice, sr_ssaice, sr_asyice)
+    end if
+    if (err /= '') then; last_msg = err; return; end if
+    err = co%set_ice_roughness(int(icergh))
+    if (err /= '') then; last_msg = err; return; end if
+    if (nstr == 1) then
+      err = o1%alloc_1scl(ncol, nlay, band_lims_wvn)
+      if (err /= '') then; last_msg = err; return; end if
+      err = co%cloud_optics(clwp, ciwp, reliq, reice, o1)
+      if (err /= '') then; last_msg = err; return; end if
+      tau = o1%tau
+      ssa = 0._wp
+      g = 0._wp
+    else
+      err = o2%alloc_2str(ncol, nlay, band_lims_wvn)
+      if (err /= '') then; last_msg = err; return; end if
+      err = co%cloud_optics(clwp, ciwp, reliq, reice, o2)
+      if (err /= '') then; last_msg = err; return; end if
+      tau = o2%tau
+      ssa = o2%ssa
+      g = o2%g
+    end if
+    ref_cloud_optics = 0
+  end function ref_cloud_optics
+
+  ! op_io (ngpt g-points, nstr_io) %increment'ed by op_in given by band (nband, nstr_in); in place.
+  integer(c_int) function ref_increment_bybnd(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, nstr_io, &
+      tau_io, ssa_io, g_io, nstr_in, tau_in, ssa_in, g_in) bind(C, name="ref_increment_bybnd")
+    integer(c_int), value :: ncol, nlay, nband, ngpt, nstr_io, nstr_in
+    integer(c_int), intent(in) :: band_lims_gpt(2, nband)
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband)
+    real(c_float),  intent(inout) :: tau_io(ngpt, nlay, ncol), ssa_io(ngpt, nlay, ncol), g_io(ngpt, nlay, ncol)
+    real(c_float),  intent(in) :: tau_in(nband, nlay, ncol), ssa_in(nband, nlay, ncol), g_in(nband, nlay, ncol)
+    type(ty_optical_props_1scl) :: a1, b1
+    type(ty_optical_props_2str) :: a2, b2
+    character(len=128) :: err
+
+    ref_increment_bybnd = 1
+    err = ''
+    if (nstr_in == 1) then
+      err = b1%alloc_1scl(ncol, nlay, band_lims_wvn)
+      b1%tau = tau_in
+    else
+      err = b2%alloc_2str(ncol, nlay, band_lims_wvn)
+      b2%tau = tau_in; b2%ssa = ssa_in; b2%g = g_in
+    end if
+    if (err /= '') then; last_msg = err; return; end if
+    if (nstr_io == 1) then
+      err = a1%alloc_1scl(ncol, nlay, band_lims_wvn, band_lims_gpt)
+      a1%tau = tau_io
+      if (nstr_in == 1) then
+        err = b1%increment(a1)
+      else
+        err = b2%increment(a1)
+      end if
+      tau_io = a1%tau
+    else
+      err = a2%alloc_2str(ncol, nlay, band_lims_wvn, band_lims_gpt)
+      a2%tau = tau_io; a2%ssa = ssa_io; a2%g = g_io
+      if (nstr_in == 1) then
+        err = b1%increment(a2)
+      else
+        err = b2%increment(a2)
+      end if
+      tau_io = a2%tau; ssa_io = a2%ssa; g_io = a2%g
+    end if
+    if (err /= '') then; last_msg = err; return; end if
+    ref_increment_bybnd = 0
+  end function ref_increment_bybnd
+
+  ! ty_optical_props_2str%delta_scale([for]) on (n, nlay, ncol) arrays, in place; has_for = 0: f = g**2.
+  integer(c_int) function ref_delta_scale(ncol, nlay, nband, band_lims_wvn, tau, ssa, g, has_for, for) &
+      bind(C, name="ref_delta_scale")
+    integer(c_int), value :: ncol, nlay, nband, has_for
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband), for(nband, nlay, ncol)
+    real(c_float),  intent(inout) :: tau(nband, nlay, ncol), ssa(nband, nlay, ncol), g(nband, nlay, ncol)
+    type(ty_optical_props_2str) :: a
+    character(len=128) :: err
+    ref_delta_scale = 1
+    err = a%alloc_2str(ncol, nlay, band_lims_wvn)
+    if (err /= '') then; last_msg = err; return; end if
+    a%tau = tau; a%ssa = ssa; a%g = g
+    if (has_for /= 0) then
+      err = a%delta_scale(for)
+    else
+      err = a%delta_scale()
+    end if
+    if (err /= '') then; last_msg = err; return; end if
+    tau = a%tau; ssa = a%ssa; g = a%g
+    ref_delta_scale = 0
+  end function ref_delta_scale
+
 end module ref_harness

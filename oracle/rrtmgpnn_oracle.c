@@ -12,7 +12,7 @@
  *     the MLP chain (network_type%output_sgemm_flat + MKL sgemm) are compiled
  *     from /root/reference sources by oracle/Makefile.ref into oracle/_ref/
  *     and compared in tests/test_oracle_vs_reference.py (container only); the
- *     comparison's outputs are frozen as tests/golden/*.rbin fixtures.
+ *     comparison's outputs are frozen as RBIN fixtures under tests/golden.
  *   - compute_nn_inputs, get_col_dry, the NN post-processing and
  *     compute_Planck_source_nn live in reference modules that need netcdf
  *     (unbuildable here); they are restated below line-by-line and pinned by the
@@ -468,6 +468,143 @@ void orc_expand(int nband, int ngpt, int ncol, const int *band_lims, const float
     for (int b = 0; b < nband; b++)
       for (int g = band_lims[2 * b] - 1; g < band_lims[2 * b + 1]; g++)
         arr_out[g + (size_t)ngpt * icol] = arr_in[b + (size_t)nband * icol];
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * Cloud optics (extensions/cloud_optics/mo_cloud_optics.F90).  Tables are the file's Fortran arrays
+ * already sliced to the chosen ice roughness: LUT tab(nsize, nband); Pade c(nband, nsizereg, 0:m+n);
+ * size-regime bounds sr[nsizereg+1].  Outputs by band (nband, nlay, ncol).
+ * ------------------------------------------------------------------------------------------- */
+/* :603-645 (compute_all_from_table) for one (band, layer, column) value */
+static void from_table(float lwp, float re, int nsteps, float step, float offset, const float *tt,
+                       const float *st, const float *at, int nband, int b, float *t, float *ts, float *tsg)
+{
+  int index = (int)floorf((re - offset) / step) + 1;
+  if (index > nsteps - 1) index = nsteps - 1;
+  float fint = (re - offset) / step - (float)(index - 1);
+  const float *T = tt + (size_t)nsteps * b, *S = st + (size_t)nsteps * b, *A = at + (size_t)nsteps * b;
+  int i = index - 1;
+  *t = lwp * (T[i] + fint * (T[i + 1] - T[i]));
+  *ts = *t * (S[i] + fint * (S[i + 1] - S[i]));
+  *tsg = *ts * (A[i] + fint * (A[i + 1] - A[i]));
+}
+
+/* :750-775 (pade_eval_1); c(nbnd, nrads, 0:m+n), irad 1-based */
+static float pade_eval(int b, int nbnd, int nrads, int m, int n, int irad, float re, const float *c)
+{
+#define C_(i) c[b + (size_t)nbnd * ((irad - 1) + (size_t)nrads * (i))]
+  float denom = C_(n + m);
+  for (int i = n - 1 + m; i >= 1 + m; i--) denom = C_(i) + re * denom;
+  denom = 1.0f + re * denom;
+  float numer = C_(m);
+  for (int i = m - 1; i >= 1; i--) numer = C_(i) + re * numer;
+  numer = C_(0) + re * numer;
+#undef C_
+  return numer / denom;
+}
+
+/* :650-714 (compute_all_from_pade) for one value; irad = min(floor((re - b(2))/b(3)) + 2, 3) (quirk:
+ * divides by the third bound, valid for exactly three size regimes) */
+static int pade_irad(float re, const float *bounds)
+{
+  int irad = (int)floorf((re - bounds[1]) / bounds[2]) + 2;
+  return irad < 3 ? irad : 3;
+}
+
+void orc_cloud_optics(int lut, int nband, int nsize_liq, int nsize_ice, float radliq_lwr, float radliq_upr,
+                      float radice_lwr, float radice_upr, const float *extliq, const float *ssaliq,
+                      const float *asyliq, const float *extice, const float *ssaice, const float *asyice,
+                      int nsizereg, const float *p_extliq, const float *p_ssaliq, const float *p_asyliq,
+                      const float *p_extice, const float *p_ssaice, const float *p_asyice, const float *sr_extliq,
+                      const float *sr_ssaliq, const float *sr_asyliq, const float *sr_extice, const float *sr_ssaice,
+                      const float *sr_asyice, int ncol, int nlay, const float *clwp, const float *ciwp,
+                      const float *reliq, const float *reice, int nstr, float *tau, float *ssa, float *g)
+{
+  /* :141-142 step sizes; :354-535 combine */
+  const float liq_step = (radliq_upr - radliq_lwr) / (float)(nsize_liq - 1);
+  const float ice_step = (radice_upr - radice_lwr) / (float)(nsize_ice - 1);
+#pragma omp parallel for schedule(static)
+  for (int icol = 0; icol < ncol; icol++)
+    for (int ilay = 0; ilay < nlay; ilay++) {
+      const size_t s = ilay + (size_t)nlay * icol;
+      for (int b = 0; b < nband; b++) {
+        float lt = 0, lts = 0, ltsg = 0, it = 0, its = 0, itsg = 0;
+        if (clwp[s] > 0.0f) {
+          if (lut)
+            from_table(clwp[s], reliq[s], nsize_liq, liq_step, radliq_lwr, extliq, ssaliq, asyliq, nband, b, &lt,
+                       &lts, &ltsg);
+          else {
+            lt = clwp[s] * pade_eval(b, nband, nsizereg, 2, 3, pade_irad(reliq[s], sr_extliq), reliq[s], p_extliq);
+            float w = pade_eval(b, nband, nsizereg, 2, 2, pade_irad(reliq[s], sr_ssaliq), reliq[s], p_ssaliq);
+            lts = lt * (1.0f - fmaxf(0.0f, w));
+            ltsg = lts * pade_eval(b, nband, nsizereg, 2, 2, pade_irad(reliq[s], sr_asyliq), reliq[s], p_asyliq);
+          }
+        }
+        if (ciwp[s] > 0.0f) {
+          if (lut)
+            from_table(ciwp[s], reice[s], nsize_ice, ice_step, radice_lwr, extice, ssaice, asyice, nband, b, &it,
+                       &its, &itsg);
+          else {
+            it = ciwp[s] * pade_eval(b, nband, nsizereg, 2, 3, pade_irad(reice[s], sr_extice), reice[s], p_extice);
+            float w = pade_eval(b, nband, nsizereg, 2, 2, pade_irad(reice[s], sr_ssaice), reice[s], p_ssaice);
+            its = it * (1.0f - fmaxf(0.0f, w));
+            itsg = its * pade_eval(b, nband, nsizereg, 2, 2, pade_irad(reice[s], sr_asyice), reice[s], p_asyice);
+          }
+        }
+        const size_t o = b + (size_t)nband * s;
+        if (nstr == 1) {
+          tau[o] = (lt - lts) + (it - its);
+        } else {
+          const float t = lt + it, ts = lts + its;
+          g[o] = (ltsg + itsg) / fmaxf(FLT_EPSILON, ts);
+          ssa[o] = ts / fmaxf(FLT_EPSILON, t);
+          tau[o] = t;
+        }
+      }
+    }
+}
+
+/* rte/kernels/mo_optical_props_kernels.F90:358-484 (inc_*_bybnd): io (ngpt,nlay,ncol) incremented by
+ * in (nbnd,nlay,ncol).  nstr_io / nstr_in in {1, 2}; eps = 3*tiny(1.0) (:31). */
+void orc_increment_bybnd(int ncol, int nlay, int ngpt, int nbnd, const int *band_lims, int nstr_io, float *tau1,
+                         float *ssa1, float *g1, int nstr_in, const float *tau2, const float *ssa2, const float *g2)
+{
+  const float eps = 3.0f * FLT_MIN;
+#pragma omp parallel for schedule(static)
+  for (int icol = 0; icol < ncol; icol++)
+    for (int ilay = 0; ilay < nlay; ilay++)
+      for (int b = 0; b < nbnd; b++) {
+        const size_t ib = b + (size_t)nbnd * (ilay + (size_t)nlay * icol);
+        for (int igpt = band_lims[2 * b] - 1; igpt < band_lims[2 * b + 1]; igpt++) {
+          const size_t i = igpt + (size_t)ngpt * (ilay + (size_t)nlay * icol);
+          if (nstr_io == 1) {
+            tau1[i] = nstr_in == 1 ? tau1[i] + tau2[ib] : tau1[i] + tau2[ib] * (1.0f - ssa2[ib]);
+          } else if (nstr_in == 1) {
+            const float tau12 = tau1[i] + tau2[ib];
+            ssa1[i] = tau1[i] * ssa1[i] / fmaxf(eps, tau12);
+            tau1[i] = tau12;
+          } else {
+            const float tau12 = tau1[i] + tau2[ib];
+            const float tauscat12 = tau1[i] * ssa1[i] + tau2[ib] * ssa2[ib];
+            g1[i] = (tau1[i] * ssa1[i] * g1[i] + tau2[ib] * ssa2[ib] * g2[ib]) / fmaxf(eps, tauscat12);
+            ssa1[i] = tauscat12 / fmaxf(eps, tau12);
+            tau1[i] = tau12;
+          }
+        }
+      }
+}
+
+/* :41-92 (delta_scale_2str_f_k with for = fwd; delta_scale_2str_k, f = g*g, when fwd == NULL) over n values */
+void orc_delta_scale_2str(long n, float *tau, float *ssa, float *g, const float *fwd)
+{
+  const float eps = 3.0f * FLT_MIN;
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < n; i++) {
+    const float f = fwd ? fwd[i] : g[i] * g[i], wf = ssa[i] * f;
+    tau[i] = (1.0f - wf) * tau[i];
+    ssa[i] = (ssa[i] - wf) / fmaxf(eps, 1.0f - wf);
+    g[i] = (g[i] - f) / fmaxf(eps, 1.0f - f);
+  }
 }
 
 int orc_num_threads(void)

@@ -520,4 +520,211 @@ int rrtmgpnn_expand_band_to_gpt(rrtmgpnn_context *ctx, int nband, int ngpt, int 
   return launch_expand(ctx, nband, ngpt, ncol, b, arr_in, arr_out);
 }
 
+// ---- cloud optics --------------------------------------------------------------------------------
+static int cloud_upload(rrtmgpnn_context *ctx, rrtmgpnn_cloud_optics *c, const std::vector<const float *> &src,
+                        const std::vector<size_t> &counts)
+{
+  size_t total = 0;
+  for (size_t k = 0; k < src.size(); k++) {
+    c->off[k] = total;
+    total += counts[k];
+  }
+  std::vector<float> img(total);
+  for (size_t k = 0; k < src.size(); k++) std::memcpy(img.data() + c->off[k], src[k], sizeof(float) * counts[k]);
+  RRTMGPNN_HIP(hipSetDevice(ctx->device));
+  RRTMGPNN_HIP(hipMalloc(&c->d_tab, sizeof(float) * total));
+  RRTMGPNN_HIP(hipMemcpy(c->d_tab, img.data(), sizeof(float) * total, hipMemcpyHostToDevice));
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_cloud_optics_create_lut(rrtmgpnn_context *ctx, int nband, const float *band_lims_wvn, int nsize_liq,
+                                     int nsize_ice, int nrghice, float radliq_lwr, float radliq_upr,
+                                     float radice_lwr, float radice_upr, const float *lut_extliq,
+                                     const float *lut_ssaliq, const float *lut_asyliq, const float *lut_extice,
+                                     const float *lut_ssaice, const float *lut_asyice, rrtmgpnn_cloud_optics **co)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!co || nband < 1 || nsize_liq < 2 || nsize_ice < 2 || nrghice < 1 || !lut_extliq || !lut_ssaliq ||
+      !lut_asyliq || !lut_extice || !lut_ssaice || !lut_asyice)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_create_lut: bad argument");
+  auto *c = new rrtmgpnn_cloud_optics();
+  c->device = ctx->device;
+  c->lut_mode = 1;
+  c->nband = nband;
+  c->nsize_liq = nsize_liq;
+  c->nsize_ice = nsize_ice;
+  c->nrghice = nrghice;
+  c->radliq_lwr = radliq_lwr; c->radliq_upr = radliq_upr;
+  c->radice_lwr = radice_lwr; c->radice_upr = radice_upr;
+  // load_lut (mo_cloud_optics.F90:141-142): step sizes in working precision
+  c->liq_step = (radliq_upr - radliq_lwr) / (float)(nsize_liq - 1);
+  c->ice_step = (radice_upr - radice_lwr) / (float)(nsize_ice - 1);
+  if (band_lims_wvn) c->band_lims_wvn.assign(band_lims_wvn, band_lims_wvn + 2 * nband);
+  const size_t nl = (size_t)nsize_liq * nband, ni = (size_t)nsize_ice * nband * nrghice;
+  if (int rc = cloud_upload(ctx, c, {lut_extliq, lut_ssaliq, lut_asyliq, lut_extice, lut_ssaice, lut_asyice},
+                            {nl, nl, nl, ni, ni, ni})) {
+    delete c;
+    return rc;
+  }
+  *co = c;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_cloud_optics_create_pade(rrtmgpnn_context *ctx, int nband, const float *band_lims_wvn, int nsizereg,
+                                      int ncoef_ext, int ncoef_ssa, int nrghice, const float *pade_extliq,
+                                      const float *pade_ssaliq, const float *pade_asyliq, const float *pade_extice,
+                                      const float *pade_ssaice, const float *pade_asyice,
+                                      const float *sizreg_extliq, const float *sizreg_ssaliq,
+                                      const float *sizreg_asyliq, const float *sizreg_extice,
+                                      const float *sizreg_ssaice, const float *sizreg_asyice,
+                                      rrtmgpnn_cloud_optics **co)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!co || nband < 1 || nrghice < 1 || !pade_extliq || !pade_ssaliq || !pade_asyliq || !pade_extice ||
+      !pade_ssaice || !pade_asyice || !sizreg_extliq || !sizreg_ssaliq || !sizreg_asyliq || !sizreg_extice ||
+      !sizreg_ssaice || !sizreg_asyice)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_create_pade: bad argument");
+  if (nsizereg != 3)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics%init(): Expecting precisely three size regimes for Pade approximants");
+  if (ncoef_ext != 6 || ncoef_ssa != 5)
+    return fail(RRTMGPNN_ERR_UNSUPPORTED, "cloud_optics: Pade approximants of order [2/3] (ext) and [2/2] (ssa, g) only");
+  auto *c = new rrtmgpnn_cloud_optics();
+  c->device = ctx->device;
+  c->lut_mode = 0;
+  c->nband = nband;
+  c->nrghice = nrghice;
+  c->nsizereg = nsizereg;
+  c->ncoef_ext = ncoef_ext;
+  c->ncoef_ssa = ncoef_ssa;
+  const int nbound = nsizereg + 1;
+  // load_pade (:250-253): radius limits from the extinction size regimes
+  c->radliq_lwr = sizreg_extliq[0]; c->radliq_upr = sizreg_extliq[nbound - 1];
+  c->radice_lwr = sizreg_extice[0]; c->radice_upr = sizreg_extice[nbound - 1];
+  if (band_lims_wvn) c->band_lims_wvn.assign(band_lims_wvn, band_lims_wvn + 2 * nband);
+  const size_t le = (size_t)nband * nsizereg * ncoef_ext, ls = (size_t)nband * nsizereg * ncoef_ssa;
+  const size_t nb = (size_t)nbound;
+  if (int rc = cloud_upload(ctx, c,
+                            {pade_extliq, pade_ssaliq, pade_asyliq, pade_extice, pade_ssaice, pade_asyice,
+                             sizreg_extliq, sizreg_ssaliq, sizreg_asyliq, sizreg_extice, sizreg_ssaice, sizreg_asyice},
+                            {le, ls, ls, le * nrghice, ls * nrghice, ls * nrghice, nb, nb, nb, nb, nb, nb})) {
+    delete c;
+    return rc;
+  }
+  *co = c;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_cloud_optics_load(rrtmgpnn_context *ctx, const char *path, int use_lut, rrtmgpnn_cloud_optics **co)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!path || !co) return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_load: null argument");
+  std::map<std::string, RbinArray> m;
+  if (int rc = read_rbin(path, m)) return rc;
+  auto need = [&](const char *k) -> const RbinArray * {
+    auto it = m.find(k);
+    return it == m.end() ? nullptr : &it->second;
+  };
+  const RbinArray *bl = need("bnd_limits_wavenumber");
+  if (!bl || bl->dims.size() != 2) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing bnd_limits_wavenumber");
+  const int nband = bl->dims[0];
+  std::vector<float> blw = as_vec<float>(*bl);
+  auto F = [&](const char *k) { return as_vec<float>(m[k]); };
+  if (use_lut) {
+    for (const char *k : {"lut_extliq", "lut_ssaliq", "lut_asyliq", "lut_extice", "lut_ssaice", "lut_asyice",
+                          "radliq_lwr", "radliq_upr", "radice_lwr", "radice_upr"})
+      if (!need(k)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing " + k);
+    const auto &li = m["lut_extice"];
+    if (li.dims.size() != 3 || m["lut_extliq"].dims.size() != 2) return fail(RRTMGPNN_ERR_IO, "cloud_optics_load: bad LUT shape");
+    std::vector<float> a = F("lut_extliq"), b = F("lut_ssaliq"), c = F("lut_asyliq"), d = F("lut_extice"),
+                       e = F("lut_ssaice"), f = F("lut_asyice");
+    return rrtmgpnn_cloud_optics_create_lut(ctx, nband, blw.data(), m["lut_extliq"].dims[1], li.dims[2], li.dims[0],
+                                            F("radliq_lwr")[0], F("radliq_upr")[0], F("radice_lwr")[0],
+                                            F("radice_upr")[0], a.data(), b.data(), c.data(), d.data(), e.data(),
+                                            f.data(), co);
+  }
+  for (const char *k : {"pade_extliq", "pade_ssaliq", "pade_asyliq", "pade_extice", "pade_ssaice", "pade_asyice",
+                        "pade_sizreg_extliq", "pade_sizreg_ssaliq", "pade_sizreg_asyliq", "pade_sizreg_extice",
+                        "pade_sizreg_ssaice", "pade_sizreg_asyice"})
+    if (!need(k)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing " + k);
+  const auto &pe = m["pade_extice"];
+  if (pe.dims.size() != 4 || m["pade_ssaliq"].dims.size() != 3) return fail(RRTMGPNN_ERR_IO, "cloud_optics_load: bad Pade shape");
+  std::vector<float> a = F("pade_extliq"), b = F("pade_ssaliq"), c = F("pade_asyliq"), d = F("pade_extice"),
+                     e = F("pade_ssaice"), f = F("pade_asyice"), s1 = F("pade_sizreg_extliq"),
+                     s2 = F("pade_sizreg_ssaliq"), s3 = F("pade_sizreg_asyliq"), s4 = F("pade_sizreg_extice"),
+                     s5 = F("pade_sizreg_ssaice"), s6 = F("pade_sizreg_asyice");
+  return rrtmgpnn_cloud_optics_create_pade(ctx, nband, blw.data(), pe.dims[2], pe.dims[1], m["pade_ssaliq"].dims[0],
+                                           pe.dims[0], a.data(), b.data(), c.data(), d.data(), e.data(), f.data(),
+                                           s1.data(), s2.data(), s3.data(), s4.data(), s5.data(), s6.data(), co);
+}
+
+int rrtmgpnn_cloud_optics_set_ice_roughness(rrtmgpnn_cloud_optics *co, int icergh)
+{
+  if (!co) return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_set_ice_roughness(): can't set before initialization");
+  if (icergh < 1 || icergh > co->nrghice)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "cloud optics: cloud ice surface roughness flag is out of bounds");
+  co->icergh = icergh;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_cloud_optics_get(const rrtmgpnn_cloud_optics *co, int *nband, int *nrghice, float radii[4])
+{
+  if (!co) return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_get: null handle");
+  if (nband) *nband = co->nband;
+  if (nrghice) *nrghice = co->nrghice;
+  if (radii) {
+    radii[0] = co->radliq_lwr; radii[1] = co->radliq_upr; radii[2] = co->radice_lwr; radii[3] = co->radice_upr;
+  }
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_cloud_optics_destroy(rrtmgpnn_cloud_optics *co)
+{
+  if (!co) return RRTMGPNN_OK;
+  if (co->d_tab) {
+    (void)hipSetDevice(co->device);
+    (void)hipFree(co->d_tab);
+  }
+  delete co;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_cloud_optics_compute(rrtmgpnn_context *ctx, const rrtmgpnn_cloud_optics *co, int ncol, int nlay,
+                                  const float *clwp, const float *ciwp, const float *reliq, const float *reice,
+                                  float *tau, float *ssa, float *g)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!co || !co->d_tab) return fail(RRTMGPNN_ERR_ARGUMENT, "cloud optics: no data has been initialized");
+  if (!clwp || !ciwp || !reliq || !reice || !tau || ncol < 0 || nlay < 0 || (ssa && !g))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "cloud optics: bad argument");
+  return launch_cloud_optics(ctx, co, ncol, nlay, clwp, ciwp, reliq, reice, tau, ssa, g);
+}
+
+int rrtmgpnn_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int nband, const int *band_lims_gpt,
+                             float *tau_io, float *ssa_io, float *g_io, const float *tau_in, const float *ssa_in,
+                             const float *g_in)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!tau_io || !tau_in || ncol < 0 || nlay < 0 || ngpt < 1 || (ssa_io && !g_io) || (ssa_in && !g_in))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "increment: bad argument");
+  BandArgs b;
+  if (int rc = band_args(nband, band_lims_gpt, ngpt, b)) return rc;
+  return launch_increment_bybnd(ctx, ncol, nlay, ngpt, &b, tau_io, ssa_io, g_io, tau_in, ssa_in, g_in);
+}
+
+int rrtmgpnn_increment(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, float *tau_io, float *ssa_io, float *g_io,
+                       const float *tau_in, const float *ssa_in, const float *g_in)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!tau_io || !tau_in || ncol < 0 || nlay < 0 || ngpt < 1 || (ssa_io && !g_io) || (ssa_in && !g_in))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "increment: bad argument");
+  return launch_increment_bybnd(ctx, ncol, nlay, ngpt, nullptr, tau_io, ssa_io, g_io, tau_in, ssa_in, g_in);
+}
+
+int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!tau || !ssa || !g || n < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "delta_scale: bad argument");
+  return launch_delta_scale(ctx, n, tau, ssa, g, fwd);
+}
+
 }  // extern "C"

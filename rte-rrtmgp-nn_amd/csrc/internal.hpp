@@ -68,7 +68,30 @@ struct rrtmgpnn_network {
   bool has_out_scaling() const { return !out_mean.empty(); }
 };
 
+// Cloud optics (extensions/cloud_optics/mo_cloud_optics.F90 ty_cloud_optics): one device buffer holding
+// the LUT or Pade tables in the file's Fortran layout; off[] are float offsets into it
+//   LUT : ext/ssa/asy liquid (nsize_liq, nband) [0..2], ice (nsize_ice, nband, nrghice) [3..5]
+//   Pade: ext/ssa/asy liquid (nband, nsizereg, ncoef) [0..2], ice (..., nrghice) [3..5], size-regime
+//         bounds [6..11]
+struct rrtmgpnn_cloud_optics {
+  int device = 0;
+  int lut_mode = 1;
+  int nband = 0, nsize_liq = 0, nsize_ice = 0, nrghice = 0, nsizereg = 0, ncoef_ext = 0, ncoef_ssa = 0;
+  int icergh = 1;
+  float radliq_lwr = 0, radliq_upr = 0, radice_lwr = 0, radice_upr = 0, liq_step = 0, ice_step = 0;
+  std::vector<float> band_lims_wvn;
+  float *d_tab = nullptr;
+  size_t off[12] = {0};
+};
+
 namespace rrtmgpnn {
+// kernels_clouds.hip
+struct BandArgs;
+int launch_cloud_optics(rrtmgpnn_context *ctx, const rrtmgpnn_cloud_optics *co, int ncol, int nlay, const float *clwp,
+                        const float *ciwp, const float *reliq, const float *reice, float *tau, float *ssa, float *g);
+int launch_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, const BandArgs *bands, float *tau1,
+                           float *ssa1, float *g1, const float *tau2, const float *ssa2, const float *g2);
+int launch_delta_scale(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);
 // kernels_nn.hip
 struct GasArgs {
   const float *p[kMaxInputs];

@@ -49,6 +49,20 @@ SIGNATURES = {
     "rrtmgpnn_sw_solver_2stream": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_expand_band_to_gpt": (c_int, [c_vp, c_int, c_int, c_int, P(c_int), c_vp, c_vp]),
+    "rrtmgpnn_cloud_optics_create_lut": (c_int, [c_vp, c_int, P(c_float), c_int, c_int, c_int, c_float, c_float,
+                                                 c_float, c_float, P(c_float), P(c_float), P(c_float), P(c_float),
+                                                 P(c_float), P(c_float), P(c_vp)]),
+    "rrtmgpnn_cloud_optics_create_pade": (c_int, [c_vp, c_int, P(c_float), c_int, c_int, c_int, c_int]
+                                          + [P(c_float)] * 12 + [P(c_vp)]),
+    "rrtmgpnn_cloud_optics_load": (c_int, [c_vp, c_char_p, c_int, P(c_vp)]),
+    "rrtmgpnn_cloud_optics_set_ice_roughness": (c_int, [c_vp, c_int]),
+    "rrtmgpnn_cloud_optics_get": (c_int, [c_vp, P(c_int), P(c_int), P(c_float)]),
+    "rrtmgpnn_cloud_optics_destroy": (c_int, [c_vp]),
+    "rrtmgpnn_cloud_optics_compute": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_increment_bybnd": (c_int, [c_vp, c_int, c_int, c_int, c_int, P(c_int), c_vp, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp]),
+    "rrtmgpnn_increment": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_delta_scale_2str": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp]),
 }
 
 

@@ -9,6 +9,9 @@ Names, argument meaning and error behaviour follow the reference:
   ty_gas_optics_rrtmgp%gas_optics  rrtmgp/mo_gas_optics_rrtmgp.F90:239-602 -> GasOpticsRRTMGP.gas_optics
   rte_lw                         rte/mo_rte_lw.F90:60-424                  -> rte_lw
   rte_sw                         rte/mo_rte_sw.F90:48-266                  -> rte_sw
+  ty_cloud_optics                extensions/cloud_optics/mo_cloud_optics.F90 -> CloudOptics
+  ty_optical_props_arry%increment / %delta_scale  rte/mo_optical_props.F90:882-1023, 565-604
+  rte_config_checks              rte/mo_rte_rrtmgp_config.F90:45-61        -> rte_config_checks
 Class-level functions RETURN an error message ('' on success), never raise for user errors, like the
 reference's `character(len=128) error_msg`; `stop_on_err` turns one into an exception.
 
@@ -23,6 +26,14 @@ from . import _lib, data, rbin
 from ._lib import check, float_array, int_array, ptr_array
 
 _CTX = {}
+# mo_rte_rrtmgp_config: value checks off by default, as in the reference (:23-24); extents are always checked
+check_values = False
+
+
+def rte_config_checks(logical):
+    """rte_config_checks (rte/mo_rte_rrtmgp_config.F90:56-61)."""
+    global check_values
+    check_values = bool(logical)
 
 
 class Context:
@@ -200,13 +211,53 @@ class OpticalProps:
             b[lo - 1:hi] = i + 1
         return b
 
+    def bands_are_equal(self, that):
+        """rte/mo_optical_props.F90:1204-1214: same nband and limits within 5 spacings."""
+        if self.get_nband() != that.get_nband() or self.get_nband() <= 0:
+            return False
+        a, b = self.band_lims_wvn, that.band_lims_wvn
+        return bool((np.abs(a - b) < np.float32(5) * np.spacing(a)).all())
+
+    def gpoints_are_equal(self, that):
+        """rte/mo_optical_props.F90:1220-1229."""
+        return self.bands_are_equal(that) and self.get_ngpt() == that.get_ngpt() and \
+            bool((self.get_gpoint_bands() == that.get_gpoint_bands()).all())
+
+    def is_initialized(self):
+        return getattr(self, "band_lims_gpt", None) is not None
+
 
 class _OpticalPropsArry(OpticalProps):
+    ssa = g = None
+
     def get_ncol(self):
         return int(self.tau.shape[0])
 
     def get_nlay(self):
         return int(self.tau.shape[1])
+
+    def increment(self, op_io):
+        """op_in%increment(op_io) (rte/mo_optical_props.F90:882-1023): add self's optical properties to op_io,
+        at the same g-point resolution or, when self is defined by band, by band into op_io's g-points."""
+        if not self.bands_are_equal(op_io):
+            return "ty_optical_props%increment: optical properties objects have different band structures"
+        ncol, nlay, ngpt = op_io.get_ncol(), op_io.get_nlay(), op_io.get_ngpt()
+        if self.get_ncol() != ncol or self.get_nlay() != nlay:
+            return "ty_optical_props%increment: optical properties objects have different extents"
+        io2, in2 = isinstance(op_io, OpticalProps2str), isinstance(self, OpticalProps2str)
+        ctx = context(op_io.tau.device.index)
+        L = _lib.lib()
+        args = (_p(op_io.tau), _p(op_io.ssa) if io2 else None, _p(op_io.g) if io2 else None,
+                _p(self.tau), _p(self.ssa) if in2 else None, _p(self.g) if in2 else None)
+        if self.gpoints_are_equal(op_io):
+            check(L.rrtmgpnn_increment(ctx.h, ncol, nlay, ngpt, *args), "increment")
+            return ""
+        # Values defined by band have ngpt() = nband() (:955-958)
+        if self.get_ngpt() != op_io.get_nband():
+            return "ty_optical_props%increment: optical properties objects have incompatible g-point structures"
+        check(L.rrtmgpnn_increment_bybnd(ctx.h, ncol, nlay, ngpt, op_io.get_nband(),
+                                         int_array(op_io.band_lims_gpt.ravel()), *args), "increment_bybnd")
+        return ""
 
 
 class OpticalProps1scl(_OpticalPropsArry):
@@ -219,6 +270,10 @@ class OpticalProps1scl(_OpticalPropsArry):
             return "optical_props%alloc: must provide positive extents for ncol, nlay"
         dev = device or "cuda:%d" % torch.cuda.current_device()
         self.tau = torch.zeros((ncol, nlay, self.get_ngpt()), dtype=torch.float32, device=dev)
+        return ""
+
+    def delta_scale(self, for_=None):
+        """delta_scale_1scl (rte/mo_optical_props.F90:565-574): nothing to do for absorption optical depth."""
         return ""
 
 
@@ -235,6 +290,20 @@ class OpticalProps2str(_OpticalPropsArry):
         self.tau = torch.zeros(shape, dtype=torch.float32, device=dev)
         self.ssa = torch.zeros(shape, dtype=torch.float32, device=dev)
         self.g = torch.zeros(shape, dtype=torch.float32, device=dev)
+        return ""
+
+    def delta_scale(self, for_=None):
+        """delta_scale_2str (rte/mo_optical_props.F90:576-604); forward fraction g**2 unless `for_` is given."""
+        ctx = context(self.tau.device.index)
+        fw = None
+        if for_ is not None:
+            fw = _f32dev(for_, self.tau.device)
+            if tuple(fw.shape) != tuple(self.tau.shape):
+                return "delta_scale: dimension of 'for' don't match optical properties arrays"
+            if bool((fw < 0).any()) or bool((fw > 1).any()):
+                return "delta_scale: values of 'for' out of bounds [0,1]"
+        check(_lib.lib().rrtmgpnn_delta_scale_2str(ctx.h, self.tau.numel(), _p(self.tau), _p(self.ssa), _p(self.g),
+                                                   _p(fw)), "delta_scale_2str")
         return ""
 
 
@@ -414,6 +483,161 @@ class GasOpticsRRTMGP(OpticalProps):
             return "gas_optics(): array toa_src has wrong size"
         toa_src.copy_(torch.as_tensor(self.solar_source, device=toa_src.device).expand(ncol, ngpt))  # :594-599
         return ""
+
+
+# ---------------------------------------------------------------------------------------------
+class CloudOptics(OpticalProps):
+    """ty_cloud_optics (extensions/cloud_optics/mo_cloud_optics.F90): liquid + ice cloud optical properties by
+    band from a lookup table or Pade approximants of effective radius.  Tables live on the device."""
+
+    def __init__(self, device=None):
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.h = None
+
+    def _adopt(self, h):
+        if self.h:
+            _lib.lib().rrtmgpnn_cloud_optics_destroy(self.h)
+        self.h = h
+        nb, nr = _lib.c_int(), _lib.c_int()
+        r = (_lib.c_float * 4)()
+        check(_lib.lib().rrtmgpnn_cloud_optics_get(h, nb, nr, r), "cloud_optics_get")
+        self.nrghice = nr.value
+        self.radii = [float(v) for v in r]
+        self.icergh = 1
+        return ""
+
+    def load(self, which, use_lut=True):
+        """Coefficients of extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-{lw,sw}.nc (RBIN conversion);
+        the LUT (load_lut) or Pade (load_pade) method."""
+        path = data.cloud_optics_path(which)
+        m = data.load_cloud_optics(which)
+        e = self.init(m["bnd_limits_wavenumber"], name="RRTMGP cloud optics")
+        if e:
+            return e
+        h = _lib.c_vp()
+        check(_lib.lib().rrtmgpnn_cloud_optics_load(context(self.device).h, path.encode(), int(bool(use_lut)), h),
+              "cloud_optics_load(%s)" % path)
+        return self._adopt(h)
+
+    def load_lut(self, band_lims_wvn, radliq_lwr, radliq_upr, radice_lwr, radice_upr, lut_extliq, lut_ssaliq,
+                 lut_asyliq, lut_extice, lut_ssaice, lut_asyice):
+        """load_lut (:91-173).  Arrays in C order = Fortran shape reversed: liquid (nband, nsize_liq),
+        ice (nrghice, nband, nsize_ice)."""
+        e = self.init(band_lims_wvn, name="RRTMGP cloud optics")
+        if e:
+            return e
+        liq = [np.ascontiguousarray(a, np.float32) for a in (lut_extliq, lut_ssaliq, lut_asyliq)]
+        ice = [np.ascontiguousarray(a, np.float32) for a in (lut_extice, lut_ssaice, lut_asyice)]
+        nband = self.get_nband()
+        if liq[0].ndim != 2 or liq[0].shape[0] != nband:
+            return "cloud_optics%init(): number of bands inconsistent between lookup tables, spectral discretization"
+        if ice[0].ndim != 3 or ice[0].shape[1] != nband:
+            return "cloud_optics%init(): array lut_extice has the wrong number of bands"
+        if any(a.shape != liq[0].shape for a in liq[1:]):
+            return "cloud_optics%init(): array lut_ssaliq isn't consistently sized"
+        if any(a.shape != ice[0].shape for a in ice[1:]):
+            return "cloud_optics%init(): array lut_ssaice  isn't consistently sized"
+        h = _lib.c_vp()
+        F = lambda a: a.ctypes.data_as(_lib.P(_lib.c_float))  # noqa: E731
+        check(_lib.lib().rrtmgpnn_cloud_optics_create_lut(
+            context(self.device).h, nband, F(np.ascontiguousarray(self.band_lims_wvn)), liq[0].shape[1],
+            ice[0].shape[2], ice[0].shape[0], float(radliq_lwr), float(radliq_upr), float(radice_lwr),
+            float(radice_upr), *[F(a) for a in liq + ice], h), "cloud_optics_create_lut")
+        return self._adopt(h)
+
+    def load_pade(self, band_lims_wvn, pade_extliq, pade_ssaliq, pade_asyliq, pade_extice, pade_ssaice, pade_asyice,
+                  pade_sizreg_extliq, pade_sizreg_ssaliq, pade_sizreg_asyliq, pade_sizreg_extice, pade_sizreg_ssaice,
+                  pade_sizreg_asyice):
+        """load_pade (:179-301).  Coefficients in C order: liquid (ncoef, nsizereg, nband), ice
+        (nrghice, ncoef, nsizereg, nband); size-regime bounds (nsizereg + 1)."""
+        e = self.init(band_lims_wvn, name="RRTMGP cloud optics")
+        if e:
+            return e
+        c = [np.ascontiguousarray(a, np.float32) for a in (pade_extliq, pade_ssaliq, pade_asyliq, pade_extice,
+                                                            pade_ssaice, pade_asyice)]
+        b = [np.ascontiguousarray(a, np.float32) for a in (pade_sizreg_extliq, pade_sizreg_ssaliq, pade_sizreg_asyliq,
+                                                            pade_sizreg_extice, pade_sizreg_ssaice, pade_sizreg_asyice)]
+        if c[0].ndim != 3 or c[3].ndim != 4:
+            return "cloud_optics%init(): array pade_extice isn't consistently sized"
+        nsizereg = c[0].shape[1]
+        if nsizereg != 3:
+            return "cloud optics: code assumes exactly three size regimes for Pade approximants but data is otherwise"
+        if c[0].shape[2] != self.get_nband():
+            return "cloud_optics%init(): number of bands inconsistent between lookup tables, spectral discretization"
+        if any(x.shape != (nsizereg + 1,) for x in b):
+            return "cloud_optics%init(): one or more Pade size regime arrays are inconsistently sized"
+        h = _lib.c_vp()
+        F = lambda a: a.ctypes.data_as(_lib.P(_lib.c_float))  # noqa: E731
+        check(_lib.lib().rrtmgpnn_cloud_optics_create_pade(
+            context(self.device).h, self.get_nband(), F(np.ascontiguousarray(self.band_lims_wvn)), nsizereg,
+            c[0].shape[0], c[1].shape[0], c[3].shape[0], *[F(a) for a in c + b], h), "cloud_optics_create_pade")
+        return self._adopt(h)
+
+    def set_ice_roughness(self, icergh):
+        """set_ice_roughness (:541-554)."""
+        if not self.h:
+            return "cloud_optics%set_ice_roughness(): can't set before initialization"
+        if icergh < 1 or icergh > self.nrghice:
+            return "cloud optics: cloud ice surface roughness flag is out of bounds"
+        check(_lib.lib().rrtmgpnn_cloud_optics_set_ice_roughness(self.h, int(icergh)), "set_ice_roughness")
+        self.icergh = int(icergh)
+        return ""
+
+    def get_num_ice_roughness_types(self):
+        return self.nrghice if self.h else 0
+
+    def get_min_radius_liq(self):
+        return self.radii[0]
+
+    def get_max_radius_liq(self):
+        return self.radii[1]
+
+    def get_min_radius_ice(self):
+        return self.radii[2]
+
+    def get_max_radius_ice(self):
+        return self.radii[3]
+
+    def cloud_optics(self, clwp, ciwp, reliq, reice, optical_props):
+        """cloud_optics (:354-535): (ncol, nlay) water paths [g/m2] and effective radii [microns] -> optical
+        properties by band; absorption optical depth for 1scl, tau/ssa/g for 2str."""
+        if not self.h:
+            return "cloud optics: no data has been initialized"
+        ncol, nlay = clwp.shape
+        for name, a in (("ciwp", ciwp), ("reliq", reliq), ("reice", reice)):
+            if tuple(a.shape) != (ncol, nlay):
+                return "cloud optics: %s has wrong extents" % name
+        if optical_props.get_ncol() != ncol or optical_props.get_nlay() != nlay:
+            return "cloud optics: optical_props have wrong extents"
+        e = ""
+        if not self.bands_are_equal(optical_props):
+            e = "cloud optics: optical properties don't have the same band structure"
+        if optical_props.get_nband() != optical_props.get_ngpt():
+            e = "cloud optics: optical properties must be requested by band not g-points"
+        if e:
+            return e
+        dev = optical_props.tau.device
+        lwp, iwp, rl, ri = (_f32dev(a, dev) for a in (clwp, ciwp, reliq, reice))
+        if check_values:  # :436-444
+            liq, ice = lwp > 0, iwp > 0
+            if bool(((rl < self.radii[0]) | (rl > self.radii[1]))[liq].any()):
+                e = "cloud optics: liquid effective radius is out of bounds"
+            if bool(((ri < self.radii[2]) | (ri > self.radii[3]))[ice].any()):
+                e = "cloud optics: ice effective radius is out of bounds"
+            if e:
+                return e
+        is2 = isinstance(optical_props, OpticalProps2str)
+        check(_lib.lib().rrtmgpnn_cloud_optics_compute(
+            context(dev.index).h, self.h, ncol, nlay, _p(lwp), _p(iwp), _p(rl), _p(ri), _p(optical_props.tau),
+            _p(optical_props.ssa) if is2 else None, _p(optical_props.g) if is2 else None), "cloud_optics")
+        return ""
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.lib().rrtmgpnn_cloud_optics_destroy(self.h)
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------------------------

@@ -50,6 +50,34 @@ def load_kdist(which):
     return out
 
 
+def cloud_optics_path(which):
+    return os.path.join(DATA_DIR, "cloud_optics_%s.rbin" % which)
+
+
+def load_cloud_optics(which):
+    """Cloud-optics coefficients (extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-{lw,sw}.nc as RBIN):
+    LUT and Pade tables in the file's layout (C order = Fortran arrays reversed)."""
+    return rbin.read(cloud_optics_path(which))
+
+
+def allsky_clouds(problem, co):
+    """The all-sky example's cloud recipe (examples/all-sky/rrtmgp_allsky.F90:323-349): clouds where
+    100 hPa < p < 900 hPa in columns with mod(icol, 3) /= 0 (1-based icol); liquid water path 10 g/m2
+    where T > 263 K, ice 10 g/m2 where T < 273 K; effective radii at the middle of the tables' ranges.
+    Returns clwp, ciwp, rel, rei as (ncol, nlay) float32."""
+    play, tlay = np.asarray(problem["play"], np.float32), np.asarray(problem["tlay"], np.float32)
+    ncol = play.shape[0]
+    col = (np.arange(ncol) + 1) % 3 != 0
+    mask = (play > np.float32(100 * 100)) & (play < np.float32(900 * 100)) & col[:, None]
+    rel_val = np.float32(0.5) * (np.float32(co["radliq_lwr"][0]) + np.float32(co["radliq_upr"][0]))
+    rei_val = np.float32(0.5) * (np.float32(co["radice_lwr"][0]) + np.float32(co["radice_upr"][0]))
+    lwp = np.where(mask & (tlay > np.float32(263)), np.float32(10), np.float32(0)).astype(np.float32)
+    iwp = np.where(mask & (tlay < np.float32(273)), np.float32(10), np.float32(0)).astype(np.float32)
+    rel = np.where(lwp > 0, rel_val, np.float32(0)).astype(np.float32)
+    rei = np.where(iwp > 0, rei_val, np.float32(0)).astype(np.float32)
+    return lwp, iwp, rel, rei
+
+
 def spacing(x):
     x = np.float32(x)
     return np.float32(np.nextafter(x, np.float32(np.inf)) - x)

@@ -19,6 +19,11 @@ the band->g emissivity expansion, both solvers and the broadband reductions.  Co
 inputs that do not depend on the atmospheric state are prepared once: the SW incident flux
 (solar_source after set_tsi, renormalised to each column's TSI) and the per-g-point albedos.
 col_dry is computed once per step and shared by LW and SW (same h2o and plev).
+
+clouds=(lwp, iwp, rel, rei) makes it the all-sky step of examples/all-sky/rrtmgp_allsky.F90:366-446
+(config C4) with NN gas optics: cloud optics by band (LUT by default, ice roughness 2 as in the example,
+:219), added to the LW absorption optical depth by band (1scl increment), and for SW delta-scaled and
+added as a two-stream increment; the SW solver then sees a non-zero asymmetry parameter.
 """
 import numpy as np
 import torch
@@ -34,8 +39,9 @@ def _t(a, dev):
 
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
-                 sw_models=("sw_abs", "sw_ray"), fused=True):
+                 sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True):
         self.dev = torch.device("cuda", device)
+        self.allsky = clouds is not None
         self.fused = fused
         self.ctx = ctx or Context(device)
         L = self.L = _lib.lib()
@@ -78,7 +84,14 @@ class ClearSkyStep:
         if not fused:  # arrays the fused step never materialises
             self.lev_src = f(ncol, nlay + 1, self.ng_lw)
             self.sfc_src, self.sfc_jac = f(ncol, self.ng_lw), f(ncol, self.ng_lw)
+        if not fused or self.allsky:
             self.g_sw = f(ncol, nlay, self.ng_sw)
+        if self.allsky:
+            self.nb_sw = self.kd_sw["nband"]
+            self.lwp, self.iwp, self.rel, self.rei = (_t(a, dev) for a in clouds)
+            self.cld_tau_lw = f(ncol, nlay, self.nb_lw)
+            self.cld_tau_sw, self.cld_ssa_sw, self.cld_g_sw = (f(ncol, nlay, self.nb_sw) for _ in range(3))
+            self.cloud_lw, self.cloud_sw = (self._cloud_optics(w, cloud_lut, icergh) for w in ("lw", "sw"))
         self.lw_up, self.lw_dn = f(ncol, nlay + 1), f(ncol, nlay + 1)
         self.sw_up, self.sw_dn, self.sw_dir = f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1)
 
@@ -134,10 +147,20 @@ class ClearSkyStep:
                  (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None, p(self.tau_lw),
                   p(self.lay_src), p(self.lev_src), p(self.emis_gpt), p(self.sfc_src), p(self.lw_up), p(self.lw_dn))),
             ]
+        if self.allsky:  # clouds%increment(atmos) before rte_lw (rrtmgp_allsky.F90:383-395)
+            self._lims_sw = int_array(self.kd_sw["band_lims_gpt"].ravel())
+            self.calls += [
+                ("cloud_optics_lw", L.rrtmgpnn_cloud_optics_compute,
+                 (c, self.cloud_lw, ncol, nlay, p(self.lwp), p(self.iwp), p(self.rel), p(self.rei),
+                  p(self.cld_tau_lw), None, None)),
+                ("increment_lw", L.rrtmgpnn_increment_bybnd,
+                 (c, ncol, nlay, self.ng_lw, self.nb_lw, self._lims_lw, p(self.tau_lw), None, None,
+                  p(self.cld_tau_lw), None, None)),
+            ]
         self.calls += lw_calls
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
-        g_sw = None if fused else p(self.g_sw)
+        g_sw = p(self.g_sw) if (not fused or self.allsky) else None
         self.calls += [
             ("nn_inputs_sw", L.rrtmgpnn_compute_nn_inputs,
              (c, ncol, nlay, self.nx_sw, p(self.play), p(self.tlay), self._g_sw, self._nd_sw, self.sw_nets[0],
@@ -145,11 +168,40 @@ class ClearSkyStep:
             ("predict_nn_sw", L.rrtmgpnn_predict_nn_sw,
              (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.x_sw), p(self.col_dry), self._nets_sw, p(self.tau_sw),
               p(self.ssa_sw), g_sw)),
+        ]
+        if self.allsky:  # clouds%delta_scale(); clouds%increment(atmos) before rte_sw (rrtmgp_allsky.F90:420-433)
+            self.calls += [
+                ("cloud_optics_sw", L.rrtmgpnn_cloud_optics_compute,
+                 (c, self.cloud_sw, ncol, nlay, p(self.lwp), p(self.iwp), p(self.rel), p(self.rei),
+                  p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw))),
+                ("delta_scale_sw", L.rrtmgpnn_delta_scale_2str,
+                 (c, ncol * nlay * self.nb_sw, p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw), None)),
+                ("increment_sw", L.rrtmgpnn_increment_bybnd,
+                 (c, ncol, nlay, self.ng_sw, self.nb_sw, self._lims_sw, p(self.tau_sw), p(self.ssa_sw), g_sw,
+                  p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw))),
+            ]
+        self.calls += [
             ("sw_solver", L.rrtmgpnn_sw_solver_2stream,
              (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
               g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
         ]
         self.graph = None
+
+    def _cloud_optics(self, which, lut, icergh):
+        h = _lib.c_vp()
+        check(self.L.rrtmgpnn_cloud_optics_load(self.ctx.h, data.cloud_optics_path(which).encode(), int(bool(lut)), h),
+              "cloud_optics_load " + which)
+        check(self.L.rrtmgpnn_cloud_optics_set_ice_roughness(h, int(icergh)), "set_ice_roughness")
+        return h
+
+    def __del__(self):
+        for k in ("cloud_lw", "cloud_sw"):
+            h = getattr(self, k, None)
+            if h:
+                try:
+                    self.L.rrtmgpnn_cloud_optics_destroy(h)
+                except Exception:
+                    pass
 
     def step(self):
         for name, fn, args in self.calls:
@@ -179,6 +231,8 @@ class ClearSkyStep:
         """(inputs, outputs): the device tensors a host-resident caller would upload / download per step."""
         ins = [self.play, self.plev, self.tlay, self.tlev, self.tsfc, *self.gases.values(), self.sfc_emis, self.mu0,
                self.toa, self.alb]
+        if self.allsky:
+            ins += [self.lwp, self.iwp, self.rel, self.rei]
         return ins, [self.lw_up, self.lw_dn, self.sw_up, self.sw_dn, self.sw_dir]
 
     def fluxes(self):

@@ -15,6 +15,8 @@ Outputs
   rfmip_clear_sky.rbin   examples/rfmip-clear-sky/multiple_input4MIPs_radiation_RFMIP_UColorado-RFMIP-1-2_none.nc
   kdist_lw_g256.rbin     SURROGATE LW k-distribution tables (see below)
   kdist_sw_g224.rbin     SURROGATE SW k-distribution tables
+  cloud_optics_lw.rbin   extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-lw.nc (LUT + Pade coefficients)
+  cloud_optics_sw.rbin   extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-sw.nc
 
 NN model layout follows the reader `neural/mod_network_rrtmgp.F90:58-122`:
   file variable nn_weights_n is C-order (n_in, n_out) = Keras kernel; the
@@ -178,8 +180,26 @@ def convert_kdist():
           " sigma T^4", 5.670374419e-8 * 300.0 ** 4)
 
 
+def convert_cloud_optics():
+    """extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-{lw,sw}.nc (classic netCDF) -> cloud_optics_{lw,sw}.rbin.
+    Every variable keeps its file shape (C order = the reference's Fortran arrays reversed) and is stored
+    float32, the kind the reference reads it into (examples/all-sky/mo_load_cloud_coefficients.F90)."""
+    for which in ("lw", "sw"):
+        d = netcdf_file(os.path.join(REF, "extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-%s.nc" % which), "r",
+                        mmap=False)
+        out = {}
+        for name, v in d.variables.items():
+            a = np.array(v[:] if v.shape else v.getValue())
+            out[name] = np.atleast_1d(a).astype(np.float32)
+        rbin.write(os.path.join(OUT, "cloud_optics_%s.rbin" % which), out)
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
+    if sys.argv[1:] == ["cloud"]:
+        convert_cloud_optics()
+        sys.exit(0)
+    convert_cloud_optics()
     convert_nn("lw-g256-2018-12-04_absorption_58_58.nc", "nn_lw_g256_abs.rbin")
     convert_nn("lw-g256-2018-12-04_planck_frac_16_16.nc", "nn_lw_g256_pfrac.rbin")
     convert_nn("sw-g224-2018-12-04-absorption_16_16.nc", "nn_sw_g224_abs.rbin")

@@ -9,6 +9,7 @@ B=${TMPDIR:-/tmp}/rrtmgpnn_var
 rm -rf $B; mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off"
 /opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/api.cpp -o $B/api.o &
+/opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/kernels_clouds.hip -o $B/clouds.o &
 names=()
 for spec in "$@"; do
   n=${spec%%:*}; d=${spec#*:}; names+=($n)
@@ -17,6 +18,6 @@ for spec in "$@"; do
 done
 wait
 for n in "${names[@]}"; do
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/api.o $B/nn_$n.o $B/rte_$n.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/api.o $B/clouds.o $B/nn_$n.o $B/rte_$n.o
 done
 python3 tools/solver_variants.py $B ${CONFIG:-c3} "${names[@]}"
