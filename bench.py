@@ -61,7 +61,10 @@ def stage_work(name, step):
     N = ncol * nlay
     glw, gsw = step.ng_lw, step.ng_sw
     f4 = 4
-    nsw_out = 2 if (step.fused and not step.allsky) else 3  # tau, ssa (+ g when it is materialised)
+    nsw_out = 2 if step.fused else 3  # tau, ssa (+ g when it is materialised)
+    # all-sky, fused: the solvers also read the band-resolved cloud properties (1 LW, 3 SW arrays of nb x L)
+    cld_lw = step.nb_lw * nlay * f4 if (step.allsky and step.fused) else 0
+    cld_sw = 3 * step.nb_sw * nlay * f4 if (step.allsky and step.fused) else 0
     if name == "predict_nn_lw":
         from rrtmgpnn import data
         fl = sum(mlp_flops([int(v) for v in data.load_model(m)["dims"]]) for m in ("lw_abs", "lw_pfrac"))
@@ -73,12 +76,12 @@ def stage_work(name, step):
     if name == "lw_solver":
         if step.fused:
             # tau, pfrac (G x L) + emis (G) + tlay, tlev, tsfc read; flux up/dn written (124 880 B/col at L=60)
-            return "byte", ncol * ((2 * glw * nlay + glw + 2 * nlay + 2) * f4 + 2 * (nlay + 1) * f4), None, None
+            return "byte", ncol * ((2 * glw * nlay + glw + 2 * nlay + 2) * f4 + 2 * (nlay + 1) * f4 + cld_lw), None, None
         # tau, lay (G x L) + lev (G x (L+1)) + emis, sfc (G) read; flux up/dn (L+1) written
         return "byte", ncol * ((2 * glw * nlay + glw * (nlay + 1) + 2 * glw) * f4 + 2 * (nlay + 1) * f4), None, None
     if name == "sw_solver":
         # tau, ssa (, g) (G x L) + toa, alb_dir, alb_dif (G) + mu0 read; up/dn/dir written
-        return "byte", ncol * ((nsw_out * gsw * nlay + 3 * gsw + 1) * f4 + 3 * (nlay + 1) * f4), None, None
+        return "byte", ncol * ((nsw_out * gsw * nlay + 3 * gsw + 1) * f4 + 3 * (nlay + 1) * f4 + cld_sw), None, None
     if name in ("cloud_optics_lw", "cloud_optics_sw"):
         # lwp, iwp, rel, rei read; 1 (LW 1scl) or 3 (SW 2str) by-band arrays written
         nb = step.nb_lw if name.endswith("lw") else step.nb_sw
@@ -272,8 +275,9 @@ def main():
             "config": {"workload": workload, "ncol_per_gpu": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
                        "ngpt_sw": step.ng_sw, "parallelism": "column-sharded, 1 process per GPU",
                        "launch": "hipGraph replay" if use_graph else "eager",
-                       "kernels": ("class-layer sequence" if not step.fused else "fused Planck-in-LW-solver" +
-                                   ("" if step.allsky else ", g=0 elided"))},
+                       "kernels": ("class-layer sequence" if not step.fused else
+                                   "fused Planck-in-LW-solver, g=0 elided" +
+                                   (", cloud increments fused into both solvers" if step.allsky else ""))},
             "column_layers_per_s": round(value * nlay, 1),
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -135,6 +135,16 @@ int rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, 
                                      const float *tlev, const float *tsfc, int sfc_lay, const int *band_lims_gpt,
                                      float temp_ref_min, float totplnk_delta, const float *totplnk,
                                      const float *sfc_emis_gpt, float *flux_up, float *flux_dn);
+/* rrtmgpnn_lw_solver_noscat_planck with the atmosphere incremented by a band-resolved absorption optical depth
+ * tau_bnd (nbnd, nlay, ncol), e.g. cloud optics: the same fluxes as rrtmgpnn_increment_bybnd (1scl by 1scl)
+ * followed by rrtmgpnn_lw_solver_noscat_planck, but the g-point tau array is only read (it is left as it was). */
+int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                         int nmus, const float *Ds, const float *weights, const float *inc_flux,
+                                         const float *tau, const float *tau_bnd, const float *pfrac, int nbnd,
+                                         int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
+                                         int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
+                                         float totplnk_delta, const float *totplnk, const float *sfc_emis_gpt,
+                                         float *flux_up, float *flux_dn);
 /* sw_solver_2stream (:541-692).  inc_flux_dif may be NULL (zero, rte/mo_rte_sw.F90:197-210).
  * g may be NULL: asymmetry parameter identically zero, as gas_optics_ext's NN branch produces
  * (mo_gas_optics_rrtmgp.F90:560-567) -- same fluxes as passing a zero-filled array. */
@@ -143,6 +153,17 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
                                const float *tau, const float *ssa, const float *g, const float *mu0,
                                const float *sfc_alb_dir_gpt, const float *sfc_alb_dif_gpt,
                                float *flux_up, float *flux_dn, float *flux_dir);
+/* rrtmgpnn_sw_solver_2stream of the atmosphere incremented by band-resolved two-stream properties
+ * (tau, ssa, g)_bnd (nbnd, nlay, ncol) -- clouds%increment(atmos) (inc_2stream_by_2stream_bybnd,
+ * rte/kernels/mo_optical_props_kernels.F90:430-463) fused into the solver: same fluxes, bit for bit, as
+ * rrtmgpnn_increment_bybnd then rrtmgpnn_sw_solver_2stream; the inputs are left unchanged.  g may be NULL
+ * (zero).  band_lims_gpt HOST (2, nbnd) and must put every g-point in a band. */
+int rrtmgpnn_sw_solver_2stream_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                   const float *inc_flux, const float *inc_flux_dif, const float *tau,
+                                   const float *ssa, const float *g, int nbnd, const int *band_lims_gpt,
+                                   const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, const float *mu0,
+                                   const float *sfc_alb_dir_gpt, const float *sfc_alb_dif_gpt, float *flux_up,
+                                   float *flux_dn, float *flux_dir);
 /* expand (rte/mo_rte_lw.F90:429-447): (nband,ncol) -> (ngpt,ncol).  band_lims_gpt HOST (2,nband). */
 int rrtmgpnn_expand_band_to_gpt(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const int *band_lims_gpt,
                                 const float *arr_in, float *arr_out);

@@ -122,6 +122,17 @@ static int band_args(int nbnd, const int *lims, int ngpt, BandArgs &b)
   return RRTMGPNN_OK;
 }
 
+// the fused increments give every g-point a band: refuse band limits that leave one out
+static int bands_cover(const BandArgs &b, int ngpt)
+{
+  for (int g = 1; g <= ngpt; g++) {
+    bool in = false;
+    for (int i = 0; i < b.nbnd && !in; i++) in = g >= b.lims[2 * i] && g <= b.lims[2 * i + 1];
+    if (!in) return fail(RRTMGPNN_ERR_ARGUMENT, "band limits leave g-points outside every band");
+  }
+  return RRTMGPNN_OK;
+}
+
 }  // namespace rrtmgpnn
 
 using namespace rrtmgpnn;
@@ -494,7 +505,28 @@ int rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, 
   if (int rc = band_args(nbnd, band_lims_gpt, ngpt, b)) return rc;
   return launch_lw_noscat_planck(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, pfrac,
                                  nPlanckTemp, tlay, tlev, tsfc, sfc_lay, b, temp_ref_min, totplnk_delta, totplnk,
-                                 sfc_emis_gpt, flux_up, flux_dn);
+                                 sfc_emis_gpt, nullptr, flux_up, flux_dn);
+}
+
+int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                         int nmus, const float *Ds, const float *weights, const float *inc_flux,
+                                         const float *tau, const float *tau_bnd, const float *pfrac, int nbnd,
+                                         int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
+                                         int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
+                                         float totplnk_delta, const float *totplnk, const float *sfc_emis_gpt,
+                                         float *flux_up, float *flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!Ds || !weights || !tau || !tau_bnd || !pfrac || !tlay || !tlev || !tsfc || !totplnk || !sfc_emis_gpt ||
+      !flux_up || !flux_dn || ngpt < 1 || nlay < 1 || ncol < 0 || nPlanckTemp < 2 || sfc_lay < 1 || sfc_lay > nlay ||
+      !(totplnk_delta > 0.0f))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw_solver_noscat_planck_inc: bad argument");
+  BandArgs b;
+  if (int rc = band_args(nbnd, band_lims_gpt, ngpt, b)) return rc;
+  if (int rc = bands_cover(b, ngpt)) return rc;
+  return launch_lw_noscat_planck(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, pfrac,
+                                 nPlanckTemp, tlay, tlev, tsfc, sfc_lay, b, temp_ref_min, totplnk_delta, totplnk,
+                                 sfc_emis_gpt, tau_bnd, flux_up, flux_dn);
 }
 
 int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
@@ -507,7 +539,25 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
       !flux_dir || ngpt < 1 || nlay < 1 || ncol < 0)
     return fail(RRTMGPNN_ERR_ARGUMENT, "sw_solver_2stream: bad argument");
   return launch_sw_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, sfc_alb_dir_gpt,
-                           sfc_alb_dif_gpt, flux_up, flux_dn, flux_dir);
+                           sfc_alb_dif_gpt, nullptr, nullptr, nullptr, nullptr, flux_up, flux_dn, flux_dir);
+}
+
+int rrtmgpnn_sw_solver_2stream_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                   const float *inc_flux, const float *inc_flux_dif, const float *tau,
+                                   const float *ssa, const float *g, int nbnd, const int *band_lims_gpt,
+                                   const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, const float *mu0,
+                                   const float *sfc_alb_dir_gpt, const float *sfc_alb_dif_gpt, float *flux_up,
+                                   float *flux_dn, float *flux_dir)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!inc_flux || !tau || !ssa || !tau_bnd || !ssa_bnd || !g_bnd || !mu0 || !sfc_alb_dir_gpt || !sfc_alb_dif_gpt ||
+      !flux_up || !flux_dn || !flux_dir || ngpt < 1 || nlay < 1 || ncol < 0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "sw_solver_2stream_inc: bad argument");
+  BandArgs b;
+  if (int rc = band_args(nbnd, band_lims_gpt, ngpt, b)) return rc;
+  if (int rc = bands_cover(b, ngpt)) return rc;
+  return launch_sw_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, sfc_alb_dir_gpt,
+                           sfc_alb_dif_gpt, &b, tau_bnd, ssa_bnd, g_bnd, flux_up, flux_dn, flux_dir);
 }
 
 int rrtmgpnn_expand_band_to_gpt(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const int *band_lims_gpt,

@@ -260,13 +260,17 @@ struct LwPlanck {
 // fused Planck table size in floats, padded so the ring that follows stays 16-byte aligned
 __host__ __device__ constexpr size_t lw_btab_floats(int nbnd, int nlay) { return ((size_t)nbnd * (2 * nlay + 2) + 3) & ~(size_t)3; }
 
-template <bool kFused, int kPF>
+// kInc: tau is incremented by a band-resolved absorption optical depth tau_bnd (nbnd, nlay, ncol) as it is
+// read -- inc_1scalar_by_1scalar_bybnd (rte/kernels/mo_optical_props_kernels.F90:358-372), tau + tau_bnd(band),
+// the same single add -- so clouds%increment(atmos) never makes a pass over the g-point array.
+template <bool kFused, bool kInc, int kPF>
 __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwAngles ang,
                                            const float *__restrict__ inc_flux, const float *__restrict__ tau,
                                            const float *__restrict__ lay, const float *__restrict__ lev,
                                            const float *__restrict__ emis, const float *__restrict__ sfc,
-                                           LwPlanck pl, BandArgs bands, float *__restrict__ ws,
-                                           float *__restrict__ flux_up, float *__restrict__ flux_dn)
+                                           LwPlanck pl, BandArgs bands, const float *__restrict__ tau_bnd,
+                                           float *__restrict__ ws, float *__restrict__ flux_up,
+                                           float *__restrict__ flux_dn)
 {
   static_assert(kRing % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -289,6 +293,11 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   const ColArr Tlay(lay, (size_t)ngpt * nlay * icol, row * nlay);  // lay_source, or pfrac when fused
   const ColArr Tlev(lev, (size_t)ngpt * nlev * icol, row * nlev);
   const float *bl = btab;  // this lane's band row
+  // kInc: this lane's band-resolved increment, one value per layer at stride nbnd
+  const uint32_t irow = 4u * (uint32_t)bands.nbnd, vb = kInc ? 4u * (uint32_t)band_of(bands, gc) : 0u;
+  const ColArr Tinc(kInc ? tau_bnd : tau, kInc ? (size_t)bands.nbnd * nlay * icol : 0, irow * nlay);
+  auto ld_inc = [&](int l) { return kInc ? Tinc.ld(vb, irow * (uint32_t)l) : 0.0f; };
+  auto tau_of = [&](float t, float ti) { return kInc ? t + ti : t; };
   float ss;
   if constexpr (kFused) {
     // band Planck values for this column: B_b(tlay(l)) at [b][l], B_b(tlev(l)) at [b][nlay+l], B_b(tsfc) at
@@ -350,11 +359,11 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     // downward: lw_transport_noscat_dn (:982-1009); j-th layer from the top is l = lay_dn(j)
     auto lay_dn = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
     {
-      float pt[kPF], py[kPF], pv[kPF];
+      float pt[kPF], py[kPF], pv[kPF], pi[kPF];
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int l = lay_dn(min(p, nlay - 1));
-        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pv[p] = lev_ld(l + 1);
+        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pv[p] = lev_ld(l + 1); pi[p] = ld_inc(l);
       }
       for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
@@ -362,10 +371,11 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
           const int j = j0 + r, p = r % kPF;
           if (j < nlay) {
             const int l = lay_dn(j);
-            const float t = pt[p] * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
+            const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
             {
               const int ln = lay_dn(min(j + kPF, nlay - 1));
               pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
+              pi[p] = ld_inc(ln);
             }
             const float T = ref_expf_nb(-t, etab);
             const float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
@@ -384,11 +394,11 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     // upward: lw_transport_noscat_up (:950-980); j-th layer from the surface is l = lay_up(j)
     auto lay_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
     {
-      float pt[kPF], py[kPF], pv[kPF];
+      float pt[kPF], py[kPF], pv[kPF], pi[kPF];
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int l = lay_up(min(p, nlay - 1));
-        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l);
+        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
         if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * l);
       }
       for (int j0 = 0; j0 < nlay; j0 += kRing) {
@@ -398,10 +408,11 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
           if (j < nlay) {
             const int l = lay_up(j);
             // fused: lev(l) = pfrac(l) * B(tlev(l)) (l < nlay), from the layer's own pfrac
-            const float t = pt[p] * D, ly = lay_src(py[p], l), lvup = lev_src(kFused ? py[p] : pv[p], l);
+            const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l);
+            const float lvup = lev_src(kFused ? py[p] : pv[p], l);
             {
               const int ln = lay_up(min(j + kPF, nlay - 1));
-              pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln);
+              pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pi[p] = ld_inc(ln);
               if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * ln);
             }
             const float T = ref_expf_nb(-t, etab);
@@ -432,12 +443,12 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   }
 }
 
-template <bool kFused>
+template <bool kFused, bool kInc>
 static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
                           const float *Ds, const float *wts, const float *inc_flux, const float *tau,
                           const float *lay_or_pfrac, const float *lev_source, const float *sfc_emis,
-                          const float *sfc_source, const LwPlanck &pl, const BandArgs &bands, float *flux_up,
-                          float *flux_dn)
+                          const float *sfc_source, const LwPlanck &pl, const BandArgs &bands, const float *tau_bnd,
+                          float *flux_up, float *flux_dn)
 {
   if (ncol == 0) return RRTMGPNN_OK;
   if (nmus < 1 || nmus > 4) return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: nmus must be 1..4");
@@ -454,10 +465,10 @@ static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, i
     int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL((lw_noscat_kernel<kFused, kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF>), dim3(ncol),
+  hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF>), dim3(ncol),
                      dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac,
-                     kFused ? lay_or_pfrac : lev_source, sfc_emis, sfc_source, pl, bands, (float *)ws, flux_up,
-                     flux_dn);
+                     kFused ? lay_or_pfrac : lev_source, sfc_emis, sfc_source, pl, bands, tau_bnd, (float *)ws,
+                     flux_up, flux_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_noscat_kernel");
   return RRTMGPNN_OK;
 }
@@ -469,19 +480,23 @@ int launch_lw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
 {
   LwPlanck pl{};
   BandArgs b{};
-  return launch_lw_impl<false>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, lay_source, lev_source,
-                               sfc_emis, sfc_source, pl, b, flux_up, flux_dn);
+  return launch_lw_impl<false, false>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, lay_source,
+                                      lev_source, sfc_emis, sfc_source, pl, b, nullptr, flux_up, flux_dn);
 }
 
 int launch_lw_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
                             const float *Ds, const float *wts, const float *inc_flux, const float *tau,
                             const float *pfrac, int ntemp, const float *tlay, const float *tlev, const float *tsfc,
                             int sfc_lay, const BandArgs &bands, float temp_ref_min, float totplnk_delta,
-                            const float *totplnk, const float *sfc_emis, float *flux_up, float *flux_dn)
+                            const float *totplnk, const float *sfc_emis, const float *tau_bnd, float *flux_up,
+                            float *flux_dn)
 {
   LwPlanck pl{tlay, tlev, tsfc, totplnk, ntemp, sfc_lay, temp_ref_min, totplnk_delta};
-  return launch_lw_impl<true>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, pfrac, nullptr, sfc_emis,
-                              nullptr, pl, bands, flux_up, flux_dn);
+  if (tau_bnd)
+    return launch_lw_impl<true, true>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, pfrac, nullptr,
+                                      sfc_emis, nullptr, pl, bands, tau_bnd, flux_up, flux_dn);
+  return launch_lw_impl<true, false>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, pfrac, nullptr,
+                                     sfc_emis, nullptr, pl, bands, nullptr, flux_up, flux_dn);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -555,12 +570,29 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   return c;
 }
 
-template <bool kHasG, int kPF>
+// inc_2stream_by_2stream_bybnd (rte/kernels/mo_optical_props_kernels.F90:430-463) for one g-point: the
+// same expressions as increment_bybnd_kernel, so the incremented properties are bit-identical.
+__device__ __forceinline__ void inc_2str(float &t1, float &w1, float &g1, float t2, float w2, float g2)
+{
+  const float eps = 3.0f * FLT_MIN;
+  const float tau12 = t1 + t2;
+  const float tauscat12 = t1 * w1 + t2 * w2;
+  g1 = (t1 * w1 * g1 + t2 * w2 * g2) / fmaxf(eps, tauscat12);
+  w1 = tauscat12 / fmaxf(eps, tau12);
+  t1 = tau12;
+}
+
+// kInc: the atmosphere is incremented by band-resolved two-stream properties (tau, ssa, g)_bnd as it is read
+// (clouds%increment(atmos) fused).  Pass 1 needs only tau + tau_bnd; pass 2 forms the full increment and
+// parks (tau, ssa, g) in three workspace planes that pass 3 reads in place of the inputs.
+template <bool kHasG, bool kInc, int kPF>
 __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1,
                                             const float *__restrict__ inc_flux, const float *__restrict__ inc_dif,
                                             const float *__restrict__ tau, const float *__restrict__ ssa,
                                             const float *__restrict__ gg, const float *__restrict__ mu0p,
                                             const float *__restrict__ alb_dir, const float *__restrict__ alb_dif,
+                                            BandArgs bands, const float *__restrict__ tau_bnd,
+                                            const float *__restrict__ ssa_bnd, const float *__restrict__ g_bnd,
                                             float *__restrict__ ws, float *__restrict__ flux_up,
                                             float *__restrict__ flux_dn, float *__restrict__ flux_dir)
 {
@@ -580,6 +612,16 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   const ColArr Ttau(tau, cl, row * nlay), Tssa(ssa, cl, row * nlay), Tg(kHasG ? gg : tau, cl, row * nlay);
   const ColArr WA(ws, cv, row * nlev), WB(ws + plane, cv, row * nlev), WS(ws + 2 * plane, cv, row * nlev),
       WD(ws + 3 * plane, cv, row * nlev);
+  // kInc: incremented (tau, ssa, g) planes (ngpt, nlay, ncol) after the four level planes
+  const size_t lplane = (size_t)ngpt * nlay * ncol;
+  float *wi = ws + 4 * plane;
+  const ColArr WT(wi, cl, row * nlay), WW(wi + lplane, cl, row * nlay), WG(wi + 2 * lplane, cl, row * nlay);
+  // band-resolved increments: this lane's band in the VGPR offset, the layer in the SGPR offset
+  const size_t cb = (size_t)bands.nbnd * nlay * icol;
+  const uint32_t brow = 4u * (uint32_t)bands.nbnd, vb = kInc ? 4u * (uint32_t)band_of(bands, gc) : 0u;
+  const ColArr Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, brow * nlay), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, brow * nlay),
+      Bg(kInc ? g_bnd : tau, kInc ? cb : 0, brow * nlay);
+  auto ld_bnd = [&](const ColArr &a, int l) { return kInc ? a.ld(vb, brow * (uint32_t)l) : 0.0f; };
   const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
   // "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
   auto lev_above = [&](int l) { return top_at_1 ? l : l + 1; };
@@ -594,17 +636,25 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   float Fd = Ftop;
   if (on) WA.st(Fd, vg, row * top);
   {
-    float pt[kPF];
+    float pt[kPF], pi[kPF];
 #pragma unroll
-    for (int p = 0; p < kPF; p++) pt[p] = Ttau.ld(vg, row * lay_of_down(min(p, nlay - 1)));
+    for (int p = 0; p < kPF; p++) {
+      const int l = lay_of_down(min(p, nlay - 1));
+      pt[p] = Ttau.ld(vg, row * l);
+      pi[p] = ld_bnd(Bt, l);
+    }
     for (int j0 = 0; j0 < nlay; j0 += kPF) {
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
         if (j < nlay) {
           const int l = lay_of_down(j);
-          const float t = pt[p];
-          pt[p] = Ttau.ld(vg, row * lay_of_down(min(j + kPF, nlay - 1)));
+          const float t = kInc ? pt[p] + pi[p] : pt[p];  // tau12 of the increment
+          {
+            const int ln = lay_of_down(min(j + kPF, nlay - 1));
+            pt[p] = Ttau.ld(vg, row * ln);
+            pi[p] = ld_bnd(Bt, ln);
+          }
           Fd = ref_expf_nb(-t * mu0_inv, etab) * Fd;
           if (on) WA.st(Fd, vg, row * lev_below(l));
         }
@@ -619,26 +669,34 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
     WS.st(src_b, vg, row * sfcl);
   }
   {
-    float pt[kPF], pw[kPF], pg[kPF], pf[kPF];
-#pragma unroll
-    for (int p = 0; p < kPF; p++) {
-      const int l = lay_of_up(min(p, nlay - 1));
+    float pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
+    auto load2 = [&](int p, int l) {
       const uint32_t s = row * l;
       pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(l));
-    }
+      if constexpr (kInc) {
+        qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < kPF; p++) load2(p, lay_of_up(min(p, nlay - 1)));
     for (int j0 = 0; j0 < nlay; j0 += kPF) {
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
         if (j < nlay) {
           const int l = lay_of_up(j);
-          const float t = pt[p], w0 = pw[p], g0 = pg[p], Fin = pf[p];
-          {
-            const int ln = lay_of_up(min(j + kPF, nlay - 1));
-            const uint32_t s = row * ln;
-            pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(ln));
+          float t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : 0.0f;
+          const float Fin = pf[p];
+          if constexpr (kInc) {
+            inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);
+            if (on) {
+              WT.st(t, vg, row * l);
+              WW.st(w0, vg, row * l);
+              WG.st(g0, vg, row * l);
+            }
           }
-          SwCoef c = sw_two_stream(t, w0, kHasG ? g0 : 0.0f, mu0, mu0_inv, Fin, etab);
+          load2(p, lay_of_up(min(j + kPF, nlay - 1)));
+          SwCoef c = sw_two_stream(t, w0, g0, mu0, mu0_inv, Fin, etab);
           const float denom = rcp_rn_normal(1.0f - c.Rdif * alb_b);
           const float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
           const float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
@@ -675,7 +733,12 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
     float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF];
     auto load = [&](int p, int l) {
       const uint32_t s = row * l, sb = row * lev_below(l);
-      pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pd[p] = WD.ld(vg, s);
+      if constexpr (kInc) {
+        pt[p] = WT.ld(vg, s); pw[p] = WW.ld(vg, s); pg[p] = WG.ld(vg, s);
+      } else {
+        pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s);
+      }
+      pd[p] = WD.ld(vg, s);
       pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb); pf[p] = WA.ld(vg, sb);
     };
 #pragma unroll
@@ -688,7 +751,7 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
           const float t = pt[p], w0 = pw[p], g0 = pg[p], Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
           load(p, lay_of_down(min(j + kPF, nlay - 1)));
           // R_dif, T_dif exactly as pass 2 computed them (same inputs, same expressions -> same bits)
-          const SwDif d = sw_dif(t, w0, kHasG ? g0 : 0.0f, etab);
+          const SwDif d = sw_dif(t, w0, (kHasG || kInc) ? g0 : 0.0f, etab);
           const float denom = rcp_rn_normal(1.0f - d.Rdif * alb);
           Fdn = (d.Tdif * Fdn + d.Rdif * src + Sdn) * denom;  // Eq 13 (adding :1583-1591)
           const float up = Fdn * alb + src;                    // Eq 12
@@ -705,26 +768,47 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   }
 }
 
+template <bool kHasG, bool kInc>
+static void sw_launch(rrtmgpnn_context *ctx, size_t lds, int threads, int ngpt, int nlay, int ncol, int top_at_1,
+                      const float *inc_flux, const float *inc_flux_dif, const float *tau, const float *ssa,
+                      const float *g, const float *mu0, const float *alb_dir, const float *alb_dif,
+                      const BandArgs &bands, const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws,
+                      float *flux_up, float *flux_dn, float *flux_dir)
+{
+  hipLaunchKernelGGL((sw_2stream_kernel<kHasG, kInc, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream,
+                     ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, bands,
+                     tau_bnd, ssa_bnd, g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
+}
+
 int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                       const float *inc_flux_dif, const float *tau, const float *ssa, const float *g, const float *mu0,
-                      const float *alb_dir, const float *alb_dif, float *flux_up, float *flux_dn, float *flux_dir)
+                      const float *alb_dir, const float *alb_dif, const BandArgs *bands, const float *tau_bnd,
+                      const float *ssa_bnd, const float *g_bnd, float *flux_up, float *flux_dn, float *flux_dir)
 {
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
+  const bool inc = bands != nullptr;
   void *ws = nullptr;
-  int rc = ctx->workspace(sizeof(float) * 4 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
+  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc ? 3 * (size_t)ngpt * nlay * ncol : 0);
+  int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;
   int threads = (ngpt + 63) / 64 * 64;
   size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRingSw * ngpt + (size_t)3 * (nlay + 1) * 4);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
-  if (g)
-    hipLaunchKernelGGL((sw_2stream_kernel<true, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
-                       nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, (float *)ws,
-                       flux_up, flux_dn, flux_dir);
+  const BandArgs nob{};
+  const BandArgs &b = inc ? *bands : nob;
+  if (inc && g)
+    sw_launch<true, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
+                          alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
+  else if (inc)
+    sw_launch<false, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
+                           alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
+  else if (g)
+    sw_launch<true, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
+                           alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
   else
-    hipLaunchKernelGGL((sw_2stream_kernel<false, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream,
-                       ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif,
-                       (float *)ws, flux_up, flux_dn, flux_dir);
+    sw_launch<false, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
+                            alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
   RRTMGPNN_LAUNCH_CHECK("sw_2stream_kernel");
   return RRTMGPNN_OK;
 }

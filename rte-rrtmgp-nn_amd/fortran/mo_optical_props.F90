@@ -1,7 +1,10 @@
 ! mo_optical_props -- drop-in for rte/mo_optical_props.F90: spectral discretisation and the
 ! (ngpt, nlay, ncol) optical-property arrays, g-point fastest (the fork's layout, :99,179-180).
+! increment (:882-1023) and delta_scale (:565-604) run in the HIP kernels behind the C ABI.
 module mo_optical_props
+  use, intrinsic :: iso_c_binding
   use mo_rte_kind, only: wp
+  use mo_rrtmgpnn_c
   implicit none
   private
 
@@ -21,6 +24,8 @@ module mo_optical_props
     procedure, public  :: get_gpoint_bands
     procedure, public  :: set_name
     procedure, public  :: get_name
+    procedure, public  :: bands_are_equal
+    procedure, public  :: gpoints_are_equal
   end type ty_optical_props
 
   type, extends(ty_optical_props), public :: ty_optical_props_arry
@@ -28,6 +33,7 @@ module mo_optical_props
   contains
     procedure, public :: get_ncol
     procedure, public :: get_nlay
+    procedure, public :: increment
   end type ty_optical_props_arry
 
   type, extends(ty_optical_props_arry), public :: ty_optical_props_1scl
@@ -37,6 +43,7 @@ module mo_optical_props
     procedure, private :: copy_and_alloc_1scl
     generic,   public  :: alloc_1scl => alloc_only_1scl, init_and_alloc_1scl, copy_and_alloc_1scl
     procedure, public  :: finalize => finalize_1scl
+    procedure, public  :: delta_scale => delta_scale_1scl
   end type ty_optical_props_1scl
 
   type, extends(ty_optical_props_arry), public :: ty_optical_props_2str
@@ -47,6 +54,7 @@ module mo_optical_props
     procedure, private :: copy_and_alloc_2str
     generic,   public  :: alloc_2str => alloc_only_2str, init_and_alloc_2str, copy_and_alloc_2str
     procedure, public  :: finalize => finalize_2str
+    procedure, public  :: delta_scale => delta_scale_2str
   end type ty_optical_props_2str
 
 contains
@@ -144,6 +152,22 @@ contains
     character(len=len_trim(this%name)) :: get_name
     get_name = trim(this%name)
   end function get_name
+
+  ! Same number of bands, limits within 5 spacings (rte/mo_optical_props.F90:1204-1214)
+  pure logical function bands_are_equal(this, that)
+    class(ty_optical_props), intent(in) :: this, that
+    bands_are_equal = this%get_nband() == that%get_nband() .and. this%get_nband() > 0
+    if (.not. bands_are_equal) return
+    bands_are_equal = all(abs(this%band_lims_wvn - that%band_lims_wvn) < 5._wp * spacing(this%band_lims_wvn))
+  end function bands_are_equal
+
+  ! Same bands, same g-points, same band <-> g-point mapping (:1220-1229)
+  pure logical function gpoints_are_equal(this, that)
+    class(ty_optical_props), intent(in) :: this, that
+    gpoints_are_equal = this%bands_are_equal(that) .and. this%get_ngpt() == that%get_ngpt()
+    if (.not. gpoints_are_equal) return
+    gpoints_are_equal = all(this%get_gpoint_bands() == that%get_gpoint_bands())
+  end function gpoints_are_equal
 
   pure integer function get_ncol(this)
     class(ty_optical_props_arry), intent(in) :: this
@@ -253,4 +277,109 @@ contains
     if (allocated(this%band2gpt)) deallocate(this%band2gpt)
     if (allocated(this%band_lims_wvn)) deallocate(this%band_lims_wvn)
   end subroutine finalize_2str
+
+  ! op_in%increment(op_io) (rte/mo_optical_props.F90:882-1023): add op_in to op_io, at the same g-point
+  ! resolution or, when op_in is defined by band, by band into op_io's g-points.
+  function increment(op_in, op_io) result(err_message)
+    class(ty_optical_props_arry), intent(in)    :: op_in
+    class(ty_optical_props_arry), intent(inout) :: op_io
+    character(len=128) :: err_message
+    integer :: ncol, nlay, ngpt, n_io, n_in
+    logical :: same
+    type(c_ptr) :: t1, s1, g1, t2, s2, g2
+    character(len=128) :: e
+
+    err_message = ""
+    if (.not. op_in%bands_are_equal(op_io)) then
+      err_message = "ty_optical_props%increment: optical properties objects have different band structures"; return
+    end if
+    ncol = op_io%get_ncol()
+    nlay = op_io%get_nlay()
+    ngpt = op_io%get_ngpt()
+    if (op_in%get_ncol() /= ncol .or. op_in%get_nlay() /= nlay) then
+      err_message = "ty_optical_props%increment: optical properties objects have different extents"; return
+    end if
+    same = op_in%gpoints_are_equal(op_io)
+    if (.not. same .and. op_in%get_ngpt() /= op_io%get_nband()) then  ! by band: ngpt() = nband() (:955-958)
+      err_message = "ty_optical_props%increment: optical properties objects have incompatible g-point structures"
+      return
+    end if
+    n_io = size(op_io%tau)
+    n_in = size(op_in%tau)
+    s1 = c_null_ptr; g1 = c_null_ptr; s2 = c_null_ptr; g2 = c_null_ptr
+    t1 = dev_upload(op_io%tau, n_io)
+    select type (op_io)
+    class is (ty_optical_props_2str)
+      s1 = dev_upload(op_io%ssa, n_io)
+      g1 = dev_upload(op_io%g, n_io)
+    end select
+    t2 = dev_upload(op_in%tau, n_in)
+    select type (op_in)
+    class is (ty_optical_props_2str)
+      s2 = dev_upload(op_in%ssa, n_in)
+      g2 = dev_upload(op_in%g, n_in)
+    end select
+    if (same) then
+      err_message = rrtmgpnn_check(c_rrtmgpnn_increment(rrtmgpnn_ctx(), ncol, nlay, ngpt, t1, s1, g1, t2, s2, g2), &
+                                   "ty_optical_props%increment")
+    else
+      err_message = rrtmgpnn_check(c_rrtmgpnn_increment_bybnd(rrtmgpnn_ctx(), ncol, nlay, ngpt, op_io%get_nband(), &
+                                   op_io%band2gpt, t1, s1, g1, t2, s2, g2), "ty_optical_props%increment")
+    end if
+    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "ty_optical_props%increment")
+    if (err_message == '') err_message = e
+    if (err_message == '') then
+      call dev_download(op_io%tau, t1, n_io)
+      select type (op_io)
+      class is (ty_optical_props_2str)
+        call dev_download(op_io%ssa, s1, n_io)
+        call dev_download(op_io%g, g1, n_io)
+      end select
+    end if
+    call dev_free(t1); call dev_free(s1); call dev_free(g1)
+    call dev_free(t2); call dev_free(s2); call dev_free(g2)
+  end function increment
+
+  ! delta_scale_1scl (:565-574): absorption optical depth needs no scaling
+  function delta_scale_1scl(this, for) result(err_message)
+    class(ty_optical_props_1scl), intent(inout) :: this
+    real(wp), dimension(:,:,:), optional, intent(in) :: for
+    character(len=128) :: err_message
+    err_message = ''
+  end function delta_scale_1scl
+
+  ! delta_scale_2str (:576-604): forward-scattering fraction `for`, g**2 if absent
+  function delta_scale_2str(this, for) result(err_message)
+    class(ty_optical_props_2str), intent(inout) :: this
+    real(wp), dimension(:,:,:), optional, intent(in) :: for
+    character(len=128) :: err_message
+    integer :: n
+    type(c_ptr) :: dt, ds, dg, df
+    character(len=128) :: e
+    err_message = ''
+    n = size(this%tau)
+    df = c_null_ptr
+    if (present(for)) then
+      if (any(shape(for) /= shape(this%tau))) then
+        err_message = "delta_scale: dimension of 'for' don't match optical properties arrays"; return
+      end if
+      if (any(for < 0._wp .or. for > 1._wp)) then
+        err_message = "delta_scale: values of 'for' out of bounds [0,1]"; return
+      end if
+      df = dev_upload(for, n)
+    end if
+    dt = dev_upload(this%tau, n)
+    ds = dev_upload(this%ssa, n)
+    dg = dev_upload(this%g, n)
+    err_message = rrtmgpnn_check(c_rrtmgpnn_delta_scale_2str(rrtmgpnn_ctx(), int(n, c_long_long), dt, ds, dg, df), &
+                                 "delta_scale")
+    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "delta_scale")
+    if (err_message == '') err_message = e
+    if (err_message == '') then
+      call dev_download(this%tau, dt, n)
+      call dev_download(this%ssa, ds, n)
+      call dev_download(this%g, dg, n)
+    end if
+    call dev_free(dt); call dev_free(ds); call dev_free(dg); call dev_free(df)
+  end function delta_scale_2str
 end module mo_optical_props

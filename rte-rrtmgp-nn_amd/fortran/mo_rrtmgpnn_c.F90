@@ -13,6 +13,10 @@ module mo_rrtmgpnn_c
             c_rrtmgpnn_interpolate_tlev, c_rrtmgpnn_predict_nn_lw, c_rrtmgpnn_predict_nn_sw, &
             c_rrtmgpnn_compute_planck_source_nn, c_rrtmgpnn_lw_solver_noscat, c_rrtmgpnn_sw_solver_2stream, &
             c_rrtmgpnn_expand_band_to_gpt, c_rrtmgpnn_context_synchronize, c_rrtmgpnn_network_destroy
+  public :: c_rrtmgpnn_cloud_optics_create_lut, c_rrtmgpnn_cloud_optics_create_pade, &
+            c_rrtmgpnn_cloud_optics_set_ice_roughness, c_rrtmgpnn_cloud_optics_load, c_rrtmgpnn_cloud_optics_get, &
+            c_rrtmgpnn_cloud_optics_destroy, c_rrtmgpnn_cloud_optics_compute, c_rrtmgpnn_increment_bybnd, &
+            c_rrtmgpnn_increment, c_rrtmgpnn_delta_scale_2str
 
   type(c_ptr), save :: ctx_ = c_null_ptr
   !$omp threadprivate(ctx_)
@@ -125,6 +129,78 @@ module mo_rrtmgpnn_c
       type(c_ptr), value :: ctx, arr_in, arr_out
       integer(c_int), value :: nband, ngpt, ncol
       integer(c_int), dimension(*), intent(in) :: band_lims_gpt
+    end function
+    ! ---- all-sky: cloud optics, increment, delta scaling ----
+    integer(c_int) function c_rrtmgpnn_cloud_optics_create_lut(ctx, nband, band_lims_wvn, nsize_liq, nsize_ice, &
+        nrghice, radliq_lwr, radliq_upr, radice_lwr, radice_upr, lut_extliq, lut_ssaliq, lut_asyliq, lut_extice, &
+        lut_ssaice, lut_asyice, co) bind(C, name="rrtmgpnn_cloud_optics_create_lut")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: nband, nsize_liq, nsize_ice, nrghice
+      real(c_float), value :: radliq_lwr, radliq_upr, radice_lwr, radice_upr
+      real(c_float), dimension(*), intent(in) :: band_lims_wvn, lut_extliq, lut_ssaliq, lut_asyliq, lut_extice, &
+                                                 lut_ssaice, lut_asyice
+      type(c_ptr), intent(out) :: co
+    end function
+    integer(c_int) function c_rrtmgpnn_cloud_optics_create_pade(ctx, nband, band_lims_wvn, nsizereg, ncoef_ext, &
+        ncoef_ssa, nrghice, pade_extliq, pade_ssaliq, pade_asyliq, pade_extice, pade_ssaice, pade_asyice, &
+        sizreg_extliq, sizreg_ssaliq, sizreg_asyliq, sizreg_extice, sizreg_ssaice, sizreg_asyice, co) &
+        bind(C, name="rrtmgpnn_cloud_optics_create_pade")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx
+      integer(c_int), value :: nband, nsizereg, ncoef_ext, ncoef_ssa, nrghice
+      real(c_float), dimension(*), intent(in) :: band_lims_wvn, pade_extliq, pade_ssaliq, pade_asyliq, &
+                                                 pade_extice, pade_ssaice, pade_asyice, sizreg_extliq, &
+                                                 sizreg_ssaliq, sizreg_asyliq, sizreg_extice, sizreg_ssaice, &
+                                                 sizreg_asyice
+      type(c_ptr), intent(out) :: co
+    end function
+    integer(c_int) function c_rrtmgpnn_cloud_optics_load(ctx, path, use_lut, co) bind(C, name="rrtmgpnn_cloud_optics_load")
+      import :: c_int, c_ptr, c_char
+      type(c_ptr), value :: ctx
+      character(kind=c_char), dimension(*), intent(in) :: path
+      integer(c_int), value :: use_lut
+      type(c_ptr), intent(out) :: co
+    end function
+    integer(c_int) function c_rrtmgpnn_cloud_optics_set_ice_roughness(co, icergh) &
+        bind(C, name="rrtmgpnn_cloud_optics_set_ice_roughness")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: co
+      integer(c_int), value :: icergh
+    end function
+    integer(c_int) function c_rrtmgpnn_cloud_optics_get(co, nband, nrghice, radii) bind(C, name="rrtmgpnn_cloud_optics_get")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: co
+      integer(c_int), intent(out) :: nband, nrghice
+      real(c_float), dimension(4), intent(out) :: radii
+    end function
+    integer(c_int) function c_rrtmgpnn_cloud_optics_destroy(co) bind(C, name="rrtmgpnn_cloud_optics_destroy")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: co
+    end function
+    integer(c_int) function c_rrtmgpnn_cloud_optics_compute(ctx, co, ncol, nlay, clwp, ciwp, reliq, reice, tau, ssa, g) &
+        bind(C, name="rrtmgpnn_cloud_optics_compute")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, co, clwp, ciwp, reliq, reice, tau, ssa, g
+      integer(c_int), value :: ncol, nlay
+    end function
+    integer(c_int) function c_rrtmgpnn_increment_bybnd(ctx, ncol, nlay, ngpt, nband, band_lims_gpt, tau_io, ssa_io, &
+        g_io, tau_in, ssa_in, g_in) bind(C, name="rrtmgpnn_increment_bybnd")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, tau_io, ssa_io, g_io, tau_in, ssa_in, g_in
+      integer(c_int), value :: ncol, nlay, ngpt, nband
+      integer(c_int), dimension(*), intent(in) :: band_lims_gpt
+    end function
+    integer(c_int) function c_rrtmgpnn_increment(ctx, ncol, nlay, ngpt, tau_io, ssa_io, g_io, tau_in, ssa_in, g_in) &
+        bind(C, name="rrtmgpnn_increment")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, tau_io, ssa_io, g_io, tau_in, ssa_in, g_in
+      integer(c_int), value :: ncol, nlay, ngpt
+    end function
+    integer(c_int) function c_rrtmgpnn_delta_scale_2str(ctx, n, tau, ssa, g, fwd) bind(C, name="rrtmgpnn_delta_scale_2str")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, tau, ssa, g, fwd
+      integer(c_long_long), value :: n
     end function
     integer(c_size_t) function c_strlen(s) bind(C, name="strlen")
       import :: c_size_t, c_ptr

@@ -46,6 +46,13 @@ SIGNATURES = {
     "rrtmgpnn_lw_solver_noscat_planck": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float), P(c_float),
                                                  c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, P(c_int),
                                                  c_float, c_float, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_lw_solver_noscat_planck_inc": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float),
+                                                     P(c_float), c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                                                     c_vp, c_int, P(c_int), c_float, c_float, c_vp, c_vp, c_vp,
+                                                     c_vp]),
+    "rrtmgpnn_sw_solver_2stream_inc": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                               c_int, P(c_int), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp]),
     "rrtmgpnn_sw_solver_2stream": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_expand_band_to_gpt": (c_int, [c_vp, c_int, c_int, c_int, P(c_int), c_vp, c_vp]),

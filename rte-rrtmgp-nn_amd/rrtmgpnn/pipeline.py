@@ -84,7 +84,7 @@ class ClearSkyStep:
         if not fused:  # arrays the fused step never materialises
             self.lev_src = f(ncol, nlay + 1, self.ng_lw)
             self.sfc_src, self.sfc_jac = f(ncol, self.ng_lw), f(ncol, self.ng_lw)
-        if not fused or self.allsky:
+        if not fused:
             self.g_sw = f(ncol, nlay, self.ng_sw)
         if self.allsky:
             self.nb_sw = self.kd_sw["nband"]
@@ -123,16 +123,17 @@ class ClearSkyStep:
               p(self.tau_lw), p(self.lay_src))),
         ]
         if fused:
-            # compute_Planck_source_nn fused into the LW solver (sources formed in-kernel from pfrac)
+            # compute_Planck_source_nn fused into the LW solver (sources formed in-kernel from pfrac); all-sky:
+            # the cloud increment by band is added as tau is read (rrtmgpnn_lw_solver_noscat_planck_inc)
+            tail = (p(self.tau_lw),) + ((p(self.cld_tau_lw),) if self.allsky else ()) + (
+                p(self.lay_src), self.nb_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev), p(self.tsfc),
+                self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]), float(self.kd_lw["totplnk_delta"]),
+                p(self.totplnk), p(self.emis_gpt), p(self.lw_up), p(self.lw_dn))
             lw_calls = [
                 ("expand_emis", L.rrtmgpnn_expand_band_to_gpt,
                  (c, self.nb_lw, self.ng_lw, ncol, self._lims_lw, p(self.sfc_emis), p(self.emis_gpt))),
-                ("lw_solver", L.rrtmgpnn_lw_solver_noscat_planck,
-                 (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None, p(self.tau_lw),
-                  p(self.lay_src), self.nb_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev), p(self.tsfc),
-                  self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]),
-                  float(self.kd_lw["totplnk_delta"]), p(self.totplnk), p(self.emis_gpt), p(self.lw_up),
-                  p(self.lw_dn))),
+                ("lw_solver", L.rrtmgpnn_lw_solver_noscat_planck_inc if self.allsky else L.rrtmgpnn_lw_solver_noscat_planck,
+                 (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None) + tail),
             ]
         else:
             lw_calls = [
@@ -153,14 +154,17 @@ class ClearSkyStep:
                 ("cloud_optics_lw", L.rrtmgpnn_cloud_optics_compute,
                  (c, self.cloud_lw, ncol, nlay, p(self.lwp), p(self.iwp), p(self.rel), p(self.rei),
                   p(self.cld_tau_lw), None, None)),
-                ("increment_lw", L.rrtmgpnn_increment_bybnd,
-                 (c, ncol, nlay, self.ng_lw, self.nb_lw, self._lims_lw, p(self.tau_lw), None, None,
-                  p(self.cld_tau_lw), None, None)),
             ]
+            if not fused:
+                self.calls += [
+                    ("increment_lw", L.rrtmgpnn_increment_bybnd,
+                     (c, ncol, nlay, self.ng_lw, self.nb_lw, self._lims_lw, p(self.tau_lw), None, None,
+                      p(self.cld_tau_lw), None, None)),
+                ]
         self.calls += lw_calls
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
-        g_sw = p(self.g_sw) if (not fused or self.allsky) else None
+        g_sw = None if fused else p(self.g_sw)
         self.calls += [
             ("nn_inputs_sw", L.rrtmgpnn_compute_nn_inputs,
              (c, ncol, nlay, self.nx_sw, p(self.play), p(self.tlay), self._g_sw, self._nd_sw, self.sw_nets[0],
@@ -176,15 +180,26 @@ class ClearSkyStep:
                   p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw))),
                 ("delta_scale_sw", L.rrtmgpnn_delta_scale_2str,
                  (c, ncol * nlay * self.nb_sw, p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw), None)),
-                ("increment_sw", L.rrtmgpnn_increment_bybnd,
-                 (c, ncol, nlay, self.ng_sw, self.nb_sw, self._lims_sw, p(self.tau_sw), p(self.ssa_sw), g_sw,
-                  p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw))),
             ]
-        self.calls += [
-            ("sw_solver", L.rrtmgpnn_sw_solver_2stream,
-             (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
-              g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
-        ]
+            if not fused:
+                self.calls += [
+                    ("increment_sw", L.rrtmgpnn_increment_bybnd,
+                     (c, ncol, nlay, self.ng_sw, self.nb_sw, self._lims_sw, p(self.tau_sw), p(self.ssa_sw), g_sw,
+                      p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw))),
+                ]
+        if self.allsky and fused:  # clouds%increment(atmos) fused into the solver (rrtmgpnn_sw_solver_2stream_inc)
+            self.calls += [
+                ("sw_solver", L.rrtmgpnn_sw_solver_2stream_inc,
+                 (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw), None,
+                  self.nb_sw, self._lims_sw, p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw), p(self.mu0),
+                  p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
+            ]
+        else:
+            self.calls += [
+                ("sw_solver", L.rrtmgpnn_sw_solver_2stream,
+                 (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
+                  g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
+            ]
         self.graph = None
 
     def _cloud_optics(self, which, lut, icergh):

@@ -250,3 +250,81 @@ def test_allsky_graph_replay_matches_eager(dev, rfmip):
     b = step.fluxes()
     for k in a:
         np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("top_at_1", [True, False])
+@pytest.mark.parametrize("nmus", [1, 3])
+def test_fused_increment_solvers_match_increment_then_solve(dev, rfmip, top_at_1, nmus):
+    """rrtmgpnn_{lw_solver_noscat_planck,sw_solver_2stream}_inc == increment_bybnd followed by the plain solver,
+    bit for bit, in both orientations (and for LW with several angles); the inputs are left untouched."""
+    from rrtmgpnn import _lib, data
+    from rrtmgpnn._lib import float_array, int_array
+    from rrtmgpnn.api import GAUSS_DS, GAUSS_WTS, context
+    L = _lib.lib()
+    rng = np.random.default_rng(5 + nmus + 10 * top_at_1)
+    ncol, nlay = 45, 33
+    kl, ks = data.load_kdist("lw"), data.load_kdist("sw")
+    ctx = context(0).h
+    t = lambda a: T(a, dev)  # noqa: E731
+    # ---- LW ----
+    ng, nb = kl["ngpt"], kl["nband"]
+    tau = t(rng.lognormal(-2, 2, (ncol, nlay, ng)))
+    pfrac = t(rng.uniform(0, 0.2, (ncol, nlay, ng)))
+    tb = t(np.where(rng.uniform(size=(ncol, nlay, nb)) < 0.4, rng.lognormal(0, 1, (ncol, nlay, nb)), 0))
+    tlay = t(rng.uniform(200, 300, (ncol, nlay)))
+    tlev = t(rng.uniform(200, 300, (ncol, nlay + 1)))
+    tsfc = t(rng.uniform(250, 310, ncol))
+    emis = t(rng.uniform(0.9, 1, (ncol, ng)))
+    lims = int_array(kl["band_lims_gpt"].ravel())
+    totplnk = t(kl["totplnk"])
+    f = lambda *s: torch.empty(s, device=dev)  # noqa: E731
+    up1, dn1, up2, dn2 = f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1)
+    tau0 = tau.clone()
+    common = (nb, kl["nPlanckTemp"], tlay.data_ptr(), tlev.data_ptr(), tsfc.data_ptr(), nlay if top_at_1 else 1, lims,
+              float(kl["temp_ref_min"][0]), float(kl["totplnk_delta"]), totplnk.data_ptr(), emis.data_ptr())
+    Ds, W = float_array(GAUSS_DS[nmus]), float_array(GAUSS_WTS[nmus])
+    _lib.check(L.rrtmgpnn_lw_solver_noscat_planck_inc(ctx, ng, nlay, ncol, int(top_at_1), nmus, Ds, W, None,
+                                                      tau.data_ptr(), tb.data_ptr(), pfrac.data_ptr(), *common,
+                                                      up1.data_ptr(), dn1.data_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(tau, tau0)
+    _lib.check(L.rrtmgpnn_increment_bybnd(ctx, ncol, nlay, ng, nb, lims, tau.data_ptr(), None, None, tb.data_ptr(),
+                                          None, None))
+    _lib.check(L.rrtmgpnn_lw_solver_noscat_planck(ctx, ng, nlay, ncol, int(top_at_1), nmus, Ds, W, None,
+                                                  tau.data_ptr(), pfrac.data_ptr(), *common, up2.data_ptr(),
+                                                  dn2.data_ptr()))
+    torch.cuda.synchronize()
+    assert torch.equal(up1, up2) and torch.equal(dn1, dn2)
+    # ---- SW ----
+    ng, nb = ks["ngpt"], ks["nband"]
+    tau = t(rng.lognormal(-2, 2, (ncol, nlay, ng)))
+    ssa = t(rng.uniform(0, 1, (ncol, nlay, ng)))
+    gg = t(rng.uniform(0, 0.8, (ncol, nlay, ng)))
+    cl = rng.uniform(size=(ncol, nlay, nb)) < 0.4
+    bt = t(np.where(cl, rng.lognormal(0, 1, (ncol, nlay, nb)), 0))
+    bw = t(np.where(cl, rng.uniform(0.5, 1, (ncol, nlay, nb)), 0))
+    bg = t(np.where(cl, rng.uniform(0, 0.9, (ncol, nlay, nb)), 0))
+    mu0 = t(rng.uniform(0.1, 1, ncol))
+    inc = t(rng.uniform(0, 5, (ncol, ng)))
+    alb = t(rng.uniform(0, 1, (ncol, ng)))
+    lims = int_array(ks["band_lims_gpt"].ravel())
+    outs = [[f(ncol, nlay + 1) for _ in range(3)] for _ in range(2)]
+    for with_g in (True, False):
+        g_in = gg if with_g else None
+        saved = [a.clone() for a in (tau, ssa, gg)]
+        _lib.check(L.rrtmgpnn_sw_solver_2stream_inc(
+            ctx, ng, nlay, ncol, int(top_at_1), inc.data_ptr(), None, tau.data_ptr(), ssa.data_ptr(),
+            None if g_in is None else g_in.data_ptr(), nb, lims, bt.data_ptr(), bw.data_ptr(), bg.data_ptr(),
+            mu0.data_ptr(), alb.data_ptr(), alb.data_ptr(), *[o.data_ptr() for o in outs[0]]))
+        torch.cuda.synchronize()
+        assert all(torch.equal(a, b) for a, b in zip(saved, (tau, ssa, gg)))
+        t2, s2 = tau.clone(), ssa.clone()
+        g2 = gg.clone() if with_g else torch.zeros_like(gg)
+        _lib.check(L.rrtmgpnn_increment_bybnd(ctx, ncol, nlay, ng, nb, lims, t2.data_ptr(), s2.data_ptr(),
+                                              g2.data_ptr(), bt.data_ptr(), bw.data_ptr(), bg.data_ptr()))
+        _lib.check(L.rrtmgpnn_sw_solver_2stream(ctx, ng, nlay, ncol, int(top_at_1), inc.data_ptr(), None,
+                                                t2.data_ptr(), s2.data_ptr(), g2.data_ptr(), mu0.data_ptr(),
+                                                alb.data_ptr(), alb.data_ptr(), *[o.data_ptr() for o in outs[1]]))
+        torch.cuda.synchronize()
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), "with_g=%s" % with_g
