@@ -594,7 +594,7 @@ int rrtmgpnn_cloud_optics_create_lut(rrtmgpnn_context *ctx, int nband, const flo
                                      const float *lut_ssaice, const float *lut_asyice, rrtmgpnn_cloud_optics **co)
 {
   if (int rc = check_ctx(ctx)) return rc;
-  if (!co || nband < 1 || nsize_liq < 2 || nsize_ice < 2 || nrghice < 1 || !lut_extliq || !lut_ssaliq ||
+  if (!co || nband < 1 || nband > 256 || nsize_liq < 2 || nsize_ice < 2 || nrghice < 1 || !lut_extliq || !lut_ssaliq ||
       !lut_asyliq || !lut_extice || !lut_ssaice || !lut_asyice)
     return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_create_lut: bad argument");
   auto *c = new rrtmgpnn_cloud_optics();
@@ -630,7 +630,7 @@ int rrtmgpnn_cloud_optics_create_pade(rrtmgpnn_context *ctx, int nband, const fl
                                       rrtmgpnn_cloud_optics **co)
 {
   if (int rc = check_ctx(ctx)) return rc;
-  if (!co || nband < 1 || nrghice < 1 || !pade_extliq || !pade_ssaliq || !pade_asyliq || !pade_extice ||
+  if (!co || nband < 1 || nband > 256 || nrghice < 1 || !pade_extliq || !pade_ssaliq || !pade_asyliq || !pade_extice ||
       !pade_ssaice || !pade_asyice || !sizreg_extliq || !sizreg_ssaliq || !sizreg_asyliq || !sizreg_extice ||
       !sizreg_ssaice || !sizreg_asyice)
     return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_create_pade: bad argument");

@@ -73,14 +73,16 @@ __device__ __forceinline__ void from_pade(float wp, float re, const CloudTab &c,
   tsg = ts * pade_eval<2, 2>(b, c.nband, c.nsizereg, pade_irad(re, c.sizreg[3 * k + 2]), re, c.pade[3 * k + 2]);
 }
 
-__global__ void cloud_optics_kernel(long long n, CloudTab c, const float *__restrict__ clwp,
+// block = rpb (lay, col) rows x nband bands; a thread keeps its band and strides over rows
+__global__ void cloud_optics_kernel(long long nrow, int rpb, CloudTab c, const float *__restrict__ clwp,
                                     const float *__restrict__ ciwp, const float *__restrict__ reliq,
                                     const float *__restrict__ reice, float *__restrict__ tau, float *__restrict__ ssa,
                                     float *__restrict__ g)
 {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const long long s = i / c.nband;
-    const int b = (int)(i - s * c.nband);
+  const int b = threadIdx.x % c.nband, r0 = threadIdx.x / c.nband;
+  if (r0 >= rpb) return;
+  for (long long s = (long long)blockIdx.x * rpb + r0; s < nrow; s += (long long)gridDim.x * rpb) {
+    const long long i = b + (long long)c.nband * s;
     float lt = 0.0f, lts = 0.0f, ltsg = 0.0f, it = 0.0f, its = 0.0f, itsg = 0.0f;
     const float lw = clwp[s], iw = ciwp[s];
     if (lw > 0.0f) {
@@ -137,8 +139,11 @@ int launch_cloud_optics(rrtmgpnn_context *ctx, const rrtmgpnn_cloud_optics *co, 
     c.pade[5] = co->d_tab + co->off[5] + stride_ssa * r;
     for (int k = 0; k < 6; k++) c.sizreg[k] = co->d_tab + co->off[6 + k];
   }
-  hipLaunchKernelGGL(cloud_optics_kernel, dim3(grid_for(ctx, n, 256)), dim3(256), 0, ctx->stream, n, c, clwp, ciwp,
-                     reliq, reice, tau, ssa, g);
+  const long long nrow = (long long)nlay * ncol;
+  const int rpb = 256 / co->nband;
+  const long long want = (nrow + rpb - 1) / rpb, cap = (long long)ctx->num_cus * 8;
+  hipLaunchKernelGGL(cloud_optics_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(rpb * co->nband), 0,
+                     ctx->stream, nrow, rpb, c, clwp, ciwp, reliq, reice, tau, ssa, g);
   RRTMGPNN_LAUNCH_CHECK("cloud_optics_kernel");
   return RRTMGPNN_OK;
 }
@@ -146,23 +151,27 @@ int launch_cloud_optics(rrtmgpnn_context *ctx, const rrtmgpnn_cloud_optics *co, 
 // ------------------------------------------------------------------------------------------
 // increment by band (:358-484).  nstr_io / nstr_in: 1 (tau) or 2 (tau, ssa, g).
 // ------------------------------------------------------------------------------------------
+// One thread per g-point (block = ngpt rounded up to a wave), blocks striding over (lay, col) rows: the
+// g-point's band is looked up once per thread and every row is a contiguous load/store of ngpt values.
 template <int IO, int IN, bool kSame>
-__global__ void increment_bybnd_kernel(long long n, int ngpt, int nbnd, BandArgs bands, float *__restrict__ tau1,
+__global__ void increment_bybnd_kernel(long long nrow, int ngpt, int nbnd, BandArgs bands, float *__restrict__ tau1,
                                        float *__restrict__ ssa1, float *__restrict__ g1,
                                        const float *__restrict__ tau2, const float *__restrict__ ssa2,
                                        const float *__restrict__ g2)
 {
   const float eps = 3.0f * FLT_MIN;  // 3*tiny(1.0_wp) (mo_optical_props_kernels.F90:31)
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    long long ib = i;  // kSame: both sets at the same g-point resolution (increment_*_by_*, :109-219)
-    if constexpr (!kSame) {
-      const long long s = i / ngpt;
-      const int igpt = (int)(i - s * ngpt);
-      int b = 0;
-      while (b < bands.nbnd - 1 && igpt >= bands.lims[2 * b + 1]) b++;  // lims 1-based: band b ends at lims[2b+1]
-      if (igpt < bands.lims[2 * b] - 1 || igpt >= bands.lims[2 * b + 1]) continue;  // g-point in no band: untouched
-      ib = b + s * nbnd;
-    }
+  const int igpt = threadIdx.x;
+  if (igpt >= ngpt) return;
+  int b = igpt;  // kSame: both sets at the same g-point resolution (increment_*_by_*, :109-219)
+  if constexpr (!kSame) {
+    b = -1;  // lims 1-based; a g-point in no band is left untouched
+    for (int k = 0; k < bands.nbnd && b < 0; k++)
+      if (igpt >= bands.lims[2 * k] - 1 && igpt < bands.lims[2 * k + 1]) b = k;
+    if (b < 0) return;
+  }
+  const int nin = kSame ? ngpt : nbnd;
+  for (long long r = blockIdx.x; r < nrow; r += gridDim.x) {
+    const long long i = igpt + (long long)ngpt * r, ib = b + (long long)nin * r;
     if constexpr (IO == 1) {
       tau1[i] = IN == 1 ? tau1[i] + tau2[ib] : tau1[i] + tau2[ib] * (1.0f - ssa2[ib]);
     } else if constexpr (IN == 1) {
@@ -181,29 +190,32 @@ __global__ void increment_bybnd_kernel(long long n, int ngpt, int nbnd, BandArgs
 }
 
 template <bool kSame>
-static void launch_inc(rrtmgpnn_context *ctx, long long n, int ngpt, const BandArgs &bands, float *tau1, float *ssa1,
+static void launch_inc(rrtmgpnn_context *ctx, long long nrow, int ngpt, const BandArgs &bands, float *tau1, float *ssa1,
                        float *g1, const float *tau2, const float *ssa2, const float *g2)
 {
-  const dim3 grid(grid_for(ctx, n, 256)), block(256);
+  const int threads = (ngpt + 63) / 64 * 64;
+  const long long cap = (long long)ctx->num_cus * (2048 / threads);
+  const dim3 grid((unsigned)(nrow < cap ? nrow : cap)), block(threads);
   const int nb = bands.nbnd;
   if (!ssa1 && !ssa2)
-    hipLaunchKernelGGL((increment_bybnd_kernel<1, 1, kSame>), grid, block, 0, ctx->stream, n, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
+    hipLaunchKernelGGL((increment_bybnd_kernel<1, 1, kSame>), grid, block, 0, ctx->stream, nrow, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
   else if (!ssa1)
-    hipLaunchKernelGGL((increment_bybnd_kernel<1, 2, kSame>), grid, block, 0, ctx->stream, n, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
+    hipLaunchKernelGGL((increment_bybnd_kernel<1, 2, kSame>), grid, block, 0, ctx->stream, nrow, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
   else if (!ssa2)
-    hipLaunchKernelGGL((increment_bybnd_kernel<2, 1, kSame>), grid, block, 0, ctx->stream, n, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
+    hipLaunchKernelGGL((increment_bybnd_kernel<2, 1, kSame>), grid, block, 0, ctx->stream, nrow, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
   else
-    hipLaunchKernelGGL((increment_bybnd_kernel<2, 2, kSame>), grid, block, 0, ctx->stream, n, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
+    hipLaunchKernelGGL((increment_bybnd_kernel<2, 2, kSame>), grid, block, 0, ctx->stream, nrow, ngpt, nb, bands, tau1, ssa1, g1, tau2, ssa2, g2);
 }
 
 // bands == nullptr: both sets at the same resolution (ngpt values per layer each)
 int launch_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, const BandArgs *bands, float *tau1,
                            float *ssa1, float *g1, const float *tau2, const float *ssa2, const float *g2)
 {
-  const long long n = (long long)ngpt * nlay * ncol;
-  if (n == 0) return RRTMGPNN_OK;
-  if (bands) launch_inc<false>(ctx, n, ngpt, *bands, tau1, ssa1, g1, tau2, ssa2, g2);
-  else launch_inc<true>(ctx, n, ngpt, BandArgs{}, tau1, ssa1, g1, tau2, ssa2, g2);
+  const long long nrow = (long long)nlay * ncol;
+  if (nrow == 0) return RRTMGPNN_OK;
+  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "increment: more than 1024 g-points");
+  if (bands) launch_inc<false>(ctx, nrow, ngpt, *bands, tau1, ssa1, g1, tau2, ssa2, g2);
+  else launch_inc<true>(ctx, nrow, ngpt, BandArgs{}, tau1, ssa1, g1, tau2, ssa2, g2);
   RRTMGPNN_LAUNCH_CHECK("increment_bybnd_kernel");
   return RRTMGPNN_OK;
 }

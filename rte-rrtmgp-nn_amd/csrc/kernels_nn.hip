@@ -44,27 +44,44 @@ struct NnInArgs {
   float mx[kMaxInputs];
 };
 
-__global__ void nn_inputs_kernel(int ncol, int nlay, int nx, const float *__restrict__ play,
-                                 const float *__restrict__ tlay, GasArgs gas, NnInArgs sc, float *__restrict__ out)
+// One thread per (lay, col) sample.  The gas loop is unrolled over kMaxInputs so every gas pointer and
+// scaling constant stays a kernel-argument SGPR (a runtime index would put them in scratch), and the
+// block's (nx x 256) outputs are staged in LDS so the store to `out` is one contiguous stream.
+constexpr int kInThreads = 256;
+
+__global__ void __launch_bounds__(kInThreads) nn_inputs_kernel(int ncol, int nlay, int nx,
+                                                               const float *__restrict__ play,
+                                                               const float *__restrict__ tlay, GasArgs gas,
+                                                               NnInArgs sc, float *__restrict__ out)
 {
-  long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long N = (long long)ncol * nlay;
-  if (s >= N) return;
-  int ilay = (int)(s % nlay);
-  float *o = out + (size_t)nx * s;
-  o[0] = (tlay[s] - sc.mn[0]) / (sc.mx[0] - sc.mn[0]);
-  o[1] = (ref_logf(play[s]) - sc.mn[1]) / (sc.mx[1] - sc.mn[1]);
-  o[2] = (sqrtf(sqrtf(gas.p[2][s])) - sc.mn[2]) / (sc.mx[2] - sc.mn[2]);
-  o[3] = (sqrtf(sqrtf(gas.p[3][s])) - sc.mn[3]) / (sc.mx[3] - sc.mn[3]);
-  for (int k = 4; k < nx; k++) {
-    float c;
-    const float *p = gas.p[k];
-    if (!p) c = 0.0f;
-    else if (gas.nd[k] == 0) c = p[0];
-    else if (gas.nd[k] == 1) c = p[ilay];
-    else c = p[s];
-    o[k] = (c - sc.mn[k]) / (sc.mx[k] - sc.mn[k]);
+  __shared__ float st[kInThreads * kMaxInputs];
+  const long long N = (long long)ncol * nlay;
+  const long long s0 = (long long)blockIdx.x * kInThreads;
+  const long long s = s0 + threadIdx.x;
+  const int ns = (int)min((long long)kInThreads, N - s0);
+  if (s < N) {
+    const int ilay = (int)(s % nlay);
+    float *o = st + nx * threadIdx.x;
+    o[0] = (tlay[s] - sc.mn[0]) / (sc.mx[0] - sc.mn[0]);
+    o[1] = (ref_logf(play[s]) - sc.mn[1]) / (sc.mx[1] - sc.mn[1]);
+    o[2] = (sqrtf(sqrtf(gas.p[2][s])) - sc.mn[2]) / (sc.mx[2] - sc.mn[2]);
+    o[3] = (sqrtf(sqrtf(gas.p[3][s])) - sc.mn[3]) / (sc.mx[3] - sc.mn[3]);
+#pragma unroll
+    for (int k = 4; k < kMaxInputs; k++) {
+      if (k < nx) {
+        float c;
+        const float *p = gas.p[k];
+        if (!p) c = 0.0f;
+        else if (gas.nd[k] == 0) c = p[0];
+        else if (gas.nd[k] == 1) c = p[ilay];
+        else c = p[s];
+        o[k] = (c - sc.mn[k]) / (sc.mx[k] - sc.mn[k]);
+      }
+    }
   }
+  __syncthreads();
+  float *dst = out + (size_t)nx * s0;
+  for (int i = threadIdx.x; i < nx * ns; i += kInThreads) dst[i] = st[i];
 }
 
 __global__ void col_dry_kernel(int ncol, int nlay, const float *__restrict__ h2o, const float *__restrict__ plev,
@@ -108,8 +125,9 @@ int launch_nn_inputs(rrtmgpnn_context *ctx, int ncol, int nlay, int nx, const fl
   for (int k = 0; k < nx; k++) { sc.mn[k] = in_min_max[k]; sc.mx[k] = in_min_max[nx + k]; }
   long long N = (long long)ncol * nlay;
   if (N == 0) return RRTMGPNN_OK;
-  hipLaunchKernelGGL(nn_inputs_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream, ncol, nlay,
-                     nx, play, tlay, gas, sc, out);
+  if (nx < 4 || nx > kMaxInputs) return fail(RRTMGPNN_ERR_ARGUMENT, "nn_inputs: need 4..32 inputs");
+  hipLaunchKernelGGL(nn_inputs_kernel, dim3((unsigned)((N + kInThreads - 1) / kInThreads)), dim3(kInThreads), 0,
+                     ctx->stream, ncol, nlay, nx, play, tlay, gas, sc, out);
   RRTMGPNN_LAUNCH_CHECK("nn_inputs_kernel");
   return RRTMGPNN_OK;
 }
