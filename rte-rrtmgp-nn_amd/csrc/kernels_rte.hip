@@ -155,6 +155,12 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 #define SW_BOUNDS
 #endif
 static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
+// SW with a fused increment: park the incremented (tau, ssa, g) in workspace for pass 3 (1), or have pass 3
+// re-read the inputs and form the increment again (0: three fewer planes written, one fewer read)
+#ifndef RRTMGPNN_SW_INC_PARK
+#define RRTMGPNN_SW_INC_PARK 1
+#endif
+static constexpr bool kSwIncPark = RRTMGPNN_SW_INC_PARK != 0;
 static constexpr int kLwMaxG = RRTMGPNN_LW_WAVES > 0 ? 256 : 1024;  // g-points per column block
 static constexpr int kSwMaxG = RRTMGPNN_SW_WAVES > 0 ? 256 : 1024;
 static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS
@@ -689,7 +695,7 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
           const float Fin = pf[p];
           if constexpr (kInc) {
             inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);
-            if (on) {
+            if (kSwIncPark && on) {
               WT.st(t, vg, row * l);
               WW.st(w0, vg, row * l);
               WG.st(g0, vg, row * l);
@@ -730,13 +736,16 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0);  // Eq 12 at the top; alb_b/src_b hold the top level's values
   flush(1, top, 1);
   {
-    float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF];
+    float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load = [&](int p, int l) {
       const uint32_t s = row * l, sb = row * lev_below(l);
-      if constexpr (kInc) {
+      if constexpr (kInc && kSwIncPark) {
         pt[p] = WT.ld(vg, s); pw[p] = WW.ld(vg, s); pg[p] = WG.ld(vg, s);
       } else {
         pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s);
+      }
+      if constexpr (kInc && !kSwIncPark) {
+        qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
       pd[p] = WD.ld(vg, s);
       pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb); pf[p] = WA.ld(vg, sb);
@@ -748,7 +757,9 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
       for (int r = 0; r < kRingSw; r++) {
         const int j = j0 + r, p = r % kPF;
         if (j < nlay) {
-          const float t = pt[p], w0 = pw[p], g0 = pg[p], Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
+          float t = pt[p], w0 = pw[p], g0 = kHasG || (kInc && kSwIncPark) ? pg[p] : 0.0f;
+          const float Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
+          if constexpr (kInc && !kSwIncPark) inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);  // pass 2's increment again
           load(p, lay_of_down(min(j + kPF, nlay - 1)));
           // R_dif, T_dif exactly as pass 2 computed them (same inputs, same expressions -> same bits)
           const SwDif d = sw_dif(t, w0, (kHasG || kInc) ? g0 : 0.0f, etab);
@@ -789,7 +800,7 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
   const bool inc = bands != nullptr;
   void *ws = nullptr;
-  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc ? 3 * (size_t)ngpt * nlay * ncol : 0);
+  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc && kSwIncPark ? 3 * (size_t)ngpt * nlay * ncol : 0);
   int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;
   int threads = (ngpt + 63) / 64 * 64;

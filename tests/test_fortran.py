@@ -3,7 +3,8 @@
 
 CPU: the layer and the example host program build; every C symbol it binds is declared in
 include/rrtmgpnn.h; the RBIN reader/writer and ty_gas_concs round-trip data.
-GPU: the example RFMIP host program (blocked, ragged last block) reproduces the oracle bit for bit.
+GPU: the example RFMIP clear-sky and all-sky host programs (blocked, ragged last block) reproduce the
+oracle bit for bit.
 """
 import os
 import re
@@ -99,4 +100,33 @@ def test_fortran_rfmip_driver_matches_oracle(tmp_path, orc, rfmip):
                       ("sw_dir", sr[use], got["sw_flux_dir"][use])):
         err = float(np.sqrt(np.mean((g.astype(np.float64) - ref) ** 2)))
         assert err <= 1e-3, "%s: RMS %.3g W/m2" % (k, err)
+        np.testing.assert_array_equal(g, ref, err_msg=k + ": not bit-identical")
+
+
+@pytest.mark.gpu
+@needs_fc
+def test_fortran_allsky_driver_matches_oracle(tmp_path, orc, rfmip):
+    """The all-sky host program (cloud_optics, clouds%increment, clouds%delta_scale through the Fortran class
+    layer), blocked with a ragged last block, vs the oracle's all-sky pipeline -- bit for bit."""
+    from rrtmgpnn import data, rbin
+    exe = os.path.join(FBUILD, "rrtmgpnn_allsky")
+    if not os.path.exists(exe):
+        _make()
+    prob = subset(rfmip, np.arange(0, 1800, 9))
+    fin, fout = str(tmp_path / "prob.rbin"), str(tmp_path / "flux.rbin")
+    write_problem(prob, fin)
+    r = subprocess.run(["timeout", "-k", "10", "300", exe, fin, fout, data.DATA_DIR, "64"], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = rbin.read(fout)
+    co_lw, co_sw = data.load_cloud_optics("lw"), data.load_cloud_optics("sw")
+    clouds = data.allsky_clouds(prob, co_lw)
+    lu, ld, _ = orc.all_sky_lw(prob, [data.load_model("lw_abs"), data.load_model("lw_pfrac")], data.load_kdist("lw"),
+                               co_lw, clouds)
+    su, sd, sr, _ = orc.all_sky_sw(prob, [data.load_model("sw_abs"), data.load_model("sw_ray")],
+                                   data.load_kdist("sw"), co_sw, clouds)
+    use = prob["usecol"]
+    for k, ref, g in (("lw_up", lu, got["lw_flux_up"]), ("lw_dn", ld, got["lw_flux_dn"]),
+                      ("sw_up", su, got["sw_flux_up"]), ("sw_dn", sd, got["sw_flux_dn"]),
+                      ("sw_dir", sr[use], got["sw_flux_dir"][use])):
         np.testing.assert_array_equal(g, ref, err_msg=k + ": not bit-identical")

@@ -18,9 +18,12 @@ import sys
 STAGES = [
     (re.compile(r"sw_2stream_kernel"), "sw_solver"),
     (re.compile(r"lw_noscat_kernel"), "lw_solver"),
-    (re.compile(r"mlp_pair_kernel<.*,\s*1>"), "predict_nn_lw"),
-    (re.compile(r"mlp_pair_kernel<.*,\s*4>"), "predict_nn_lw"),
-    (re.compile(r"mlp_pair_kernel<.*,\s*2>"), "predict_nn_sw"),
+    # mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS>: MODE 1 LW pair, 4 LW "both", 2 SW pair
+    (re.compile(r"mlp_pair_kernel<(?:\s*\d+\s*,){6}\s*[14]\s*,"), "predict_nn_lw"),
+    (re.compile(r"mlp_pair_kernel<(?:\s*\d+\s*,){6}\s*2\s*,"), "predict_nn_sw"),
+    (re.compile(r"cloud_optics_kernel"), "cloud_optics"),
+    (re.compile(r"increment_bybnd_kernel"), "increment"),
+    (re.compile(r"delta_scale_kernel"), "delta_scale_sw"),
     (re.compile(r"planck_source_kernel"), "planck_source"),
     (re.compile(r"nn_inputs_kernel"), "nn_inputs"),
     (re.compile(r"expand_kernel"), "expand_emis"),

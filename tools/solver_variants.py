@@ -13,9 +13,12 @@ from rrtmgpnn import _lib, data  # noqa: E402
 from rrtmgpnn.pipeline import ClearSkyStep  # noqa: E402
 
 B, config, names = sys.argv[1], sys.argv[2], sys.argv[3:]
-prob = data.rfmip_problem() if config == "c3" else data.synthetic_problem(10000 if config == "c4" else 125000,
-                                                                         60 if config == "c4" else 137)
-steps = {"": ClearSkyStep(prob, device=0, fused=False), "f:": ClearSkyStep(prob, device=0, fused=True)}
+# c4a: the C4 all-sky step (clouds by the all-sky example's recipe)
+prob = data.rfmip_problem() if config == "c3" else data.synthetic_problem(125000 if config == "c5" else 10000,
+                                                                         137 if config == "c5" else 60)
+clouds = data.allsky_clouds(prob, data.load_cloud_optics("lw")) if config == "c4a" else None
+steps = {"": ClearSkyStep(prob, device=0, fused=False, clouds=clouds),
+         "f:": ClearSkyStep(prob, device=0, fused=True, clouds=clouds)}
 for st in steps.values():
     st.step()
 torch.cuda.synchronize()
