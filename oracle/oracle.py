@@ -53,6 +53,8 @@ class Oracle:
                                            c_float, c_float, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_lw_solver_noscat_gaussquad.argtypes = [c_int, c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p,
                                                      _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
+        L.orc_lw_solver_1rescl_gaussquad.argtypes = [c_int] * 5 + [_f32p] * 12
+        L.orc_lw_solver_2stream.argtypes = [c_int] * 4 + [_f32p] * 9
         L.orc_sw_solver_2stream.argtypes = [c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                             _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_expand.argtypes = [c_int, c_int, c_int, _i32p, _f32p, _f32p]
@@ -127,14 +129,30 @@ class Oracle:
                                     sfc, jac, lay, lev)
         return lay, lev, sfc, jac
 
-    def lw_solver(self, tau, lay, lev, emis_gpt, sfc_src, top_at_1=True, nmus=1, inc_flux=None):
+    def lw_solver(self, tau, lay, lev, emis_gpt, sfc_src, top_at_1=True, nmus=1, inc_flux=None, ssa=None, g=None):
+        """lw_solver_noscat_GaussQuad; with ssa/g the rescaled solution (do_rescaling, rte/mo_rte_lw.F90:372-387)."""
         ncol, nlay, ngpt = tau.shape
         Ds, W = gauss(nmus)
         up = np.zeros((ncol, nlay + 1), np.float32)
         dn = np.zeros((ncol, nlay + 1), np.float32)
         inc = f32(inc_flux) if inc_flux is not None else np.zeros((ncol, ngpt), np.float32)
-        self.L.orc_lw_solver_noscat_gaussquad(ngpt, nlay, ncol, int(top_at_1), nmus, f32(Ds), f32(W), inc, f32(tau),
-                                              f32(lay), f32(lev), f32(emis_gpt), f32(sfc_src), up, dn)
+        if ssa is None:
+            self.L.orc_lw_solver_noscat_gaussquad(ngpt, nlay, ncol, int(top_at_1), nmus, f32(Ds), f32(W), inc,
+                                                  f32(tau), f32(lay), f32(lev), f32(emis_gpt), f32(sfc_src), up, dn)
+        else:
+            self.L.orc_lw_solver_1rescl_gaussquad(ngpt, nlay, ncol, int(top_at_1), nmus, f32(Ds), f32(W), inc,
+                                                  f32(tau), f32(ssa), f32(g), f32(lay), f32(lev), f32(emis_gpt),
+                                                  f32(sfc_src), up, dn)
+        return up, dn
+
+    def lw_solver_2stream(self, tau, ssa, g, lev, emis_gpt, sfc_src, top_at_1=True, inc_flux=None):
+        """lw_solver_2stream (rte/kernels/mo_rte_solver_kernels.F90:426-486)."""
+        ncol, nlay, ngpt = tau.shape
+        up = np.zeros((ncol, nlay + 1), np.float32)
+        dn = np.zeros((ncol, nlay + 1), np.float32)
+        inc = f32(inc_flux) if inc_flux is not None else np.zeros((ncol, ngpt), np.float32)
+        self.L.orc_lw_solver_2stream(ngpt, nlay, ncol, int(top_at_1), inc, f32(tau), f32(ssa), f32(g), f32(lev),
+                                     f32(emis_gpt), f32(sfc_src), up, dn)
         return up, dn
 
     def sw_solver(self, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True, inc_flux_dif=None):
@@ -285,6 +303,8 @@ class Reference:
         L.ref_rte_lw.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, c_int, _f32p, _f32p, _f32p, _f32p,
                                  _f32p, _f32p, _f32p, _f32p]
         L.ref_rte_lw.restype = c_int
+        L.ref_rte_lw_2str.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, c_int, c_int] + [_f32p] * 10
+        L.ref_rte_lw_2str.restype = c_int
         L.ref_rte_sw.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, _f32p, _f32p, _f32p, _f32p,
                                  _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.ref_rte_sw.restype = c_int
@@ -306,6 +326,17 @@ class Reference:
             buf = ctypes.create_string_buffer(256)
             self.L.ref_last_error(buf, 256)
             raise RuntimeError("reference failed: %s" % buf.value.decode())
+
+    def rte_lw_2str(self, kd, tau, ssa, g, lay, lev, sfc_src, sfc_jac, sfc_emis_band, top_at_1=True, nmus=1,
+                    use_2stream=False):
+        ncol, nlay, ngpt = tau.shape
+        up = np.zeros((ncol, nlay + 1), np.float32)
+        dn = np.zeros((ncol, nlay + 1), np.float32)
+        self._check(self.L.ref_rte_lw_2str(ncol, nlay, kd["nband"], ngpt,
+                                           np.ascontiguousarray(kd["band_lims_gpt"], np.int32), f32(kd["band_lims_wvn"]),
+                                           int(top_at_1), nmus, int(use_2stream), f32(tau), f32(ssa), f32(g), f32(lay),
+                                           f32(lev), f32(sfc_src), f32(sfc_jac), f32(sfc_emis_band), up, dn))
+        return up, dn
 
     def rte_lw(self, kd, tau, lay, lev, sfc_src, sfc_jac, sfc_emis_band, top_at_1=True, nmus=1):
         ncol, nlay, ngpt = tau.shape

@@ -220,12 +220,26 @@ void orc_planck_source_nn(int ncol, int nlay, int nbnd, int ngpt, int ntemp,
 static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weight,
                           const float *inc, const float *tau, const float *lay, const float *lev,
                           const float *emis, const float *sfc, float *radn_up, float *radn_dn,
-                          float *tau_loc, float *trans, float *src_up, float *src_dn)
+                          float *tau_loc, float *trans, float *src_up, float *src_dn,
+                          const float *ssa, const float *gg, float *An, float *Cn)
 {
   const float tau_thresh = sqrtf(FLT_EPSILON);
   int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   for (int g = 0; g < ngpt; g++)
     radn_dn[g + (size_t)ngpt * top] = inc[g] / (2.0f * PI_F * weight);
+  if (ssa) { /* do_rescaling (:209-233): scattering folded into an effective optical depth (Tang et al.) */
+    for (int l = 0; l < nlay; l++)
+      for (int g = 0; g < ngpt; g++) {
+        size_t i = g + (size_t)ngpt * l;
+        float ssal = ssa[i];
+        float wb = ssal * (1.0f - gg[i]) * 0.5f;
+        float scaleTau = (1.0f - ssal + wb);
+        Cn[i] = 0.4f * wb / scaleTau;
+        tau_loc[i] = tau[i] * D * scaleTau;
+        trans[i] = expf(-tau_loc[i]);
+        An[i] = (1.0f - trans[i] * trans[i]);
+      }
+  } else
   for (int l = 0; l < nlay; l++)
     for (int g = 0; g < ngpt; g++) {
       size_t i = g + (size_t)ngpt * l;
@@ -257,6 +271,36 @@ static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weigh
     size_t i = g + (size_t)ngpt * sfcl;
     radn_up[i] = radn_dn[i] * (1.0f - emis[g]) + emis[g] * sfc[g];
   }
+  if (ssa) { /* lw_transport_1rescl :1729-1795: up with adjustment from radn_dn, then down again from radn_up */
+    if (top_at_1) {
+      for (int l = nlay - 1; l >= 0; l--)
+        for (int g = 0; g < ngpt; g++) {
+          size_t i = g + (size_t)ngpt * l;
+          float adj = Cn[i] * (An[i] * radn_dn[i] - trans[i] * src_dn[i] - src_up[i]);
+          radn_up[i] = trans[i] * radn_up[i + ngpt] + src_up[i] + adj;
+        }
+      for (int l = 0; l < nlay; l++)
+        for (int g = 0; g < ngpt; g++) {
+          size_t i = g + (size_t)ngpt * l;
+          float adj = Cn[i] * (An[i] * radn_up[i] - trans[i] * src_up[i] - src_dn[i]);
+          radn_dn[i + ngpt] = trans[i] * radn_dn[i] + src_dn[i] + adj;
+        }
+    } else {
+      for (int l = 0; l < nlay; l++)
+        for (int g = 0; g < ngpt; g++) {
+          size_t i = g + (size_t)ngpt * l;
+          float adj = Cn[i] * (An[i] * radn_dn[i + ngpt] - trans[i] * src_dn[i] - src_up[i]);
+          radn_up[i + ngpt] = trans[i] * radn_up[i] + src_up[i] + adj;
+        }
+      for (int l = nlay - 1; l >= 0; l--)
+        for (int g = 0; g < ngpt; g++) {
+          size_t i = g + (size_t)ngpt * l;
+          float adj = Cn[i] * (An[i] * radn_up[i] - trans[i] * src_up[i] - src_dn[i]);
+          radn_dn[i] = trans[i] * radn_dn[i + ngpt] + src_dn[i] + adj;
+        }
+    }
+    return;
+  }
   if (top_at_1) {
     for (int l = nlay - 1; l >= 0; l--)
       for (int g = 0; g < ngpt; g++)
@@ -270,20 +314,22 @@ static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weigh
   }
 }
 
-/* lw_solver_noscat_GaussQuad :332-415 (+ lw_solver_noscat per angle); do_rescaling = false,
- * compute_Jac = false (rte/mo_rte_rrtmgp_config.F90:28). Ds/weights have nmus entries. */
-void orc_lw_solver_noscat_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+/* lw_solver_noscat_GaussQuad :332-415 (+ lw_solver_noscat per angle); compute_Jac = false
+ * (rte/mo_rte_rrtmgp_config.F90:28). Ds/weights have nmus entries.  ssa/g NULL: do_rescaling = false;
+ * otherwise the rescaled solution rte_lw uses for 2str optical properties (rte/mo_rte_lw.F90:372-387). */
+void orc_lw_solver_1rescl_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
                                     const float *Ds, const float *weights, const float *inc_flux,
-                                    const float *tau, const float *lay_source, const float *lev_source,
-                                    const float *sfc_emis, const float *sfc_source,
+                                    const float *tau, const float *ssa, const float *g, const float *lay_source,
+                                    const float *lev_source, const float *sfc_emis, const float *sfc_source,
                                     float *flux_up, float *flux_dn)
 {
 #pragma omp parallel
   {
     size_t nl = (size_t)ngpt * nlay, nv = (size_t)ngpt * (nlay + 1);
-    float *buf = (float *)malloc(sizeof(float) * (4 * nl + 4 * nv));
+    float *buf = (float *)malloc(sizeof(float) * (6 * nl + 4 * nv));
     float *tau_loc = buf, *trans = buf + nl, *su = buf + 2 * nl, *sd = buf + 3 * nl;
     float *ru = buf + 4 * nl, *rd = ru + nv, *acc_u = rd + nv, *acc_d = acc_u + nv;
+    float *An = acc_d + nv, *Cn = An + nl;
 #pragma omp for schedule(static)
     for (int icol = 0; icol < ncol; icol++) {
       const float *tc = tau + nl * icol, *lc = lay_source + nl * icol, *vc = lev_source + nv * icol;
@@ -292,7 +338,7 @@ void orc_lw_solver_noscat_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, 
       float *fu = flux_up + (size_t)(nlay + 1) * icol, *fd = flux_dn + (size_t)(nlay + 1) * icol;
       for (int imu = 0; imu < nmus; imu++) {
         lw_noscat_col(ngpt, nlay, top_at_1, Ds[imu], weights[imu], ic, tc, lc, vc, ec, sc, ru, rd,
-                      tau_loc, trans, su, sd);
+                      tau_loc, trans, su, sd, ssa ? ssa + nl * icol : NULL, ssa ? g + nl * icol : NULL, An, Cn);
         float fac = 2.0f * PI_F * weights[imu];
         if (nmus == 1) {
           for (int l = 0; l <= nlay; l++) {
@@ -324,6 +370,132 @@ void orc_lw_solver_noscat_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, 
           for (int g = 0; g < ngpt; g++) { a += acc_u[g + (size_t)ngpt * l]; b += acc_d[g + (size_t)ngpt * l]; }
           fu[l] = a; fd[l] = b;
         }
+    }
+    free(buf);
+  }
+}
+
+void orc_lw_solver_noscat_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                    const float *Ds, const float *weights, const float *inc_flux,
+                                    const float *tau, const float *lay_source, const float *lev_source,
+                                    const float *sfc_emis, const float *sfc_source,
+                                    float *flux_up, float *flux_dn)
+{
+  orc_lw_solver_1rescl_gaussquad(ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, NULL, NULL,
+                                 lay_source, lev_source, sfc_emis, sfc_source, flux_up, flux_dn);
+}
+
+/* adding (rte/kernels/mo_rte_solver_kernels.F90:1526-1637) for one column; flux_dn holds the incident
+ * diffuse flux at the top level on entry.  Shared by the SW and LW two-stream solvers. */
+static void adding_col(int ngpt, int nlay, int top_at_1, const float *albedo_sfc, const float *Rdif,
+                       const float *Tdif, const float *src_dn, const float *src_up, const float *src_sfc,
+                       float *rup, float *rdn, float *albedo, float *src, float *denom)
+{
+  if (top_at_1) {
+    for (int i = 0; i < ngpt; i++) {
+      albedo[i + (size_t)ngpt * nlay] = albedo_sfc[i];
+      src[i + (size_t)ngpt * nlay] = src_sfc[i];
+    }
+    for (int l = nlay - 1; l >= 0; l--)
+      for (int i = 0; i < ngpt; i++) {
+        size_t x = i + (size_t)ngpt * l, xp = x + ngpt;
+        denom[x] = 1.0f / (1.0f - Rdif[x] * albedo[xp]);
+        albedo[x] = Rdif[x] + Tdif[x] * Tdif[x] * albedo[xp] * denom[x];
+        src[x] = src_up[x] + Tdif[x] * denom[x] * (src[xp] + albedo[xp] * src_dn[x]);
+      }
+    for (int i = 0; i < ngpt; i++) rup[i] = rdn[i] * albedo[i] + src[i];
+    for (int l = 1; l <= nlay; l++)
+      for (int i = 0; i < ngpt; i++) {
+        size_t x = i + (size_t)ngpt * l, xm = x - ngpt;
+        rdn[x] = (Tdif[xm] * rdn[xm] + Rdif[xm] * src[x] + src_dn[xm]) * denom[xm];
+        rup[x] = rdn[x] * albedo[x] + src[x];
+      }
+  } else {
+    for (int i = 0; i < ngpt; i++) { albedo[i] = albedo_sfc[i]; src[i] = src_sfc[i]; }
+    for (int l = 0; l < nlay; l++)
+      for (int i = 0; i < ngpt; i++) {
+        size_t x = i + (size_t)ngpt * l, xp = x + ngpt;
+        denom[x] = 1.0f / (1.0f - Rdif[x] * albedo[x]);
+        albedo[xp] = Rdif[x] + Tdif[x] * Tdif[x] * albedo[x] * denom[x];
+        src[xp] = src_up[x] + Tdif[x] * denom[x] * (src[x] + albedo[x] * src_dn[x]);
+      }
+    for (int i = 0; i < ngpt; i++) {
+      size_t x = i + (size_t)ngpt * nlay;
+      rup[x] = rdn[x] * albedo[x] + src[x];
+    }
+    for (int l = nlay - 1; l >= 0; l--)
+      for (int i = 0; i < ngpt; i++) {
+        size_t x = i + (size_t)ngpt * l, xp = x + ngpt;
+        rdn[x] = (Tdif[x] * rdn[xp] + Rdif[x] * src[x] + src_dn[x]) * denom[x];
+        rup[x] = rdn[x] * albedo[x] + src[x];
+      }
+  }
+}
+
+/* ---------------------------------------------------------------------------------------------
+ * LW two-stream: lw_solver_2stream (rte/kernels/mo_rte_solver_kernels.F90:426-486) with lw_two_stream
+ * (:1018-1069, Fu et al. 1997 coefficients, LW_diff_sec = 1.66), lw_source_2str (:1112-1162, Toon et al.
+ * linear-in-tau sources), adding (:1526-1637) and sum_broadband_nocol (plain sequential sums).
+ * ------------------------------------------------------------------------------------------- */
+void orc_lw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux, const float *tau,
+                           const float *ssa, const float *gg, const float *lev_source, const float *sfc_emis,
+                           const float *sfc_source, float *flux_up, float *flux_dn)
+{
+  const float k_min = 1.e-4f, LW_diff_sec = 1.66f;
+#pragma omp parallel
+  {
+    size_t nl = (size_t)ngpt * nlay, nv = (size_t)ngpt * (nlay + 1);
+    float *buf = (float *)malloc(sizeof(float) * (7 * nl + 4 * nv + 2 * ngpt));
+    float *Rdif = buf, *Tdif = buf + nl, *src_up = buf + 2 * nl, *src_dn = buf + 3 * nl, *denom = buf + 4 * nl;
+    float *gamma1 = buf + 5 * nl, *gamma2 = buf + 6 * nl;
+    float *rup = buf + 7 * nl, *rdn = rup + nv, *albedo = rdn + nv, *src = albedo + nv;
+    float *src_sfc = src + nv, *alb_sfc = src_sfc + ngpt;
+#pragma omp for schedule(static)
+    for (int icol = 0; icol < ncol; icol++) {
+      const float *t = tau + nl * icol, *w0 = ssa + nl * icol, *g = gg + nl * icol, *lev = lev_source + nv * icol;
+      const float *em = sfc_emis + (size_t)ngpt * icol, *ss = sfc_source + (size_t)ngpt * icol;
+      int top = top_at_1 ? 0 : nlay;
+      for (int i = 0; i < ngpt; i++) rdn[i + (size_t)ngpt * top] = inc_flux[i + (size_t)ngpt * icol];
+      for (int j = 0; j < nlay; j++)
+        for (int i = 0; i < ngpt; i++) {
+          size_t x = i + (size_t)ngpt * j;
+          gamma1[x] = LW_diff_sec * (1.0f - 0.5f * w0[x] * (1.0f + g[x]));
+          gamma2[x] = LW_diff_sec * 0.5f * w0[x] * (1.0f - g[x]);
+          float k = sqrtf(fmaxf((gamma1[x] - gamma2[x]) * (gamma1[x] + gamma2[x]), k_min));
+          float emk = expf(-t[x] * k);
+          float em2k = emk * emk;
+          float RT = 1.0f / (k * (1.0f + em2k) + gamma1[x] * (1.0f - em2k));
+          Rdif[x] = RT * gamma2[x] * (1.0f - em2k);
+          Tdif[x] = RT * 2.0f * k * emk;
+        }
+      for (int j = 0; j < nlay; j++) {
+        const float *ltop = lev + (size_t)ngpt * (top_at_1 ? j : j + 1);
+        const float *lbot = lev + (size_t)ngpt * (top_at_1 ? j + 1 : j);
+        for (int i = 0; i < ngpt; i++) {
+          size_t x = i + (size_t)ngpt * j;
+          if (t[x] > 1.0e-8f) {
+            float Z = (lbot[i] - ltop[i]) / (t[x] * (gamma1[x] + gamma2[x]));
+            float Zup_top = Z + ltop[i], Zup_bottom = Z + lbot[i];
+            float Zdn_top = -Z + ltop[i], Zdn_bottom = -Z + lbot[i];
+            src_up[x] = PI_F * (Zup_top - Rdif[x] * Zdn_top - Tdif[x] * Zup_bottom);
+            src_dn[x] = PI_F * (Zdn_bottom - Rdif[x] * Zup_bottom - Tdif[x] * Zdn_top);
+          } else {
+            src_up[x] = 0.0f;
+            src_dn[x] = 0.0f;
+          }
+        }
+      }
+      for (int i = 0; i < ngpt; i++) {
+        src_sfc[i] = PI_F * em[i] * ss[i];
+        alb_sfc[i] = 1.0f - em[i];
+      }
+      adding_col(ngpt, nlay, top_at_1, alb_sfc, Rdif, Tdif, src_dn, src_up, src_sfc, rup, rdn, albedo, src, denom);
+      float *fu = flux_up + (size_t)(nlay + 1) * icol, *fd = flux_dn + (size_t)(nlay + 1) * icol;
+      for (int l = 0; l <= nlay; l++) {
+        float a = 0, b = 0;
+        for (int i = 0; i < ngpt; i++) { a += rup[i + (size_t)ngpt * l]; b += rdn[i + (size_t)ngpt * l]; }
+        fu[l] = a; fd[l] = b;
+      }
     }
     free(buf);
   }
