@@ -145,6 +145,22 @@ int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nl
                                          int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
                                          float totplnk_delta, const float *totplnk, const float *sfc_emis_gpt,
                                          float *flux_up, float *flux_dn);
+/* rte_lw on two-stream optical properties, default branch (rte/mo_rte_lw.F90:372-387): lw_solver_noscat_GaussQuad
+ * with do_rescaling -- tau scaled by (1 - ssa + ssa(1-g)/2), a no-scattering pass down, then
+ * lw_transport_1rescl up and down again with the adjustment terms (rte/kernels/mo_rte_solver_kernels.F90:209-233,
+ * 1729-1795).  Arguments as rrtmgpnn_lw_solver_noscat plus ssa, g (ngpt, nlay, ncol). */
+int rrtmgpnn_lw_solver_1rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                              const float *Ds, const float *weights, const float *inc_flux, const float *tau,
+                              const float *ssa, const float *g, const float *lay_source, const float *lev_source,
+                              const float *sfc_emis_gpt, const float *sfc_source, float *flux_up, float *flux_dn);
+/* rte_lw(..., use_2stream=.true.): lw_solver_2stream (rte/kernels/mo_rte_solver_kernels.F90:426-486) with
+ * lw_two_stream (:1018-1069), lw_source_2str (:1112-1162) and adding (:1526-1637).  inc_flux (ngpt, ncol) is a flux
+ * (NULL: zero); the layer sources are not used (as in the reference).  Broadband sums are sequential over g
+ * (sum_broadband_nocol). */
+int rrtmgpnn_lw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                               const float *inc_flux, const float *tau, const float *ssa, const float *g,
+                               const float *lev_source, const float *sfc_emis_gpt, const float *sfc_source,
+                               float *flux_up, float *flux_dn);
 /* sw_solver_2stream (:541-692).  inc_flux_dif may be NULL (zero, rte/mo_rte_sw.F90:197-210).
  * g may be NULL: asymmetry parameter identically zero, as gas_optics_ext's NN branch produces
  * (mo_gas_optics_rrtmgp.F90:560-567) -- same fluxes as passing a zero-filled array. */

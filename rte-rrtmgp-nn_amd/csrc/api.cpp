@@ -529,6 +529,32 @@ int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nl
                                  sfc_emis_gpt, tau_bnd, flux_up, flux_dn);
 }
 
+int rrtmgpnn_lw_solver_1rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                              const float *Ds, const float *weights, const float *inc_flux, const float *tau,
+                              const float *ssa, const float *g, const float *lay_source, const float *lev_source,
+                              const float *sfc_emis_gpt, const float *sfc_source, float *flux_up, float *flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!Ds || !weights || !tau || !ssa || !g || !lay_source || !lev_source || !sfc_emis_gpt || !sfc_source ||
+      !flux_up || !flux_dn || ngpt < 1 || nlay < 1 || ncol < 0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw_solver_1rescl: bad argument");
+  return launch_lw_rescl(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, ssa, g, lay_source,
+                         lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn);
+}
+
+int rrtmgpnn_lw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                               const float *inc_flux, const float *tau, const float *ssa, const float *g,
+                               const float *lev_source, const float *sfc_emis_gpt, const float *sfc_source,
+                               float *flux_up, float *flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!tau || !ssa || !g || !lev_source || !sfc_emis_gpt || !sfc_source || !flux_up || !flux_dn || ngpt < 1 ||
+      nlay < 1 || ncol < 0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw_solver_2stream: bad argument");
+  return launch_lw_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, ssa, g, lev_source, sfc_emis_gpt,
+                           sfc_source, flux_up, flux_dn);
+}
+
 int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
                                const float *inc_flux, const float *inc_flux_dif, const float *tau, const float *ssa,
                                const float *g, const float *mu0, const float *sfc_alb_dir_gpt,

@@ -134,6 +134,14 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
                       const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                       const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, float *flux_up,
                       float *flux_dn, float *flux_dir);
+// kernels_lw_scat.hip
+int launch_lw_rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
+                    const float *wts, const float *inc_flux, const float *tau, const float *ssa, const float *g,
+                    const float *lay_source, const float *lev_source, const float *sfc_emis, const float *sfc_source,
+                    float *flux_up, float *flux_dn);
+int launch_lw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                      const float *tau, const float *ssa, const float *g, const float *lev_source,
+                      const float *sfc_emis, const float *sfc_source, float *flux_up, float *flux_dn);
 int launch_expand(rrtmgpnn_context *ctx, int nband, int ngpt, int ncol, const BandArgs &bands, const float *in,
                   float *out);
 }  // namespace rrtmgpnn

@@ -8,16 +8,13 @@
 //  * planck_source_kernel : compute_Planck_source_nn (rrtmgp/kernels/mo_gas_optics_kernels.F90:615-683)
 //  * lw_noscat_kernel     : lw_solver_noscat[_GaussQuad] (rte/kernels/mo_rte_solver_kernels.F90:119-415)
 //  * sw_2stream kernels   : sw_solver_2stream + sw_two_stream_source + adding (:541-692, :1366-1637)
-#include "internal.hpp"
-#include "libm_ref.hpp"
+#include "rte_device.hpp"
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
 
 namespace rrtmgpnn {
-
-static constexpr float kPi = 3.14159265358979323846f;
 
 // Ablation switches for tools/ablate_solvers.sh (never set in the product build): they break parity
 // on purpose to attribute solver time.  RRTMGPNN_ABL_NATIVE_EXP: device expf instead of ref_expf;
@@ -47,13 +44,6 @@ __device__ __forceinline__ float interp1d(float val, float offset, float delta, 
   int index = min(ntemp - 1, max(1, iv + 1));
   float lo = t[index - 1], hi = t[index];
   return lo + frac * (hi - lo);
-}
-
-__device__ __forceinline__ int band_of(const BandArgs &b, int g)
-{
-  for (int i = 0; i < b.nbnd; i++)
-    if (g >= b.lims[2 * i] - 1 && g < b.lims[2 * i + 1]) return i;
-  return 0;
 }
 
 constexpr int kPlanckLayers = 4;  // layers per block: independent loads in flight per lane
@@ -110,13 +100,7 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 }
 
 // ------------------------------------------------------------------------------------------
-// Ordered broadband reduction.  The reference sums g-points into 4 interleaved partial sums,
-// partial j accumulating g = j, j+4, j+8, ... in increasing g, then ((p0+p1)+p2)+p3
-// (rte/kernels/mo_rte_solver_kernels.F90:296-318 LW, :643-686 SW).  A float32 tree reduction
-// differs from that by several ulp of the broadband flux (~1e-3 W/m2 at SW magnitudes), so the
-// kernels reproduce the reference's order exactly: each level's per-g values are staged in an
-// LDS ring of kRing levels; when it fills, 4*kRing*NQ threads each walk one (quantity, level,
-// partial) sequentially.  Deterministic and order-identical to the reference.
+// Solver tuning (the ordered broadband reduction and buffer addressing live in rte_device.hpp).
 // ------------------------------------------------------------------------------------------
 // Tuning knobs (overridable with -D for tools/solver_variants.sh):
 //   kRing : levels staged in LDS per ordered flush;
@@ -163,78 +147,6 @@ static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
 static constexpr bool kSwIncPark = RRTMGPNN_SW_INC_PARK != 0;
 static constexpr int kLwMaxG = RRTMGPNN_LW_WAVES > 0 ? 256 : 1024;  // g-points per column block
 static constexpr int kSwMaxG = RRTMGPNN_SW_WAVES > 0 ? 256 : 1024;
-static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS
-
-// Flush `n` staged levels.  ring: [nq][R][ngpt], slot c holds level lev0 + c*dl; part: [nq][nlev][4].
-// One thread per (quantity, level) walks the level's g-points with 16-byte LDS reads: element k of
-// the float4 at m is g = 4m + k, so the 4 interleaved partials advance together, each in g order.
-// dn_mode (SW): quantity 1 is accumulated as (s + ring1) + ring2, i.e. sums_dn + radn_dn + radn_dir.
-// ngpt % 4 != 0: the reference uses sum(radn, 1) instead (one sequential sum, kept in partial 0).
-template <int R>
-__device__ __forceinline__ void ring_flush(const float *ring, float *part, int nq, int n, int lev0, int dl, int ngpt,
-                                           int nlev, bool dn_mode)
-{
-  __syncthreads();
-  const int t = threadIdx.x;
-#ifdef RRTMGPNN_ABL_NO_REDUCE
-  if (false) {
-#else
-  if (t < nq * n) {
-#endif
-    const int q = t / n, c = t - q * n;
-    const float *r = ring + ((size_t)q * R + c) * ngpt;
-    const float *r2 = ring + ((size_t)2 * R + c) * ngpt;
-    const bool dn = dn_mode && q == 1;
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
-    if ((ngpt & 3) == 0) {
-      const float4 *r4 = (const float4 *)r, *q4 = (const float4 *)r2;
-      const int n4 = ngpt >> 2;
-      if (dn) {
-#pragma unroll 4
-        for (int m = 0; m < n4; m++) {
-          const float4 a = r4[m], b = q4[m];
-          s0 = (s0 + a.x) + b.x; s1 = (s1 + a.y) + b.y; s2 = (s2 + a.z) + b.z; s3 = (s3 + a.w) + b.w;
-        }
-      } else {
-#pragma unroll 4
-        for (int m = 0; m < n4; m++) {
-          const float4 a = r4[m];
-          s0 = s0 + a.x; s1 = s1 + a.y; s2 = s2 + a.z; s3 = s3 + a.w;
-        }
-      }
-    } else {
-      if (dn) for (int i = 0; i < ngpt; i++) s0 = s0 + (r[i] + r2[i]);  // radn_dn = radn_dn + radn_dir; sum
-      else    for (int i = 0; i < ngpt; i++) s0 = s0 + r[i];
-    }
-    float4 *p = (float4 *)(part + ((size_t)q * nlev + lev0 + c * dl) * 4);
-    *p = make_float4(s0, s1, s2, s3);
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]) + p[2]) + p[3]; }
-
-// ------------------------------------------------------------------------------------------
-// Column-local addressing.  Every solver array is (ngpt, n, ncol) with the column block uniform per
-// workgroup, so each array gets a per-column buffer descriptor built from wave-uniform values: a
-// load is `buffer_load v, voff=g*4, s_rsrc, soff=layer*ngpt*4` -- no per-lane 64-bit address math,
-// the layer offset lives in an SGPR.
-// ------------------------------------------------------------------------------------------
-struct ColArr {
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ ColArr() = default;
-  __device__ __forceinline__ ColArr(const float *base, size_t col_off, uint32_t bytes)
-      : r(__builtin_amdgcn_make_buffer_rsrc((void *)(base + col_off), 0, (int)bytes, 0x00020000)) {}
-  __device__ __forceinline__ float ld(uint32_t voff, uint32_t soff) const
-  {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-  }
-  __device__ __forceinline__ void st(float v, uint32_t voff, uint32_t soff) const
-  {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
-  }
-};
-
 // ------------------------------------------------------------------------------------------
 // LW no-scattering solver.  block = one column, lane = g-point.  The down pass stores nothing: the
 // up pass re-reads its layer's inputs (L2/MALL-hot) and recomputes trans and the source, bitwise
@@ -252,10 +164,7 @@ struct ColArr {
 // column into LDS.  Same products, same bits; the source arrays never touch HBM.
 // LDS: etab | [fused: B [nbnd][2*nlay+1], Bsfc[nbnd]] | ring [kRing][ngpt] | part [2][nlev][4]
 // ------------------------------------------------------------------------------------------
-struct LwAngles {
-  float D[4], w[4];
-  int nmus;
-};
+
 
 struct LwPlanck {
   const float *tlay, *tlev, *tsfc, *totplnk;

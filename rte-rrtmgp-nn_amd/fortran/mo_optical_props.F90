@@ -55,6 +55,7 @@ module mo_optical_props
     generic,   public  :: alloc_2str => alloc_only_2str, init_and_alloc_2str, copy_and_alloc_2str
     procedure, public  :: finalize => finalize_2str
     procedure, public  :: delta_scale => delta_scale_2str
+    procedure, public  :: validate => validate_2stream
   end type ty_optical_props_2str
 
 contains
@@ -339,6 +340,21 @@ contains
     call dev_free(t1); call dev_free(s1); call dev_free(g1)
     call dev_free(t2); call dev_free(s2); call dev_free(g2)
   end function increment
+
+  ! validate_2stream (:635-671)
+  function validate_2stream(this) result(err_message)
+    class(ty_optical_props_2str), intent(in) :: this
+    character(len=128) :: err_message
+    err_message = ''
+    if (.not. all([allocated(this%tau), allocated(this%ssa), allocated(this%g)])) then
+      err_message = "validate: arrays not allocated/initialized"; return
+    end if
+    if (any(shape(this%ssa) /= shape(this%tau)) .or. any(shape(this%g) /= shape(this%tau))) &
+      err_message = "validate: arrays not sized consistently"
+    if (any(this%tau < 0._wp)) err_message = "validate: tau values out of range"
+    if (any(this%ssa < 0._wp .or. this%ssa > 1.0001_wp)) err_message = "validate: ssa values out of range"
+    if (any(this%g < -1._wp .or. this%g > 1._wp)) err_message = "validate: g values out of range"
+  end function validate_2stream
 
   ! delta_scale_1scl (:565-574): absorption optical depth needs no scaling
   function delta_scale_1scl(this, for) result(err_message)

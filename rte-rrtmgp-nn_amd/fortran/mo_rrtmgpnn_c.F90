@@ -16,7 +16,8 @@ module mo_rrtmgpnn_c
   public :: c_rrtmgpnn_cloud_optics_create_lut, c_rrtmgpnn_cloud_optics_create_pade, &
             c_rrtmgpnn_cloud_optics_set_ice_roughness, c_rrtmgpnn_cloud_optics_load, c_rrtmgpnn_cloud_optics_get, &
             c_rrtmgpnn_cloud_optics_destroy, c_rrtmgpnn_cloud_optics_compute, c_rrtmgpnn_increment_bybnd, &
-            c_rrtmgpnn_increment, c_rrtmgpnn_delta_scale_2str
+            c_rrtmgpnn_increment, c_rrtmgpnn_delta_scale_2str, c_rrtmgpnn_lw_solver_1rescl, &
+            c_rrtmgpnn_lw_solver_2stream
 
   type(c_ptr), save :: ctx_ = c_null_ptr
   !$omp threadprivate(ctx_)
@@ -114,6 +115,21 @@ module mo_rrtmgpnn_c
       type(c_ptr), value :: ctx, inc_flux, tau, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn
       integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus
       real(c_float), dimension(*), intent(in) :: Ds, weights
+    end function
+    integer(c_int) function c_rrtmgpnn_lw_solver_1rescl(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, &
+        inc_flux, tau, ssa, g, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn) &
+        bind(C, name="rrtmgpnn_lw_solver_1rescl")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx, inc_flux, tau, ssa, g, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, &
+                            flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus
+      real(c_float), dimension(*), intent(in) :: Ds, weights
+    end function
+    integer(c_int) function c_rrtmgpnn_lw_solver_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, ssa, g, &
+        lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn) bind(C, name="rrtmgpnn_lw_solver_2stream")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, inc_flux, tau, ssa, g, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1
     end function
     integer(c_int) function c_rrtmgpnn_sw_solver_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, &
         tau, ssa, g, mu0, sfc_alb_dir_gpt, sfc_alb_dif_gpt, flux_up, flux_dn, flux_dir) &

@@ -1,13 +1,13 @@
 ! mo_rte_lw -- drop-in for rte/mo_rte_lw.F90 (rte_lw, :60-424) in the fork's configuration
-! (no-scattering solver, compute_Jac = .false., rte/mo_rte_rrtmgp_config.F90:28).
-! Inputs are staged to the device, expand(sfc_emis) and lw_solver_noscat_GaussQuad run as HIP kernels
-! with the broadband reduction fused into the solver, and the broadband fluxes come back into the
-! caller's flux_up / flux_dn / flux_net.  g-point fluxes, the two-stream / rescaled paths, lw_Ds and the
-! Jacobians return an error string, as the reference does for unsupported combinations.
+! (compute_Jac = .false., rte/mo_rte_rrtmgp_config.F90:28).
+! Inputs are staged to the device, expand(sfc_emis) and the solver run as HIP kernels with the broadband
+! reduction fused in, and the broadband fluxes come back into the caller's flux_up / flux_dn / flux_net.
+! 1scl: lw_solver_noscat_GaussQuad; 2str: the rescaled solution (default) or lw_solver_2stream
+! (use_2stream).  g-point fluxes, lw_Ds and the Jacobians return an error string.
 module mo_rte_lw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,         only: wp
-  use mo_optical_props,    only: ty_optical_props_arry, ty_optical_props_1scl
+  use mo_optical_props,    only: ty_optical_props_arry, ty_optical_props_1scl, ty_optical_props_2str
   use mo_source_functions, only: ty_source_func_lw
   use mo_fluxes,           only: ty_fluxes_flexible
   use mo_rte_rrtmgp_config, only: check_values
@@ -45,7 +45,8 @@ contains
     character(len=128) :: error_msg
     integer :: ncol, nlay, ngpt, nband, nmus
     integer(c_int), allocatable :: lims(:,:)
-    type(c_ptr) :: d_tau, d_lay, d_lev, d_sfc, d_emis, d_emis_gpt, d_inc, d_up, d_dn
+    type(c_ptr) :: d_tau, d_ssa, d_g, d_lay, d_lev, d_sfc, d_emis, d_emis_gpt, d_inc, d_up, d_dn
+    logical :: two_str, use_2s
     real(wp), allocatable :: up(:,:), dn(:,:)
     character(len=128) :: e
 
@@ -93,15 +94,27 @@ contains
     if (present(flux_up_Jac) .or. present(flux_dn_Jac)) then
       error_msg = "rte_lw: compute_Jac is .false. in this configuration (mo_rte_rrtmgp_config.F90:28)"; return
     end if
+    use_2s = .false.
+    if (present(use_2stream)) use_2s = use_2stream
+    two_str = .false.
+    d_ssa = c_null_ptr
+    d_g = c_null_ptr
     select type (optical_props)
     type is (ty_optical_props_1scl)
-      if (present(use_2stream)) then
-        if (use_2stream) then
-          error_msg = "rte_lw: can't use two-stream methods with only absorption optical depth"; return
-        end if
+      if (use_2s) then
+        error_msg = "rte_lw: can't use two-stream methods with only absorption optical depth"; return
       end if
+    type is (ty_optical_props_2str)
+      if (use_2s .and. nmus /= 1) then
+        error_msg = "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"; return
+      end if
+      if (use_2s .or. check_values) error_msg = optical_props%validate()  ! unconditional for 2-stream (:360)
+      if (error_msg /= '') return
+      two_str = .true.
+      d_ssa = dev_upload(optical_props%ssa, ngpt * nlay * ncol)
+      d_g   = dev_upload(optical_props%g, ngpt * nlay * ncol)
     class default
-      error_msg = "rte_lw: two-stream / rescaled longwave solvers are not implemented (1scl only)"; return
+      error_msg = "lw_solver(...ty_optical_props_nstr...) not yet implemented"; return
     end select
 
     lims = optical_props%get_band_lims_gpoint()
@@ -115,14 +128,26 @@ contains
     if (present(inc_flux)) d_inc = dev_upload(inc_flux, ngpt * ncol)
     d_up = dev_alloc((nlay + 1) * ncol)
     d_dn = dev_alloc((nlay + 1) * ncol)
-    ! sfc_emis expanded to g-points (:429-447), then lw_solver_noscat_GaussQuad (:332-415)
+    ! sfc_emis expanded to g-points (:429-447), then the solver (:326-387)
     error_msg = rrtmgpnn_check(c_rrtmgpnn_expand_band_to_gpt(rrtmgpnn_ctx(), nband, ngpt, ncol, lims, d_emis, &
                                                              d_emis_gpt), "rte_lw: expand")
-    if (error_msg == '') &
-      error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                                 merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
-                                 gauss_wts(1:nmus, nmus), d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, d_up, d_dn), &
-                                 "rte_lw: lw_solver_noscat")
+    if (error_msg == '') then
+      if (two_str .and. use_2s) then
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                   merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_ssa, d_g, d_lev, d_emis_gpt, &
+                                   d_sfc, d_up, d_dn), "rte_lw: lw_solver_2stream")
+      else if (two_str) then
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_1rescl(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                   merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
+                                   gauss_wts(1:nmus, nmus), d_inc, d_tau, d_ssa, d_g, d_lay, d_lev, d_emis_gpt, &
+                                   d_sfc, d_up, d_dn), "rte_lw: lw_solver_noscat (rescaled)")
+      else
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                   merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
+                                   gauss_wts(1:nmus, nmus), d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, d_up, &
+                                   d_dn), "rte_lw: lw_solver_noscat")
+      end if
+    end if
     e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "rte_lw")
     if (error_msg == '') error_msg = e
     if (error_msg == '') then
@@ -133,6 +158,7 @@ contains
       if (associated(fluxes%flux_dn)) fluxes%flux_dn = dn
       if (associated(fluxes%flux_net)) fluxes%flux_net = dn - up
     end if
+    call dev_free(d_ssa); call dev_free(d_g)
     call dev_free(d_tau); call dev_free(d_lay); call dev_free(d_lev); call dev_free(d_sfc)
     call dev_free(d_emis); call dev_free(d_emis_gpt); call dev_free(d_inc); call dev_free(d_up); call dev_free(d_dn)
   end function rte_lw

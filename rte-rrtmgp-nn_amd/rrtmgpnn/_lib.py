@@ -53,6 +53,9 @@ SIGNATURES = {
     "rrtmgpnn_sw_solver_2stream_inc": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                c_int, P(c_int), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                c_vp]),
+    "rrtmgpnn_lw_solver_1rescl": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float), P(c_float)]
+                                  + [c_vp] * 10),
+    "rrtmgpnn_lw_solver_2stream": (c_int, [c_vp, c_int, c_int, c_int, c_int] + [c_vp] * 9),
     "rrtmgpnn_sw_solver_2stream": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_expand_band_to_gpt": (c_int, [c_vp, c_int, c_int, c_int, P(c_int), c_vp, c_vp]),

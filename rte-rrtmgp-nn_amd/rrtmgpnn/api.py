@@ -292,6 +292,19 @@ class OpticalProps2str(_OpticalPropsArry):
         self.g = torch.zeros(shape, dtype=torch.float32, device=dev)
         return ""
 
+    def validate(self):
+        """validate_2stream (rte/mo_optical_props.F90:635-671)."""
+        if self.tau.shape != self.ssa.shape or self.tau.shape != self.g.shape:
+            return "validate: arrays not sized consistently"
+        e = ""
+        if bool((self.tau < 0).any()):
+            e = "validate: tau values out of range"
+        if bool(((self.ssa < 0) | (self.ssa > 1.0001)).any()):
+            e = "validate: ssa values out of range"
+        if bool(((self.g < -1) | (self.g > 1)).any()):
+            e = "validate: g values out of range"
+        return e
+
     def delta_scale(self, for_=None):
         """delta_scale_2str (rte/mo_optical_props.F90:576-604); forward fraction g**2 unless `for_` is given."""
         ctx = context(self.tau.device.index)
@@ -657,10 +670,15 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
         return "rte_lw: asking for too many quadrature points for no-scattering calculation"
     if nmu < 1:
         return "rte_lw: have to ask for at least one quadrature point for no-scattering calculation"
-    if not isinstance(optical_props, OpticalProps1scl):
-        return "rte_lw: two-stream / rescaled longwave solvers are not implemented (1scl only)"
-    if use_2stream:
+    is2 = isinstance(optical_props, OpticalProps2str)
+    if not is2 and not isinstance(optical_props, OpticalProps1scl):
+        return "lw_solver(...ty_optical_props_nstr...) not yet implemented"
+    if not is2 and use_2stream:
         return "rte_lw: can't use two-stream methods with only absorption optical depth"
+    if is2 and lw_Ds is not None:
+        return "rte_lw: lw_Ds not valid input for _2str class"
+    if is2 and use_2stream and n_gauss_angles is not None and nmu != 1:
+        return "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"
     if lw_Ds is not None:
         return "rte_lw: lw_Ds (column-dependent diffusivity) is not implemented"
     if flux_up_Jac is not None or flux_dn_Jac is not None:
@@ -679,10 +697,29 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
                                         _p(emis), _p(emis_gpt)), "expand")
     up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=emis.device)
     dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=emis.device)
-    check(L.rrtmgpnn_lw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu, float_array(GAUSS_DS[nmu]),
-                                      float_array(GAUSS_WTS[nmu]), _p(inc_flux), _p(optical_props.tau),
-                                      _p(sources.lay_source), _p(sources.lev_source), _p(emis_gpt),
-                                      _p(sources.sfc_source), _p(up), _p(dn)), "lw_solver_noscat")
+    op = optical_props
+    if is2 and use_2stream:  # lw_solver_2stream (rte/mo_rte_lw.F90:357-371); validate() runs unconditionally
+        e = op.validate()
+        if e:
+            return e
+        check(L.rrtmgpnn_lw_solver_2stream(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux), _p(op.tau),
+                                           _p(op.ssa), _p(op.g), _p(sources.lev_source), _p(emis_gpt),
+                                           _p(sources.sfc_source), _p(up), _p(dn)), "lw_solver_2stream")
+    elif is2:  # rescaled no-scattering solution (:372-387)
+        if check_values:
+            e = op.validate()
+            if e:
+                return e
+        check(L.rrtmgpnn_lw_solver_1rescl(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu,
+                                          float_array(GAUSS_DS[nmu]), float_array(GAUSS_WTS[nmu]), _p(inc_flux),
+                                          _p(op.tau), _p(op.ssa), _p(op.g), _p(sources.lay_source),
+                                          _p(sources.lev_source), _p(emis_gpt), _p(sources.sfc_source), _p(up),
+                                          _p(dn)), "lw_solver_1rescl")
+    else:
+        check(L.rrtmgpnn_lw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu,
+                                          float_array(GAUSS_DS[nmu]), float_array(GAUSS_WTS[nmu]), _p(inc_flux),
+                                          _p(op.tau), _p(sources.lay_source), _p(sources.lev_source),
+                                          _p(emis_gpt), _p(sources.sfc_source), _p(up), _p(dn)), "lw_solver_noscat")
     if fluxes.flux_net is not None:
         torch.sub(dn, up, out=fluxes.flux_net)
     return ""

@@ -1,0 +1,97 @@
+"""GPU: the LW scattering solvers through rte_lw on two-stream optical properties,
+bit for bit against the oracle (which tests/test_lw_scattering_oracle.py pins to the reference's Fortran):
+the rescaled no-scattering solution (default) for 1-4 angles and lw_solver_2stream (use_2stream=True), in both
+vertical orientations; plus rte_lw's argument checks for these branches."""
+import numpy as np
+import pytest
+
+from test_lw_scattering_oracle import _flip, lw_2str_problem
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    torch.cuda.set_device(0)
+    return torch.device("cuda", 0)
+
+
+def T(a, dev):
+    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
+
+
+def _gpu_lw(p, dev, top_at_1, nmus=None, use_2stream=False, inc=None):
+    from rrtmgpnn import api
+    kd = p["kd"]
+    ncol, nlay, _ = p["tau"].shape
+    op = api.OpticalProps2str()
+    assert op.init(kd["band_lims_wvn"], kd["band_lims_gpt"]) == ""
+    assert op.alloc_2str(ncol, nlay, device=dev) == ""
+    op.tau.copy_(T(p["tau"], dev)), op.ssa.copy_(T(p["ssa"], dev)), op.g.copy_(T(p["g"], dev))
+    src = api.SourceFuncLW()
+    assert src.alloc(ncol, nlay, op, device=dev) == ""
+    src.lay_source.copy_(T(p["lay"], dev)), src.lev_source.copy_(T(p["lev"], dev))
+    src.sfc_source.copy_(T(p["sfc"], dev))
+    f = lambda: torch.empty((ncol, nlay + 1), device=dev)  # noqa: E731
+    fl = api.FluxesBroadband(f(), f())
+    e = api.rte_lw(op, top_at_1, src, T(p["emis_band"], dev), fl, inc_flux=None if inc is None else T(inc, dev),
+                   n_gauss_angles=nmus, use_2stream=use_2stream)
+    assert e == "", e
+    torch.cuda.synchronize()
+    return fl.flux_up.cpu().numpy(), fl.flux_dn.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def prob(orc, rfmip):
+    return lw_2str_problem(orc, rfmip, ncol=64)
+
+
+@pytest.mark.parametrize("top_at_1", [True, False])
+@pytest.mark.parametrize("nmus", [1, 2, 3, 4])
+def test_lw_rescaled_bitwise_vs_oracle(dev, orc, prob, top_at_1, nmus):
+    p = prob if top_at_1 else _flip(prob)
+    got = _gpu_lw(p, dev, top_at_1, nmus)
+    want = orc.lw_solver(p["tau"], p["lay"], p["lev"], p["emis_gpt"], p["sfc"], top_at_1, nmus, ssa=p["ssa"], g=p["g"])
+    for x, y, k in zip(got, want, ("up", "dn")):
+        np.testing.assert_array_equal(x, y, err_msg=k)
+
+
+@pytest.mark.parametrize("top_at_1", [True, False])
+@pytest.mark.parametrize("with_inc", [False, True])
+def test_lw_2stream_bitwise_vs_oracle(dev, orc, prob, top_at_1, with_inc):
+    p = prob if top_at_1 else _flip(prob)
+    inc = np.random.default_rng(4).uniform(0, 2, p["emis_gpt"].shape).astype(np.float32) if with_inc else None
+    got = _gpu_lw(p, dev, top_at_1, use_2stream=True, inc=inc)
+    want = orc.lw_solver_2stream(p["tau"], p["ssa"], p["g"], p["lev"], p["emis_gpt"], p["sfc"], top_at_1, inc)
+    for x, y, k in zip(got, want, ("up", "dn")):
+        np.testing.assert_array_equal(x, y, err_msg=k)
+
+
+def test_lw_scattering_argument_checks(dev, prob):
+    from rrtmgpnn import api
+    kd = prob["kd"]
+    op = api.OpticalProps2str()
+    assert op.alloc_2str(2, 3, kd_spec(kd), device=dev) == ""
+    src = api.SourceFuncLW()
+    assert src.alloc(2, 3, op, device=dev) == ""
+    f = lambda: torch.empty((2, 4), device=dev)  # noqa: E731
+    fl = api.FluxesBroadband(f(), f())
+    emis = torch.ones((2, kd["nband"]), device=dev)
+    assert api.rte_lw(op, True, src, emis, fl, n_gauss_angles=2, use_2stream=True) == \
+        "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"
+    op.ssa.fill_(2.0)
+    assert api.rte_lw(op, True, src, emis, fl, use_2stream=True) == "validate: ssa values out of range"
+    one = api.OpticalProps1scl()
+    assert one.alloc_1scl(2, 3, kd_spec(kd), device=dev) == ""
+    assert api.rte_lw(one, True, src, emis, fl, use_2stream=True) == \
+        "rte_lw: can't use two-stream methods with only absorption optical depth"
+
+
+def kd_spec(kd):
+    from rrtmgpnn import api
+    s = api.OpticalProps()
+    assert s.init(kd["band_lims_wvn"], kd["band_lims_gpt"]) == ""
+    return s
