@@ -41,6 +41,7 @@ extern "C" {
 typedef struct rrtmgpnn_context rrtmgpnn_context;
 typedef struct rrtmgpnn_network rrtmgpnn_network;
 typedef struct rrtmgpnn_cloud_optics rrtmgpnn_cloud_optics;
+typedef struct rrtmgpnn_file rrtmgpnn_file;
 
 /* ---- runtime ------------------------------------------------------------------------------ */
 int         rrtmgpnn_version(void);
@@ -227,6 +228,25 @@ int rrtmgpnn_increment(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, floa
 /* ty_optical_props_2str%delta_scale([for]) (rte/mo_optical_props.F90:576-604; kernels
  * rte/kernels/mo_optical_props_kernels.F90:41-92) on n values in place.  fwd == NULL: f = g**2. */
 int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);
+
+/* ---- data files ---------------------------------------------------------
+ * Native readers for the files the path consumes, replacing the netCDF-Fortran calls of
+ * neural/mod_network_rrtmgp.F90:58-122 (load_netcdf), examples/all-sky/mo_load_cloud_coefficients.F90 and
+ * examples/rfmip-clear-sky/mo_rfmip_io.F90: classic netCDF (CDF-1/2/5, parsed natively), netCDF-4 (HDF5,
+ * through libhdf5 bound at run time: RRTMGPNN_HDF5_LIB or the loader path) and this repository's RBIN.
+ * rrtmgpnn_network_load and rrtmgpnn_cloud_optics_load accept all three.  A file is read whole on open;
+ * dims are in file (C) order; dtype 0 float32 (floating-point variables, doubles rounded), 1 int32,
+ * 2 char.  Variable-length strings and netCDF-4 dimension-only scales are not exposed.  Host memory only. */
+int rrtmgpnn_file_open(const char *path, rrtmgpnn_file **f);
+int rrtmgpnn_file_close(rrtmgpnn_file *f);
+int rrtmgpnn_file_nvars(const rrtmgpnn_file *f, int *nvars);
+int rrtmgpnn_file_var_name(const rrtmgpnn_file *f, int i, char *name, int len);
+/* dims: room for 8 entries */
+int rrtmgpnn_file_var(const rrtmgpnn_file *f, const char *name, int *dtype, int *ndim, long long *dims);
+/* count = number of elements; numeric variables convert to the requested dtype (0 or 1) */
+int rrtmgpnn_file_read(const rrtmgpnn_file *f, const char *name, int dtype, void *out, long long count);
+/* text attribute `att` of variable `var` (NULL or "": global) */
+int rrtmgpnn_file_att(const rrtmgpnn_file *f, const char *var, const char *att, char *text, int len);
 
 #ifdef __cplusplus
 }

@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include "datafile.hpp"
 #include "internal.hpp"
 
 namespace rrtmgpnn {
@@ -22,60 +23,16 @@ int fail(int code, const std::string &msg)
   return code;
 }
 
-// ---- RBIN reader (format: tools/rbin.py) ----
-struct RbinArray {
-  int dtype = 0;
-  std::vector<int> dims;
-  std::vector<char> data;
-  size_t count() const
-  {
-    size_t n = 1;
-    for (int d : dims) n *= (size_t)d;
-    return n;
-  }
-};
-
-static int read_rbin(const char *path, std::map<std::string, RbinArray> &out)
+// activation names of neural/mod_layer.F90:64-121 (set_activation) -> the codes of network_create
+static int activation_code(std::string n)
 {
-  std::ifstream f(path, std::ios::binary);
-  if (!f) return fail(RRTMGPNN_ERR_IO, std::string("cannot open ") + path);
-  char magic[4];
-  uint32_t ver = 0, count = 0;
-  f.read(magic, 4);
-  f.read((char *)&ver, 4);
-  f.read((char *)&count, 4);
-  if (!f || std::memcmp(magic, "RBIN", 4) != 0 || ver != 1)
-    return fail(RRTMGPNN_ERR_IO, std::string(path) + ": not an RBIN v1 file");
-  for (uint32_t e = 0; e < count; e++) {
-    char name[64];
-    uint32_t dt = 0, nd = 0;
-    f.read(name, 64);
-    f.read((char *)&dt, 4);
-    f.read((char *)&nd, 4);
-    if (!f || dt > 2 || nd > 8) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": corrupt entry header");
-    RbinArray a;
-    a.dtype = (int)dt;
-    for (uint32_t i = 0; i < nd; i++) {
-      uint32_t d = 0;
-      f.read((char *)&d, 4);
-      a.dims.push_back((int)d);
-    }
-    size_t isz = dt == 2 ? 1 : 4;
-    a.data.resize(a.count() * isz);
-    f.read(a.data.data(), (std::streamsize)a.data.size());
-    if (!f) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": truncated");
-    name[63] = 0;
-    out[std::string(name)] = std::move(a);
-  }
-  return RRTMGPNN_OK;
-}
-
-template <typename T>
-static std::vector<T> as_vec(const RbinArray &a)
-{
-  std::vector<T> v(a.count());
-  std::memcpy(v.data(), a.data.data(), v.size() * sizeof(T));
-  return v;
+  while (!n.empty() && (n.back() == ' ' || n.back() == '\0')) n.pop_back();
+  size_t i = n.find_first_not_of(' ');
+  n = i == std::string::npos ? "" : n.substr(i);
+  static const char *names[] = {"linear", "softsign", "relu", "sigmoid", "hard_sigmoid", "tanh", "gaussian"};
+  for (int k = 0; k < 7; k++)
+    if (n == names[k]) return k;
+  return -1;
 }
 
 static int finalize_network(rrtmgpnn_network *net)
@@ -244,34 +201,58 @@ int rrtmgpnn_network_load(rrtmgpnn_context *ctx, const char *path, rrtmgpnn_netw
 {
   if (int rc = check_ctx(ctx)) return rc;
   if (!path || !net) return fail(RRTMGPNN_ERR_ARGUMENT, "network_load: null argument");
-  std::map<std::string, RbinArray> m;
-  if (int rc = read_rbin(path, m)) return rc;
-  for (const char *k : {"dims", "activation", "input_min", "input_max"})
-    if (!m.count(k)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing " + k);
-  std::vector<int> dims = as_vec<int>(m["dims"]);
-  std::vector<int> act = as_vec<int>(m["activation"]);
+  DataFile df;
+  if (int rc = read_data_file(path, df)) return rc;
+  auto &m = df.vars;
+  std::vector<int> dims, act;
+  std::vector<char> names;
+  const bool nc = df.has("nn_dimsize");  // the reference's netCDF model file (mod_network_rrtmgp.F90:58-122)
+  const char *kmin = nc ? "nn_input_coeffs_min" : "input_min", *kmax = nc ? "nn_input_coeffs_max" : "input_max";
+  const char *kmean = nc ? "nn_output_coeffs_mean" : "output_mean", *kstd = nc ? "nn_output_coeffs_std" : "output_std";
+  if (nc) {
+    for (const char *k : {"nn_activation_char", "nn_input_coeffs_min", "nn_input_coeffs_max"})
+      if (!df.has(k)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing " + k);
+    std::vector<int> hidden = to_int(m["nn_dimsize"]);
+    dims.push_back((int)m["nn_input_coeffs_min"].count());  // nn_dim_input
+    dims.insert(dims.end(), hidden.begin(), hidden.end());
+    const DataVar &ac = m["nn_activation_char"];  // (num_layers, string_len) characters
+    const size_t len = ac.dims.size() == 2 ? (size_t)ac.dims[1] : 0;
+    for (size_t n = 0; len && n < (size_t)ac.dims[0]; n++) {
+      const int code = activation_code(std::string(&ac.data[n * len], len));
+      if (code < 0) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": unknown activation function");
+      act.push_back(code);
+    }
+    if (df.has("nn_inputs_char")) {  // (nx, 32) characters, the layout of network_create's input_names
+      const DataVar &ic = m["nn_inputs_char"];
+      if (ic.dims.size() == 2 && ic.dims[1] == 32) names = ic.data;
+    }
+  } else {
+    for (const char *k : {"dims", "activation", "input_min", "input_max"})
+      if (!df.has(k)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing " + k);
+    dims = to_int(m["dims"]);
+    act = to_int(m["activation"]);
+    if (df.has("input_names")) names = m["input_names"].data;
+  }
   int nl = (int)dims.size() - 1;
   if (nl < 1 || nl > kMaxLayers || (int)act.size() != nl) return fail(RRTMGPNN_ERR_IO, "network_load: bad dims");
   std::vector<std::vector<float>> W(nl), B(nl);
   std::vector<const float *> wp(nl), bp(nl);
   for (int n = 0; n < nl; n++) {
-    std::string wn = "w" + std::to_string(n + 1), bn = "b" + std::to_string(n + 1);
-    if (!m.count(wn) || !m.count(bn)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing layer " + wn);
-    W[n] = as_vec<float>(m[wn]);
-    B[n] = as_vec<float>(m[bn]);
+    std::string wn = (nc ? "nn_weights_" : "w") + std::to_string(n + 1), bn = (nc ? "nn_bias_" : "b") + std::to_string(n + 1);
+    if (!df.has(wn) || !df.has(bn)) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing layer " + wn);
+    W[n] = to_float(m[wn]);  // file (C) order (n_in, n_out) in both formats
+    B[n] = to_float(m[bn]);
     if (W[n].size() != (size_t)dims[n] * dims[n + 1] || B[n].size() != (size_t)dims[n + 1])
       return fail(RRTMGPNN_ERR_IO, std::string(path) + ": layer size mismatch");
     wp[n] = W[n].data();
     bp[n] = B[n].data();
   }
-  std::vector<float> mn = as_vec<float>(m["input_min"]), mx = as_vec<float>(m["input_max"]);
+  std::vector<float> mn = to_float(m[kmin]), mx = to_float(m[kmax]);
   std::vector<float> om, os;
-  if (m.count("output_mean")) {
-    om = as_vec<float>(m["output_mean"]);
-    os = as_vec<float>(m["output_std"]);
+  if (df.has(kmean) && df.has(kstd)) {
+    om = to_float(m[kmean]);
+    os = to_float(m[kstd]);
   }
-  std::vector<char> names;
-  if (m.count("input_names")) names = m["input_names"].data;
   return rrtmgpnn_network_create(ctx, nl, dims.data(), act.data(), wp.data(), bp.data(), mn.data(), mx.data(),
                                  om.empty() ? nullptr : om.data(), os.empty() ? nullptr : os.data(),
                                  names.empty() ? nullptr : names.data(), net);
@@ -694,17 +675,18 @@ int rrtmgpnn_cloud_optics_load(rrtmgpnn_context *ctx, const char *path, int use_
 {
   if (int rc = check_ctx(ctx)) return rc;
   if (!path || !co) return fail(RRTMGPNN_ERR_ARGUMENT, "cloud_optics_load: null argument");
-  std::map<std::string, RbinArray> m;
-  if (int rc = read_rbin(path, m)) return rc;
-  auto need = [&](const char *k) -> const RbinArray * {
+  DataFile df;  // RBIN conversion or the coefficient file itself (classic netCDF)
+  if (int rc = read_data_file(path, df)) return rc;
+  auto &m = df.vars;
+  auto need = [&](const char *k) -> const DataVar * {
     auto it = m.find(k);
     return it == m.end() ? nullptr : &it->second;
   };
-  const RbinArray *bl = need("bnd_limits_wavenumber");
+  const DataVar *bl = need("bnd_limits_wavenumber");
   if (!bl || bl->dims.size() != 2) return fail(RRTMGPNN_ERR_IO, std::string(path) + ": missing bnd_limits_wavenumber");
   const int nband = bl->dims[0];
-  std::vector<float> blw = as_vec<float>(*bl);
-  auto F = [&](const char *k) { return as_vec<float>(m[k]); };
+  std::vector<float> blw = to_float(*bl);
+  auto F = [&](const char *k) { return to_float(m[k]); };
   if (use_lut) {
     for (const char *k : {"lut_extliq", "lut_ssaliq", "lut_asyliq", "lut_extice", "lut_ssaice", "lut_asyice",
                           "radliq_lwr", "radliq_upr", "radice_lwr", "radice_upr"})
@@ -801,6 +783,90 @@ int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, fl
   if (int rc = check_ctx(ctx)) return rc;
   if (!tau || !ssa || !g || n < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "delta_scale: bad argument");
   return launch_delta_scale(ctx, n, tau, ssa, g, fwd);
+}
+
+// ---- data files: RBIN, classic netCDF, netCDF-4 (datafile.cpp) ----
+struct rrtmgpnn_file {
+  DataFile df;
+  std::vector<std::string> names;
+};
+
+int rrtmgpnn_file_open(const char *path, rrtmgpnn_file **f)
+{
+  if (!path || !f) return fail(RRTMGPNN_ERR_ARGUMENT, "file_open: null argument");
+  rrtmgpnn_file *h = new rrtmgpnn_file();
+  if (int rc = read_data_file(path, h->df)) {
+    delete h;
+    return rc;
+  }
+  for (const auto &kv : h->df.vars) h->names.push_back(kv.first);
+  *f = h;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_file_close(rrtmgpnn_file *f)
+{
+  delete f;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_file_nvars(const rrtmgpnn_file *f, int *nvars)
+{
+  if (!f || !nvars) return fail(RRTMGPNN_ERR_ARGUMENT, "file_nvars: null argument");
+  *nvars = (int)f->names.size();
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_file_var_name(const rrtmgpnn_file *f, int i, char *name, int len)
+{
+  if (!f || !name || len < 1 || i < 0 || i >= (int)f->names.size())
+    return fail(RRTMGPNN_ERR_ARGUMENT, "file_var_name: bad argument");
+  std::snprintf(name, (size_t)len, "%s", f->names[i].c_str());
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_file_var(const rrtmgpnn_file *f, const char *name, int *dtype, int *ndim, long long *dims)
+{
+  if (!f || !name) return fail(RRTMGPNN_ERR_ARGUMENT, "file_var: null argument");
+  auto it = f->df.vars.find(name);
+  if (it == f->df.vars.end()) return fail(RRTMGPNN_ERR_IO, std::string("file: no variable ") + name);
+  if (dtype) *dtype = it->second.dtype;
+  if (ndim) *ndim = (int)it->second.dims.size();
+  if (dims)
+    for (size_t k = 0; k < it->second.dims.size(); k++) dims[k] = it->second.dims[k];
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_file_read(const rrtmgpnn_file *f, const char *name, int dtype, void *out, long long count)
+{
+  if (!f || !name || !out || count < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "file_read: bad argument");
+  auto it = f->df.vars.find(name);
+  if (it == f->df.vars.end()) return fail(RRTMGPNN_ERR_IO, std::string("file: no variable ") + name);
+  const DataVar &v = it->second;
+  if ((long long)v.count() != count) return fail(RRTMGPNN_ERR_ARGUMENT, std::string("file_read: ") + name + ": size mismatch");
+  if (dtype == kChar || v.dtype == kChar) {
+    if (dtype != v.dtype) return fail(RRTMGPNN_ERR_ARGUMENT, std::string("file_read: ") + name + ": character/numeric mismatch");
+    std::memcpy(out, v.data.data(), v.data.size());
+  } else if (dtype == kF32) {
+    std::vector<float> a = to_float(v);
+    std::memcpy(out, a.data(), a.size() * 4);
+  } else if (dtype == kI32) {
+    std::vector<int> a = to_int(v);
+    std::memcpy(out, a.data(), a.size() * 4);
+  } else {
+    return fail(RRTMGPNN_ERR_ARGUMENT, "file_read: dtype must be 0 (float32), 1 (int32) or 2 (char)");
+  }
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_file_att(const rrtmgpnn_file *f, const char *var, const char *att, char *text, int len)
+{
+  if (!f || !att || !text || len < 1) return fail(RRTMGPNN_ERR_ARGUMENT, "file_att: bad argument");
+  auto it = f->df.atts.find(std::string(var ? var : "") + ":" + att);
+  if (it == f->df.atts.end())
+    return fail(RRTMGPNN_ERR_IO, std::string("file: no text attribute ") + (var ? var : "") + ":" + att);
+  std::snprintf(text, (size_t)len, "%s", it->second.c_str());
+  return RRTMGPNN_OK;
 }
 
 }  // extern "C"

@@ -1,9 +1,9 @@
 ! mo_cloud_optics -- drop-in for extensions/cloud_optics/mo_cloud_optics.F90 (ty_cloud_optics): liquid and
 ! ice cloud optical properties by band, from a lookup table (load_lut) or Pade approximants (load_pade) of
 ! effective radius.  The coefficient tables live on the device inside an rrtmgpnn_cloud_optics handle;
-! cloud_optics (:354-535) runs as one HIP kernel over (band, layer, column).  load_rbin reads the RBIN
-! conversion of rrtmgp-cloud-optics-coeffs-{lw,sw}.nc (the netCDF reader of the example drivers,
-! mo_load_cloud_coefficients, is outside this build).
+! cloud_optics (:354-535) runs as one HIP kernel over (band, layer, column).  load_rbin reads the coefficient
+! file rrtmgp-cloud-optics-coeffs-{lw,sw}.nc itself (classic netCDF, native reader) or its RBIN conversion --
+! what the example drivers' mo_load_cloud_coefficients does with netcdf-fortran.
 module mo_cloud_optics
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,          only: wp
@@ -114,7 +114,8 @@ contains
     error_msg = this%adopt(h)
   end function load_pade
 
-  ! The RBIN conversion of rrtmgp-cloud-optics-coeffs-{lw,sw}.nc; use_lut selects load_lut or load_pade.
+  ! rrtmgp-cloud-optics-coeffs-{lw,sw}.nc (classic netCDF) or its RBIN conversion, read by the library's native
+  ! readers; use_lut selects load_lut or load_pade (mo_load_cloud_coefficients wraps this for the drivers).
   function load_rbin(this, filename, use_lut) result(error_msg)
     class(ty_cloud_optics), intent(inout) :: this
     character(len=*),       intent(in)    :: filename
@@ -138,12 +139,16 @@ contains
   end function load_rbin
 
   function band_limits_of(filename, wvn) result(error_msg)
-    use mo_rrtmgpnn_rbin, only: rbin_real2
+    use mo_rrtmgpnn_file, only: ty_data_file
     character(len=*), intent(in) :: filename
     real(wp), dimension(:,:), intent(out) :: wvn
     character(len=128) :: error_msg
+    type(ty_data_file) :: f
     real(wp), allocatable :: a(:,:)
-    call rbin_real2(filename, "bnd_limits_wavenumber", a, error_msg)
+    error_msg = f%open(filename)
+    if (error_msg /= '') return
+    error_msg = f%real2("bnd_limits_wavenumber", a)
+    call f%close()
     if (error_msg /= '') return
     if (any(shape(a) /= shape(wvn))) then
       error_msg = "cloud_optics%load: bnd_limits_wavenumber inconsistently sized"; return

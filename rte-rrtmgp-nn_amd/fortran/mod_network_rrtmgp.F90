@@ -2,13 +2,13 @@
 ! rrtmgp_network_type keeps the public components the drivers read (layers(:)%w_transposed, layers(:)%b,
 ! input_names, coeffs_input_min/max, coeffs_output_mean/std) and `load_netcdf(filename)`; the model is
 ! uploaded once to the device (MFMA-packed weight image) and evaluated by the fused HIP MLP kernels.
-! netcdf-fortran is absent in this image, so `load_netcdf` reads the RBIN conversion of the model
-! (tools/convert_reference_data.py); the file layout of every variable is unchanged.
+! `load_netcdf` reads the reference's netCDF model file with the library's native reader (netcdf-fortran is
+! absent in this image), or the RBIN conversion of it (tools/convert_reference_data.py).
 module mod_network_rrtmgp
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,      only: sp
   use mo_rrtmgpnn_c,    only: rrtmgpnn_ctx, c_rrtmgpnn_network_load, rrtmgpnn_error_message
-  use mo_rrtmgpnn_rbin, only: rbin_real1, rbin_real2, rbin_int1, rbin_strings
+  use mo_rrtmgpnn_file, only: ty_data_file
   implicit none
   private
   public :: rrtmgp_network_type, layer_type
@@ -32,37 +32,57 @@ module mod_network_rrtmgp
 
 contains
 
+  ! load_netcdf (neural/mod_network_rrtmgp.F90:58-122): the reference's netCDF model file, read natively
+  ! (mo_rrtmgpnn_file), or its RBIN conversion; both hold the same arrays.
   subroutine load_netcdf(self, filename)
     class(rrtmgp_network_type), intent(inout) :: self
     character(len=*), intent(in) :: filename
+    type(ty_data_file) :: f
     character(len=128) :: err
     integer :: n, nl
-    real(sp), allocatable :: wflat(:,:)
+    real(sp), allocatable :: wflat(:,:), mn(:)
+    integer(c_int), allocatable :: hidden(:)
     integer(c_int) :: rc
+    logical :: nc
     character(len=8) :: cn
-    call rbin_int1(filename, "dims", self%dims, err)
+    err = f%open(filename)
     if (err /= '') call fail(err)
+    nc = f%has("nn_dimsize")
+    if (nc) then
+      call check(f%int1("nn_dimsize", hidden))
+      call check(f%real1("nn_input_coeffs_min", mn))
+      self%dims = [size(mn), int(hidden)]                  ! nn_dim_input, nn_dimsize
+    else
+      call check(f%int1("dims", hidden))
+      self%dims = int(hidden)
+    end if
     nl = size(self%dims) - 1
+    if (allocated(self%layers)) deallocate(self%layers)
     allocate(self%layers(nl))
     do n = 1, nl
       write(cn, '(i0)') n
-      call rbin_real2(filename, "w" // trim(cn), wflat, err)  ! C (n_in,n_out) -> Fortran (n_out,n_in)
-      if (err /= '') call fail(err)
+      ! file (n_in, n_out) C order = Fortran (n_out, n_in): w_transposed as is, w its transpose (:92-95)
+      call check(f%real2(merge("nn_weights_" // trim(cn), "w" // trim(cn) // "         ", nc), wflat))
       self%layers(n)%w_transposed = wflat
       self%layers(n)%w = transpose(wflat)
-      call rbin_real1(filename, "b" // trim(cn), self%layers(n)%b, err)
-      if (err /= '') call fail(err)
+      call check(f%real1(merge("nn_bias_" // trim(cn), "b" // trim(cn) // "      ", nc), self%layers(n)%b))
     end do
-    call rbin_real1(filename, "input_min", self%coeffs_input_min, err)
-    call rbin_real1(filename, "input_max", self%coeffs_input_max, err)
-    call rbin_strings(filename, "input_names", self%input_names, err)
-    call rbin_real1(filename, "output_mean", self%coeffs_output_mean, err)
-    if (err /= '' .and. allocated(self%coeffs_output_mean)) deallocate(self%coeffs_output_mean)
-    call rbin_real1(filename, "output_std", self%coeffs_output_std, err)
-    if (err /= '' .and. allocated(self%coeffs_output_std)) deallocate(self%coeffs_output_std)
+    call check(f%real1(merge("nn_input_coeffs_min", "input_min          ", nc), self%coeffs_input_min))
+    call check(f%real1(merge("nn_input_coeffs_max", "input_max          ", nc), self%coeffs_input_max))
+    if (f%has(merge("nn_inputs_char", "input_names   ", nc))) &
+      call check(f%strings(merge("nn_inputs_char", "input_names   ", nc), self%input_names))
+    if (f%has(merge("nn_output_coeffs_mean", "output_mean          ", nc))) then
+      call check(f%real1(merge("nn_output_coeffs_mean", "output_mean          ", nc), self%coeffs_output_mean))
+      call check(f%real1(merge("nn_output_coeffs_std ", "output_std           ", nc), self%coeffs_output_std))
+    end if
+    call f%close()
     rc = c_rrtmgpnn_network_load(rrtmgpnn_ctx(), trim(filename) // c_null_char, self%handle)
-    if (rc /= 0) call fail("mod_network_rrtmgp:load_netcdf: " // trim(rrtmgpnn_error_message()))
+    if (rc /= 0) call fail(trim(rrtmgpnn_error_message()))
   contains
+    subroutine check(msg)
+      character(len=*), intent(in) :: msg
+      if (msg /= '') call fail(msg)
+    end subroutine check
     subroutine fail(msg)
       character(len=*), intent(in) :: msg
       write(*, '(a)') "mod_network_rrtmgp:load_netcdf: " // trim(msg)

@@ -3,8 +3,10 @@
 ! optics by band (LUT, ice roughness 2), clouds%increment(atmos) for LW, clouds%delta_scale() then
 ! clouds%increment(atmos) for SW -- the same class calls a reference user makes, now on the GPU.
 !
-! usage: rrtmgpnn_allsky <problem.rbin> <output.rbin> <data_dir> [block_size]
-!   problem.rbin / output.rbin as for rrtmgpnn_rfmip_clear_sky.
+! usage: rrtmgpnn_allsky <problem.rbin> <output.rbin> <data_dir> [block_size] [nc]
+!   problem.rbin / output.rbin as for rrtmgpnn_rfmip_clear_sky.  With "nc" the NN models and the cloud-optics
+!   coefficients are the reference's own netCDF files, by their reference names, in data_dir (read by the
+!   library's native readers: load_netcdf, load_cld_lutcoeff); otherwise their RBIN conversions.
 program rrtmgpnn_allsky
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -14,6 +16,7 @@ program rrtmgpnn_allsky
   use mo_gas_optics_rrtmgp,  only: ty_gas_optics_rrtmgp
   use mod_network_rrtmgp,    only: rrtmgp_network_type
   use mo_cloud_optics,       only: ty_cloud_optics
+  use mo_load_cloud_coefficients, only: load_cld_lutcoeff
   use mo_rte_lw,             only: rte_lw
   use mo_rte_sw,             only: rte_sw
   use mo_rrtmgpnn_rbin
@@ -35,12 +38,12 @@ program rrtmgpnn_allsky
   type(ty_source_func_lw) :: sources
   type(ty_fluxes_flexible) :: fluxes
   character(len=128) :: e
-  logical :: top_at_1, cloudy
+  logical :: top_at_1, cloudy, nc
   real(wp) :: rel_val, rei_val
   integer :: ncol, nlay, ngas, nmus, block_size, b0, b1, nb, icol, ilay, igpt, ig, u
 
   if (command_argument_count() < 3) then
-    write(*, '(a)') "usage: rrtmgpnn_allsky <problem.rbin> <output.rbin> <data_dir> [block_size]"
+    write(*, '(a)') "usage: rrtmgpnn_allsky <problem.rbin> <output.rbin> <data_dir> [block_size] [nc]"
     stop 2
   end if
   call get_command_argument(1, problem_file)
@@ -50,6 +53,11 @@ program rrtmgpnn_allsky
   if (command_argument_count() >= 4) then
     call get_command_argument(4, arg)
     read(arg, *) block_size
+  end if
+  nc = .false.
+  if (command_argument_count() >= 5) then
+    call get_command_argument(5, arg)
+    nc = trim(arg) == "nc"
   end if
 
   call rbin_real2(problem_file, "play", play, e); call stop_on_err(e)
@@ -72,15 +80,27 @@ program rrtmgpnn_allsky
   ngas = size(gas_names)
   if (block_size <= 0) block_size = ncol
 
-  call nets_lw(1)%load_netcdf(trim(data_dir) // "/nn_lw_g256_abs.rbin")
-  call nets_lw(2)%load_netcdf(trim(data_dir) // "/nn_lw_g256_pfrac.rbin")
-  call nets_sw(1)%load_netcdf(trim(data_dir) // "/nn_sw_g224_abs.rbin")
-  call nets_sw(2)%load_netcdf(trim(data_dir) // "/nn_sw_g224_ray.rbin")
+  if (nc) then  ! neural/data/ file names of the reference
+    call nets_lw(1)%load_netcdf(trim(data_dir) // "/lw-g256-2018-12-04_absorption_58_58.nc")
+    call nets_lw(2)%load_netcdf(trim(data_dir) // "/lw-g256-2018-12-04_planck_frac_16_16.nc")
+    call nets_sw(1)%load_netcdf(trim(data_dir) // "/sw-g224-2018-12-04-absorption_16_16.nc")
+    call nets_sw(2)%load_netcdf(trim(data_dir) // "/sw-g224-2018-12-04-rayleigh_16_16.nc")
+  else
+    call nets_lw(1)%load_netcdf(trim(data_dir) // "/nn_lw_g256_abs.rbin")
+    call nets_lw(2)%load_netcdf(trim(data_dir) // "/nn_lw_g256_pfrac.rbin")
+    call nets_sw(1)%load_netcdf(trim(data_dir) // "/nn_sw_g224_abs.rbin")
+    call nets_sw(2)%load_netcdf(trim(data_dir) // "/nn_sw_g224_ray.rbin")
+  end if
   call stop_on_err(kdist_lw%load_rbin(trim(data_dir) // "/kdist_lw_g256.rbin", gas_names))
   call stop_on_err(kdist_sw%load_rbin(trim(data_dir) // "/kdist_sw_g224.rbin", gas_names))
   call stop_on_err(kdist_sw%set_tsi(1361.0_wp))                  ! rrtmgp_rfmip_sw.F90:317
-  call stop_on_err(cloud_optics_lw%load_rbin(trim(data_dir) // "/cloud_optics_lw.rbin", .true.))
-  call stop_on_err(cloud_optics_sw%load_rbin(trim(data_dir) // "/cloud_optics_sw.rbin", .true.))
+  if (nc) then  ! rrtmgp_allsky.F90:213-217
+    call load_cld_lutcoeff(cloud_optics_lw, trim(data_dir) // "/rrtmgp-cloud-optics-coeffs-lw.nc")
+    call load_cld_lutcoeff(cloud_optics_sw, trim(data_dir) // "/rrtmgp-cloud-optics-coeffs-sw.nc")
+  else
+    call stop_on_err(cloud_optics_lw%load_rbin(trim(data_dir) // "/cloud_optics_lw.rbin", .true.))
+    call stop_on_err(cloud_optics_sw%load_rbin(trim(data_dir) // "/cloud_optics_sw.rbin", .true.))
+  end if
   call stop_on_err(cloud_optics_lw%set_ice_roughness(2))         ! rrtmgp_allsky.F90:219
   call stop_on_err(cloud_optics_sw%set_ice_roughness(2))
 

@@ -73,6 +73,13 @@ SIGNATURES = {
                                          c_vp]),
     "rrtmgpnn_increment": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_delta_scale_2str": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_file_open": (c_int, [c_char_p, P(c_vp)]),
+    "rrtmgpnn_file_close": (c_int, [c_vp]),
+    "rrtmgpnn_file_nvars": (c_int, [c_vp, P(c_int)]),
+    "rrtmgpnn_file_var_name": (c_int, [c_vp, c_int, c_char_p, c_int]),
+    "rrtmgpnn_file_var": (c_int, [c_vp, c_char_p, P(c_int), P(c_int), P(c_ll)]),
+    "rrtmgpnn_file_read": (c_int, [c_vp, c_char_p, c_int, c_vp, c_ll]),
+    "rrtmgpnn_file_att": (c_int, [c_vp, c_char_p, c_char_p, c_char_p, c_int]),
 }
 
 

@@ -101,19 +101,41 @@ class RrtmgpNetwork:
         self.h = None
 
     def load_netcdf(self, filename):
-        """Reference name kept (mod_network_rrtmgp.F90:58); reads the RBIN conversion of the netCDF model."""
-        m = rbin.read(filename)
-        self.dims = [int(v) for v in m["dims"]]
-        self.activation = [int(v) for v in m["activation"]]
-        self.input_names = rbin.unchars(m["input_names"]) if "input_names" in m else [""] * self.dims[0]
-        self.coeffs_input_min = m["input_min"]
-        self.coeffs_input_max = m["input_max"]
-        self.coeffs_output_mean = m.get("output_mean")
-        self.coeffs_output_std = m.get("output_std")
+        """neural/mod_network_rrtmgp.F90:58-122.  `filename` is the reference's netCDF model file (read natively,
+        csrc/datafile.cpp) or its RBIN conversion."""
+        from . import ncio
+        with ncio.DataFile(filename) as f:
+            if "nn_dimsize" in f:  # the netCDF model: nn_dim_input, nn_dimsize, nn_activation_char, ...
+                self.dims = [int(f.read("nn_input_coeffs_min").size)] + [int(v) for v in f.read("nn_dimsize")]
+                acts = ["linear", "softsign", "relu", "sigmoid", "hard_sigmoid", "tanh", "gaussian"]
+                self.activation = [acts.index(a) for a in f.strings("nn_activation_char")]
+                self.input_names = f.strings("nn_inputs_char") if "nn_inputs_char" in f else [""] * self.dims[0]
+                self.coeffs_input_min = f.read("nn_input_coeffs_min", np.float32)
+                self.coeffs_input_max = f.read("nn_input_coeffs_max", np.float32)
+                has_out = "nn_output_coeffs_mean" in f
+                self.coeffs_output_mean = f.read("nn_output_coeffs_mean", np.float32) if has_out else None
+                self.coeffs_output_std = f.read("nn_output_coeffs_std", np.float32) if has_out else None
+                m = {"dims": np.array(self.dims, np.int32), "activation": np.array(self.activation, np.int32),
+                     "input_names": rbin.chars(self.input_names), "input_min": self.coeffs_input_min,
+                     "input_max": self.coeffs_input_max}
+                for n in range(1, len(self.dims)):
+                    m["w%d" % n] = f.read("nn_weights_%d" % n, np.float32)
+                    m["b%d" % n] = f.read("nn_bias_%d" % n, np.float32)
+                if has_out:
+                    m["output_mean"], m["output_std"] = self.coeffs_output_mean, self.coeffs_output_std
+            else:
+                m = {v: f.read(v) for v in f.vars}
+                self.dims = [int(v) for v in m["dims"]]
+                self.activation = [int(v) for v in m["activation"]]
+                self.input_names = rbin.unchars(m["input_names"]) if "input_names" in m else [""] * self.dims[0]
+                self.coeffs_input_min = m["input_min"]
+                self.coeffs_input_max = m["input_max"]
+                self.coeffs_output_mean = m.get("output_mean")
+                self.coeffs_output_std = m.get("output_std")
         self.model = m
         ctx = context(self.device)
         h = _lib.c_vp()
-        check(_lib.lib().rrtmgpnn_network_load(ctx.h, filename.encode(), h), "network_load(%s)" % filename)
+        check(_lib.lib().rrtmgpnn_network_load(ctx.h, str(filename).encode(), h), "network_load(%s)" % filename)
         self.h = h
         return self
 
@@ -522,13 +544,18 @@ class CloudOptics(OpticalProps):
     def load(self, which, use_lut=True):
         """Coefficients of extensions/cloud_optics/rrtmgp-cloud-optics-coeffs-{lw,sw}.nc (RBIN conversion);
         the LUT (load_lut) or Pade (load_pade) method."""
-        path = data.cloud_optics_path(which)
-        m = data.load_cloud_optics(which)
-        e = self.init(m["bnd_limits_wavenumber"], name="RRTMGP cloud optics")
+        return self._load_path(data.cloud_optics_path(which), use_lut)
+
+    def _load_path(self, path, use_lut=True):
+        """The coefficient file itself (classic netCDF, read natively) or its RBIN conversion."""
+        from . import ncio
+        with ncio.DataFile(path) as f:
+            wvn = f.read("bnd_limits_wavenumber", np.float32)
+        e = self.init(wvn, name="RRTMGP cloud optics")
         if e:
             return e
         h = _lib.c_vp()
-        check(_lib.lib().rrtmgpnn_cloud_optics_load(context(self.device).h, path.encode(), int(bool(use_lut)), h),
+        check(_lib.lib().rrtmgpnn_cloud_optics_load(context(self.device).h, str(path).encode(), int(bool(use_lut)), h),
               "cloud_optics_load(%s)" % path)
         return self._adopt(h)
 

@@ -99,13 +99,15 @@ LW_GAS_ORDER = ["h2o", "o3", "co2", "n2o", "ch4", "cfc11", "cfc12", "co", "ccl4"
                 "hfc125", "hfc23", "hfc32", "hfc134a", "cf4", "o2", "n2"]
 
 
-def rfmip_problem(lw_press_clamp=True):
+def rfmip_problem(lw_press_clamp=True, fields=None):
     """All 1800 RFMIP clear-sky columns (nlay = 60, top at index 1).
 
     Returns dict with play (ncol,nlay), plev (ncol,nlay+1), tlay, tlev, tsfc (ncol), gases
     {name: (ncol,nlay)}, sfc_emis (ncol), sfc_alb (ncol), sza, tsi, mu0, usecol, top_at_1.
+    `fields`: the input file's fields, by default the committed RBIN conversion; ncio.rfmip_fields(path) reads
+    the reference's netCDF file natively instead.
     """
-    d = rbin.read(os.path.join(DATA_DIR, "rfmip_clear_sky.rbin"))
+    d = fields if fields is not None else rbin.read(os.path.join(DATA_DIR, "rfmip_clear_sky.rbin"))
     nexp, nsite, nlay = d["temp_layer"].shape
     ncol = nsite * nexp
     site = np.tile(np.arange(nsite), nexp)

@@ -105,9 +105,13 @@ def test_fortran_rfmip_driver_matches_oracle(tmp_path, orc, rfmip):
 
 @pytest.mark.gpu
 @needs_fc
-def test_fortran_allsky_driver_matches_oracle(tmp_path, orc, rfmip):
+@pytest.mark.parametrize("files", ["rbin", "nc"])
+def test_fortran_allsky_driver_matches_oracle(tmp_path, orc, rfmip, files):
     """The all-sky host program (cloud_optics, clouds%increment, clouds%delta_scale through the Fortran class
-    layer), blocked with a ragged last block, vs the oracle's all-sky pipeline -- bit for bit."""
+    layer), blocked with a ragged last block, vs the oracle's all-sky pipeline -- bit for bit.  "nc": the models
+    and cloud coefficients as netCDF files under the reference's names (load_netcdf, load_cld_lutcoeff through
+    the native readers; written here from the RBIN data in the reference's layout)."""
+    from ncfixtures import write_arrays_netcdf, write_nn_netcdf
     from rrtmgpnn import data, rbin
     exe = os.path.join(FBUILD, "rrtmgpnn_allsky")
     if not os.path.exists(exe):
@@ -115,7 +119,21 @@ def test_fortran_allsky_driver_matches_oracle(tmp_path, orc, rfmip):
     prob = subset(rfmip, np.arange(0, 1800, 9))
     fin, fout = str(tmp_path / "prob.rbin"), str(tmp_path / "flux.rbin")
     write_problem(prob, fin)
-    r = subprocess.run(["timeout", "-k", "10", "300", exe, fin, fout, data.DATA_DIR, "64"], capture_output=True,
+    ddir, extra = data.DATA_DIR, []
+    if files == "nc":
+        ddir = str(tmp_path / "data")
+        os.makedirs(ddir)
+        for k in ("kdist_lw_g256.rbin", "kdist_sw_g224.rbin"):
+            shutil.copy(os.path.join(data.DATA_DIR, k), ddir)
+        for m, name in (("lw_abs", "lw-g256-2018-12-04_absorption_58_58.nc"),
+                        ("lw_pfrac", "lw-g256-2018-12-04_planck_frac_16_16.nc"),
+                        ("sw_abs", "sw-g224-2018-12-04-absorption_16_16.nc"),
+                        ("sw_ray", "sw-g224-2018-12-04-rayleigh_16_16.nc")):
+            write_nn_netcdf(data.load_model(m), os.path.join(ddir, name))
+        for w in ("lw", "sw"):
+            write_arrays_netcdf(data.load_cloud_optics(w), os.path.join(ddir, "rrtmgp-cloud-optics-coeffs-%s.nc" % w))
+        extra = ["nc"]
+    r = subprocess.run(["timeout", "-k", "10", "300", exe, fin, fout, ddir, "64"] + extra, capture_output=True,
                        text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     got = rbin.read(fout)
