@@ -62,23 +62,33 @@ contains
     do n = 1, nl
       write(cn, '(i0)') n
       ! file (n_in, n_out) C order = Fortran (n_out, n_in): w_transposed as is, w its transpose (:92-95)
-      call check(f%real2(merge("nn_weights_" // trim(cn), "w" // trim(cn) // "         ", nc), wflat))
+      call check(f%real2(pick("nn_weights_" // trim(cn), "w" // trim(cn)), wflat))
       self%layers(n)%w_transposed = wflat
       self%layers(n)%w = transpose(wflat)
-      call check(f%real1(merge("nn_bias_" // trim(cn), "b" // trim(cn) // "      ", nc), self%layers(n)%b))
+      call check(f%real1(pick("nn_bias_" // trim(cn), "b" // trim(cn)), self%layers(n)%b))
     end do
-    call check(f%real1(merge("nn_input_coeffs_min", "input_min          ", nc), self%coeffs_input_min))
-    call check(f%real1(merge("nn_input_coeffs_max", "input_max          ", nc), self%coeffs_input_max))
-    if (f%has(merge("nn_inputs_char", "input_names   ", nc))) &
-      call check(f%strings(merge("nn_inputs_char", "input_names   ", nc), self%input_names))
-    if (f%has(merge("nn_output_coeffs_mean", "output_mean          ", nc))) then
-      call check(f%real1(merge("nn_output_coeffs_mean", "output_mean          ", nc), self%coeffs_output_mean))
-      call check(f%real1(merge("nn_output_coeffs_std ", "output_std           ", nc), self%coeffs_output_std))
+    call check(f%real1(pick("nn_input_coeffs_min", "input_min"), self%coeffs_input_min))
+    call check(f%real1(pick("nn_input_coeffs_max", "input_max"), self%coeffs_input_max))
+    if (f%has(pick("nn_inputs_char", "input_names"))) &
+      call check(f%strings(pick("nn_inputs_char", "input_names"), self%input_names))
+    if (f%has(pick("nn_output_coeffs_mean", "output_mean"))) then
+      call check(f%real1(pick("nn_output_coeffs_mean", "output_mean"), self%coeffs_output_mean))
+      call check(f%real1(pick("nn_output_coeffs_std", "output_std"), self%coeffs_output_std))
     end if
     call f%close()
     rc = c_rrtmgpnn_network_load(rrtmgpnn_ctx(), trim(filename) // c_null_char, self%handle)
     if (rc /= 0) call fail(trim(rrtmgpnn_error_message()))
   contains
+    ! the netCDF variable name, or the RBIN conversion's
+    function pick(nc_name, rbin_name) result(name)
+      character(len=*), intent(in) :: nc_name, rbin_name
+      character(len=:), allocatable :: name
+      if (nc) then
+        name = nc_name
+      else
+        name = rbin_name
+      end if
+    end function pick
     subroutine check(msg)
       character(len=*), intent(in) :: msg
       if (msg /= '') call fail(msg)
