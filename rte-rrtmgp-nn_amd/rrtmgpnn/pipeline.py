@@ -33,13 +33,17 @@ from ._lib import check, float_array, int_array, ptr_array
 from .api import GAUSS_DS, GAUSS_WTS, Context
 
 
+# calls of the SW chain (issued on the second stream when overlapping)
+SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver"}
+
+
 def _t(a, dev):
     return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
 
 
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
-                 sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True):
+                 sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True):
         self.dev = torch.device("cuda", device)
         self.allsky = clouds is not None
         self.fused = fused
@@ -200,7 +204,20 @@ class ClearSkyStep:
                  (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
+        # overlap: the SW chain runs on a second context/stream, forked after col_dry (which both streams read)
+        # and joined at the end of the step -- the VALU-bound SW solver shares the CUs with the MFMA-bound LW
+        # network and the LW solver instead of running after them
+        self.overlap = overlap
+        self.ctx2 = None
+        if overlap:
+            self.ctx2 = Context(device, torch.cuda.Stream(self.dev))
+            self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
+            self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
+
+    def stream_for(self, name):
+        """The torch stream a call of `self.calls` is issued on."""
+        return self.ctx2.stream if (self.overlap and name in SW_CHAIN) else self.ctx.stream
 
     def _cloud_optics(self, which, lut, icergh):
         h = _lib.c_vp()
@@ -223,6 +240,12 @@ class ClearSkyStep:
             rc = fn(*args)
             if rc:
                 check(rc, name)
+            if self.overlap and name == "get_col_dry":
+                self._fork.record(self.ctx.stream)
+                self.ctx2.stream.wait_event(self._fork)
+        if self.overlap:
+            self._join.record(self.ctx2.stream)
+            self.ctx.stream.wait_event(self._join)
 
     def capture(self):
         """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`."""
@@ -231,11 +254,16 @@ class ClearSkyStep:
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.dev)
         old = self.ctx.stream
+        if self.overlap:
+            old2 = self.ctx2.stream
+            self.ctx2.use_stream(torch.cuda.Stream(self.dev))
         with torch.cuda.stream(s):
             self.ctx.use_stream(s)
             with torch.cuda.graph(g, stream=s):
                 self.step()
         self.ctx.use_stream(old)
+        if self.overlap:
+            self.ctx2.use_stream(old2)
         self.graph = g
         return g
 
