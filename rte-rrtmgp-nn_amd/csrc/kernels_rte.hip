@@ -145,6 +145,11 @@ static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
 #define RRTMGPNN_SW_INC_PARK 1
 #endif
 static constexpr bool kSwIncPark = RRTMGPNN_SW_INC_PARK != 0;
+// SW solver with two g-points per lane and packed fp32 (kernels_sw_x2.hip) whenever ngpt is even
+#ifndef RRTMGPNN_SW_X2
+#define RRTMGPNN_SW_X2 1
+#endif
+static constexpr bool kSwX2 = RRTMGPNN_SW_X2 != 0;
 static constexpr int kLwMaxG = RRTMGPNN_LW_WAVES > 0 ? 256 : 1024;  // g-points per column block
 static constexpr int kSwMaxG = RRTMGPNN_SW_WAVES > 0 ? 256 : 1024;
 // ------------------------------------------------------------------------------------------
@@ -708,10 +713,14 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
   const bool inc = bands != nullptr;
+  const bool x2 = kSwX2 && (ngpt % 2) == 0;  // two g-points per lane (kernels_sw_x2.hip)
   void *ws = nullptr;
-  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc && kSwIncPark ? 3 * (size_t)ngpt * nlay * ncol : 0);
+  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc && (kSwIncPark || x2) ? 3 * (size_t)ngpt * nlay * ncol : 0);
   int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;
+  if (x2)
+    return launch_sw_2stream_x2(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
+                                alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
   int threads = (ngpt + 63) / 64 * 64;
   size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRingSw * ngpt + (size_t)3 * (nlay + 1) * 4);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");

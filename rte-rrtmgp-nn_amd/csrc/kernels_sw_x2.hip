@@ -1,0 +1,362 @@
+// kernels_sw_x2.hip -- the SW two-stream solver with two g-points per lane (packed fp32).
+//
+// Same algorithm, passes, workspace and ordered reductions as sw_2stream_kernel (kernels_rte.hip), but each
+// lane carries g-points 2i and 2i+1 as a two-wide vector: the per-layer arithmetic -- products, sums and the
+// fma chains of the correctly rounded reciprocal and square root -- issues as v_pk_mul_f32 / v_pk_add_f32 /
+// v_pk_fma_f32 (two IEEE operations each, so the same bits as the scalar kernel), loads and stores move 8
+// bytes per lane, and half as many lanes walk the column.  The glibc-exact exps (double precision), the IEEE
+// divisions and the selects stay per element.  Used when ngpt is even.
+#include "rte_device.hpp"
+
+namespace rrtmgpnn {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+namespace {
+
+__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 vmax(f2 a, f2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ f2 vmin(f2 a, f2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ f2 splat(float x) { return (f2){x, x}; }
+
+__device__ __forceinline__ f2 exp2v(f2 x, const uint64_t *etab)
+{
+  return (f2){ref_expf_nb(x.x, etab), ref_expf_nb(x.y, etab)};
+}
+
+// sqrt_rn_normal (libm_ref.hpp) with the correction fmas paired
+__device__ __forceinline__ f2 sqrt2(f2 x)
+{
+  const f2 s = (f2){__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  const f2 sm = (f2){__uint_as_float(__float_as_uint(s.x) - 1u), __uint_as_float(__float_as_uint(s.y) - 1u)};
+  const f2 sp = (f2){__uint_as_float(__float_as_uint(s.x) + 1u), __uint_as_float(__float_as_uint(s.y) + 1u)};
+  const f2 em = vfma(-sm, s, x), ep = vfma(-sp, s, x);
+  f2 r;
+  r.x = (ep.x > 0.0f) ? sp.x : ((em.x <= 0.0f) ? sm.x : s.x);
+  r.y = (ep.y > 0.0f) ? sp.y : ((em.y <= 0.0f) ? sm.y : s.y);
+  return r;
+}
+
+// rcp_rn_normal (libm_ref.hpp) with the Newton fmas paired
+__device__ __forceinline__ f2 rcp2(f2 b)
+{
+  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  const f2 one = splat(1.0f);
+  r = vfma(vfma(-b, r, one), r, r);
+  f2 q = r;
+  q = vfma(vfma(-b, q, one), r, q);
+  return vfma(vfma(-b, q, one), r, q);
+}
+
+struct SwDif2 {
+  f2 gamma1, gamma2, k, emk, em2k, RT, Rdif, Tdif;
+};
+
+__device__ __forceinline__ SwDif2 sw_dif2(f2 tau, f2 w0, f2 g, const uint64_t *etab)
+{
+  const float k_min = 1.e-4f;
+  SwDif2 d;
+  d.gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
+  d.gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
+  d.k = sqrt2(vmax((d.gamma1 - d.gamma2) * (d.gamma1 + d.gamma2), splat(k_min)));
+  d.emk = exp2v(-tau * d.k, etab);
+  d.em2k = d.emk * d.emk;
+  d.RT = rcp2(d.k * (1.0f + d.em2k) + d.gamma1 * (1.0f - d.em2k));
+  d.Rdif = d.RT * d.gamma2 * (1.0f - d.em2k);
+  d.Tdif = d.RT * 2.0f * d.k * d.emk;
+  return d;
+}
+
+struct SwCoef2 {
+  f2 Rdif, Tdif, Sup, Sdn;
+};
+
+// sw_two_stream of kernels_rte.hip, term by term
+__device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0, float mu0_inv, f2 dir_inc,
+                                                 const uint64_t *etab)
+{
+  const float eps = FLT_EPSILON;
+  SwCoef2 c;
+  const SwDif2 d = sw_dif2(tau, w0, g, etab);
+  const f2 gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
+  const f2 Tnoscat = exp2v(-tau * mu0_inv, etab);
+  const f2 gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
+  const f2 gamma4 = 1.0f - gamma3;
+  const f2 alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
+  const f2 alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
+  const f2 k2e = 2.0f * k * emk;
+  c.Rdif = d.Rdif;
+  c.Tdif = d.Tdif;
+  const f2 k_mu = k * mu0, k_mu2 = k_mu * k_mu, k_g3 = k * gamma3, k_g4 = k * gamma4;
+  const f2 omk = 1.0f - k_mu2;
+  f2 dd;
+  dd.x = (fabsf(omk.x) >= eps) ? omk.x : eps;
+  dd.y = (fabsf(omk.y) >= eps) ? omk.y : eps;
+  const f2 RT = w0 * d.RT / dd;
+  f2 Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
+                  k2e * (gamma3 - alpha2 * mu0) * Tnoscat);
+  f2 Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
+                  Tnoscat * ((1.0f + k_mu) * (alpha1 + k_g4) - (1.0f - k_mu) * (alpha1 - k_g4) * em2k));
+  Rdir = vmax(splat(0.0f), vmin(Rdir, (1.0f - Tnoscat)));
+  Tdir = vmax(splat(0.0f), vmin(Tdir, (1.0f - Tnoscat - Rdir)));
+  c.Sup = Rdir * dir_inc;
+  c.Sdn = Tdir * dir_inc;
+  return c;
+}
+
+// inc_2str of kernels_rte.hip for a pair
+__device__ __forceinline__ void inc_2str2(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, f2 g2)
+{
+  const float eps = 3.0f * FLT_MIN;
+  const f2 tau12 = t1 + t2;
+  const f2 tauscat12 = t1 * w1 + t2 * w2;
+  g1 = (t1 * w1 * g1 + t2 * w2 * g2) / vmax(splat(eps), tauscat12);
+  w1 = tauscat12 / vmax(splat(eps), tau12);
+  t1 = tau12;
+}
+
+// 8-byte column-local loads and stores (g-point pair at byte offset voff, layer at soff)
+struct ColArr2 {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ ColArr2(const float *base, size_t col_off, uint32_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void *)(base + col_off), 0, (int)bytes, 0x00020000)) {}
+  __device__ __forceinline__ f2 ld(uint32_t voff, uint32_t soff) const
+  {
+    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  }
+  __device__ __forceinline__ float ld1(uint32_t voff, uint32_t soff) const
+  {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+  }
+  __device__ __forceinline__ void st(f2 v, uint32_t voff, uint32_t soff) const
+  {
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, voff, soff, 0);
+  }
+};
+
+}  // namespace
+
+#ifndef RRTMGPNN_SW2_PF
+#define RRTMGPNN_SW2_PF 2
+#endif
+#ifndef RRTMGPNN_SW2_WAVES
+#define RRTMGPNN_SW2_WAVES 6
+#endif
+constexpr int kSw2Ring = 6;
+
+template <bool kHasG, bool kInc, int kPF>
+__global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
+    sw_2stream_x2_kernel(int ngpt, int nlay, int ncol, int top_at_1, const float *__restrict__ inc_flux,
+                         const float *__restrict__ inc_dif, const float *__restrict__ tau,
+                         const float *__restrict__ ssa, const float *__restrict__ gg, const float *__restrict__ mu0p,
+                         const float *__restrict__ alb_dir, const float *__restrict__ alb_dif, BandArgs bands,
+                         const float *__restrict__ tau_bnd, const float *__restrict__ ssa_bnd,
+                         const float *__restrict__ g_bnd, float *__restrict__ ws, float *__restrict__ flux_up,
+                         float *__restrict__ flux_dn, float *__restrict__ flux_dir)
+{
+  static_assert(kSw2Ring % kPF == 0, "prefetch depth must divide the ring");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int icol = blockIdx.x, g = 2 * threadIdx.x;  // this lane's g-points: g, g + 1
+  const bool on = g < ngpt;
+  const int nlev = nlay + 1;
+  float *ring = smem + kExpTabFloats;                // [3][kSw2Ring][ngpt]: up, dif, dir
+  uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
+  load_exp_table(etab);
+  __syncthreads();
+  float *part = ring + (size_t)3 * kSw2Ring * ngpt;  // [3][nlev][4]: up, dn, dir
+  const int gc = on ? g : ngpt - 2;
+  const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
+  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol, plane = (size_t)ngpt * nlev * ncol;
+  const ColArr2 Ttau(tau, cl, row * nlay), Tssa(ssa, cl, row * nlay), Tg(kHasG ? gg : tau, cl, row * nlay);
+  const ColArr2 WA(ws, cv, row * nlev), WB(ws + plane, cv, row * nlev), WS(ws + 2 * plane, cv, row * nlev),
+      WD(ws + 3 * plane, cv, row * nlev);
+  const size_t lplane = (size_t)ngpt * nlay * ncol;
+  float *wi = ws + 4 * plane;
+  const ColArr2 WT(wi, cl, row * nlay), WW(wi + lplane, cl, row * nlay), WG(wi + 2 * lplane, cl, row * nlay);
+  // band-resolved increments: one band offset per g-point of the pair
+  const size_t cb = (size_t)bands.nbnd * nlay * icol;
+  const uint32_t brow = 4u * (uint32_t)bands.nbnd;
+  const uint32_t vb0 = kInc ? 4u * (uint32_t)band_of(bands, gc) : 0u, vb1 = kInc ? 4u * (uint32_t)band_of(bands, gc + 1) : 0u;
+  const ColArr2 Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, brow * nlay), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, brow * nlay),
+      Bg(kInc ? g_bnd : tau, kInc ? cb : 0, brow * nlay);
+  auto ld_bnd = [&](const ColArr2 &a, int l) {
+    return kInc ? (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)} : splat(0.0f);
+  };
+  const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
+  auto lev_above = [&](int l) { return top_at_1 ? l : l + 1; };
+  auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
+  auto lay_of_down = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
+  auto lay_of_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
+  auto ld_g = [&](uint32_t soff) { return kHasG ? Tg.ld(vg, soff) : splat(0.0f); };
+  auto ld_col = [&](const float *p) { return on ? *(const f2 *)(p + gc + (size_t)ngpt * icol) : splat(0.0f); };
+  const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
+  const f2 Ftop = ld_col(inc_flux) * mu0;
+
+  // ---- pass 1: direct beam ----
+  f2 Fd = Ftop;
+  if (on) WA.st(Fd, vg, row * top);
+  {
+    f2 pt[kPF], pi[kPF];
+#pragma unroll
+    for (int p = 0; p < kPF; p++) {
+      const int l = lay_of_down(min(p, nlay - 1));
+      pt[p] = Ttau.ld(vg, row * l);
+      pi[p] = ld_bnd(Bt, l);
+    }
+    for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int j = j0 + p;
+        if (j < nlay) {
+          const int l = lay_of_down(j);
+          const f2 t = kInc ? pt[p] + pi[p] : pt[p];
+          {
+            const int ln = lay_of_down(min(j + kPF, nlay - 1));
+            pt[p] = Ttau.ld(vg, row * ln);
+            pi[p] = ld_bnd(Bt, ln);
+          }
+          Fd = exp2v(-t * mu0_inv, etab) * Fd;
+          if (on) WA.st(Fd, vg, row * lev_below(l));
+        }
+      }
+    }
+  }
+  // ---- pass 2: bottom -> top adding ----
+  f2 alb_b = ld_col(alb_dif);
+  f2 src_b = Fd * ld_col(alb_dir);
+  if (on) {
+    WB.st(alb_b, vg, row * sfcl);
+    WS.st(src_b, vg, row * sfcl);
+  }
+  {
+    f2 pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
+    auto load2 = [&](int p, int l) {
+      const uint32_t s = row * l;
+      pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(l));
+      if constexpr (kInc) {
+        qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < kPF; p++) load2(p, lay_of_up(min(p, nlay - 1)));
+    for (int j0 = 0; j0 < nlay; j0 += kPF) {
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int j = j0 + p;
+        if (j < nlay) {
+          const int l = lay_of_up(j);
+          f2 t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : splat(0.0f);
+          const f2 Fin = pf[p];
+          if constexpr (kInc) {
+            inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
+            if (on) {
+              WT.st(t, vg, row * l);
+              WW.st(w0, vg, row * l);
+              WG.st(g0, vg, row * l);
+            }
+          }
+          load2(p, lay_of_up(min(j + kPF, nlay - 1)));
+          const SwCoef2 c = sw_two_stream2(t, w0, g0, mu0, mu0_inv, Fin, etab);
+          const f2 denom = rcp2(1.0f - c.Rdif * alb_b);
+          const f2 alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
+          const f2 src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+          if (on) {
+            const uint32_t sa = row * lev_above(l);
+            WB.st(alb, vg, sa);
+            WS.st(src, vg, sa);
+            WD.st(c.Sdn, vg, row * l);
+          }
+          alb_b = alb;
+          src_b = src;
+        }
+      }
+    }
+  }
+  // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
+  auto put = [&](f2 up, f2 dif, f2 dir, int r) {
+    if (on) {
+      *(f2 *)&ring[(size_t)r * ngpt + g] = up;
+      *(f2 *)&ring[((size_t)kSw2Ring + r) * ngpt + g] = dif;
+      *(f2 *)&ring[((size_t)2 * kSw2Ring + r) * ngpt + g] = dir;
+    }
+  };
+  auto flush = [&](int n, int lev0, int dl) { ring_flush<kSw2Ring>(ring, part, 3, n, lev0, dl, ngpt, nlev, true); };
+  const int dl_dn = top_at_1 ? 1 : -1;
+  f2 Fdn = inc_dif ? ld_col(inc_dif) : splat(0.0f);
+  put(Fdn * alb_b + src_b, Fdn, Ftop, 0);
+  flush(1, top, 1);
+  {
+    f2 pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF];
+    auto load = [&](int p, int l) {
+      const uint32_t s = row * l, sb = row * lev_below(l);
+      if constexpr (kInc) {
+        pt[p] = WT.ld(vg, s); pw[p] = WW.ld(vg, s); pg[p] = WG.ld(vg, s);
+      } else {
+        pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s);
+      }
+      pd[p] = WD.ld(vg, s);
+      pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb); pf[p] = WA.ld(vg, sb);
+    };
+#pragma unroll
+    for (int p = 0; p < kPF; p++) load(p, lay_of_down(min(p, nlay - 1)));
+    for (int j0 = 0; j0 < nlay; j0 += kSw2Ring) {
+#pragma unroll
+      for (int r = 0; r < kSw2Ring; r++) {
+        const int j = j0 + r, p = r % kPF;
+        if (j < nlay) {
+          const f2 t = pt[p], w0 = pw[p], g0 = (kHasG || kInc) ? pg[p] : splat(0.0f);
+          const f2 Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
+          load(p, lay_of_down(min(j + kPF, nlay - 1)));
+          const SwDif2 d = sw_dif2(t, w0, g0, etab);
+          const f2 denom = rcp2(1.0f - d.Rdif * alb);
+          Fdn = (d.Tdif * Fdn + d.Rdif * src + Sdn) * denom;
+          const f2 up = Fdn * alb + src;
+          put(up, Fdn, Fdir, r);
+        }
+      }
+      flush(min(kSw2Ring, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
+    }
+  }
+  for (int l = threadIdx.x; l < nlev; l += blockDim.x) {
+    flux_up[l + (size_t)nlev * icol] = combine4(part + 4 * l);
+    flux_dn[l + (size_t)nlev * icol] = combine4(part + (size_t)nlev * 4 + 4 * l);
+    flux_dir[l + (size_t)nlev * icol] = combine4(part + (size_t)2 * nlev * 4 + 4 * l);
+  }
+}
+
+// ngpt even and <= 256; workspace as launch_sw_2stream's (the fused increment parks tau, ssa, g)
+int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                         const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
+                         const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
+                         const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
+                         float *flux_dn, float *flux_dir)
+{
+  const int threads = (ngpt / 2 + 63) / 64 * 64;
+  const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kSw2Ring * ngpt + (size_t)3 * (nlay + 1) * 4);
+  if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
+  const BandArgs nob{};
+  const BandArgs &b = bands ? *bands : nob;
+  const dim3 grid(ncol), block(threads);
+  constexpr int PF = RRTMGPNN_SW2_PF;
+  if (bands && g)
+    hipLaunchKernelGGL((sw_2stream_x2_kernel<true, true, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
+                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd,
+                       g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
+  else if (bands)
+    hipLaunchKernelGGL((sw_2stream_x2_kernel<false, true, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
+                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd,
+                       g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
+  else if (g)
+    hipLaunchKernelGGL((sw_2stream_x2_kernel<true, false, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
+                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, nullptr, nullptr,
+                       nullptr, (float *)ws, flux_up, flux_dn, flux_dir);
+  else
+    hipLaunchKernelGGL((sw_2stream_x2_kernel<false, false, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
+                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, nullptr, nullptr,
+                       nullptr, (float *)ws, flux_up, flux_dn, flux_dir);
+  RRTMGPNN_LAUNCH_CHECK("sw_2stream_x2_kernel");
+  return RRTMGPNN_OK;
+}
+
+}  // namespace rrtmgpnn

@@ -8,16 +8,18 @@ PKG=rte-rrtmgp-nn_amd
 B=${TMPDIR:-/tmp}/rrtmgpnn_var
 rm -rf $B; mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off"
-/opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/api.cpp -o $B/api.o &
-/opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/kernels_clouds.hip -o $B/clouds.o &
+# sources without tuning knobs are built once
+COMMON="api.cpp datafile.cpp kernels_clouds.hip kernels_lw_scat.hip"
+for f in $COMMON; do /opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/$f -o $B/common_${f%.*}.o & done
 names=()
 for spec in "$@"; do
   n=${spec%%:*}; d=${spec#*:}; names+=($n)
   /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_rte.hip -o $B/rte_$n.o &
   /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_nn.hip -o $B/nn_$n.o &
+  /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_sw_x2.hip -o $B/swx2_$n.o &
 done
 wait
 for n in "${names[@]}"; do
-  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/api.o $B/clouds.o $B/nn_$n.o $B/rte_$n.o
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/common_*.o $B/nn_$n.o $B/rte_$n.o $B/swx2_$n.o -ldl
 done
 python3 tools/solver_variants.py $B ${CONFIG:-c3} "${names[@]}"
