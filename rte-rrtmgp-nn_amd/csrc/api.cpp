@@ -14,6 +14,7 @@
 namespace rrtmgpnn {
 
 static thread_local std::string g_last_error;
+int g_sw_kernel_default = 0;
 
 void set_error(const std::string &msg) { g_last_error = msg; }
 
@@ -141,6 +142,18 @@ int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx)
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode)
+{
+  if (mode < 0 || mode > 2) return fail(RRTMGPNN_ERR_ARGUMENT, "sw kernel mode must be 0, 1 or 2");
+  if (!ctx) {
+    rrtmgpnn::g_sw_kernel_default = mode;
+    return RRTMGPNN_OK;
+  }
+  if (int rc = check_ctx(ctx)) return rc;
+  ctx->sw_kernel = mode;
   return RRTMGPNN_OK;
 }
 

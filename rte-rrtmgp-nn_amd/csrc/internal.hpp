@@ -32,6 +32,7 @@ int fail(int code, const std::string &msg);
 constexpr int kMaxLayers = 7;   // network layers (excluding input)
 constexpr int kMaxInputs = 32;  // NN input features
 constexpr int kMaxBands = 64;
+extern int g_sw_kernel_default;  // rrtmgpnn_context_set_sw_kernel(NULL, mode)
 
 }  // namespace rrtmgpnn
 
@@ -42,6 +43,7 @@ struct rrtmgpnn_context {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int num_cus = 256;
+  int sw_kernel = -1;  // SW two-stream kernel: 0 by problem size, 1 / 2 g-points per lane, -1 the library default
   void *ws = nullptr;
   size_t ws_bytes = 0;
   int workspace(size_t bytes, void **out);

@@ -145,7 +145,8 @@ static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
 #define RRTMGPNN_SW_INC_PARK 1
 #endif
 static constexpr bool kSwIncPark = RRTMGPNN_SW_INC_PARK != 0;
-// SW solver with two g-points per lane and packed fp32 (kernels_sw_x2.hip) whenever ngpt is even
+// SW solver with two g-points per lane and packed fp32 (kernels_sw_x2.hip) for even ngpt, when the context's
+// mode (rrtmgpnn_context_set_sw_kernel) or the problem size picks it; 0 compiles it out
 #ifndef RRTMGPNN_SW_X2
 #define RRTMGPNN_SW_X2 1
 #endif
@@ -713,7 +714,11 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
   const bool inc = bands != nullptr;
-  const bool x2 = kSwX2 && (ngpt % 2) == 0;  // two g-points per lane (kernels_sw_x2.hip)
+  // two g-points per lane (kernels_sw_x2.hip) halves the waves: worth it only once they still fill the chip
+  // (C4, 10k columns: -3 %), not at C3's 1800 columns (+5 %, the SW chain then starves the overlapped LW chain)
+  const long long x2_waves = (long long)ncol * ((ngpt / 2 + 63) / 64);
+  const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
+  const bool x2 = kSwX2 && (ngpt % 2) == 0 && (mode == 2 || (mode == 0 && x2_waves >= 8LL * 4 * ctx->num_cus));
   void *ws = nullptr;
   const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc && (kSwIncPark || x2) ? 3 * (size_t)ngpt * nlay * ncol : 0);
   int rc = ctx->workspace(sizeof(float) * nws, &ws);

@@ -68,7 +68,7 @@ __device__ __forceinline__ SwDif2 sw_dif2(f2 tau, f2 w0, f2 g, const uint64_t *e
 }
 
 struct SwCoef2 {
-  f2 Rdif, Tdif, Sup, Sdn;
+  f2 Rdif, Tdif, Sup, Sdn, Tnoscat;
 };
 
 // sw_two_stream of kernels_rte.hip, term by term
@@ -101,6 +101,7 @@ __device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0
   Tdir = vmax(splat(0.0f), vmin(Tdir, (1.0f - Tnoscat - Rdir)));
   c.Sup = Rdir * dir_inc;
   c.Sdn = Tdir * dir_inc;
+  c.Tnoscat = Tnoscat;
   return c;
 }
 
@@ -141,8 +142,16 @@ struct ColArr2 {
 #define RRTMGPNN_SW2_PF 2
 #endif
 #ifndef RRTMGPNN_SW2_WAVES
-#define RRTMGPNN_SW2_WAVES 6
+#define RRTMGPNN_SW2_WAVES 4
 #endif
+// Pass 3 recomputes the direct beam and the layer's full two-stream coefficients (S_dn included) instead of
+// reading them back: the workspace shrinks to the albedo and source planes (+ the direct beam pass 2 needs),
+// 3 fewer plane transfers per launch (the S_dn store + load, the beam's second read) for the ~250 VALU of a
+// second sw_two_stream per g-point and layer; measured even with the stored form (C3/C4, tools/sq_pmc.sh).
+#ifndef RRTMGPNN_SW2_RECOMP
+#define RRTMGPNN_SW2_RECOMP 1
+#endif
+constexpr bool kSw2Recomp = RRTMGPNN_SW2_RECOMP != 0;
 constexpr int kSw2Ring = 6;
 
 template <bool kHasG, bool kInc, int kPF>
@@ -265,7 +274,7 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
             const uint32_t sa = row * lev_above(l);
             WB.st(alb, vg, sa);
             WS.st(src, vg, sa);
-            WD.st(c.Sdn, vg, row * l);
+            if constexpr (!kSw2Recomp) WD.st(c.Sdn, vg, row * l);
           }
           alb_b = alb;
           src_b = src;
@@ -295,9 +304,13 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
       } else {
         pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s);
       }
-      pd[p] = WD.ld(vg, s);
-      pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb); pf[p] = WA.ld(vg, sb);
+      pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb);
+      if constexpr (!kSw2Recomp) {
+        pd[p] = WD.ld(vg, s);
+        pf[p] = WA.ld(vg, sb);
+      }
     };
+    f2 Fd3 = Ftop;  // kSw2Recomp: the direct beam again, top down, exactly as pass 1 formed it
 #pragma unroll
     for (int p = 0; p < kPF; p++) load(p, lay_of_down(min(p, nlay - 1)));
     for (int j0 = 0; j0 < nlay; j0 += kSw2Ring) {
@@ -306,11 +319,24 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
         const int j = j0 + r, p = r % kPF;
         if (j < nlay) {
           const f2 t = pt[p], w0 = pw[p], g0 = (kHasG || kInc) ? pg[p] : splat(0.0f);
-          const f2 Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
+          const f2 alb = pa[p], src = ps[p];
+          f2 Rdif, Tdif, Sdn = kSw2Recomp ? splat(0.0f) : pd[p], Fdir = kSw2Recomp ? splat(0.0f) : pf[p];
           load(p, lay_of_down(min(j + kPF, nlay - 1)));
-          const SwDif2 d = sw_dif2(t, w0, g0, etab);
-          const f2 denom = rcp2(1.0f - d.Rdif * alb);
-          Fdn = (d.Tdif * Fdn + d.Rdif * src + Sdn) * denom;
+          if constexpr (kSw2Recomp) {
+            // pass 2's coefficients from the same inputs (same bits), the beam from pass 1's recurrence
+            const SwCoef2 c = sw_two_stream2(t, w0, g0, mu0, mu0_inv, Fd3, etab);
+            Rdif = c.Rdif;
+            Tdif = c.Tdif;
+            Sdn = c.Sdn;
+            Fd3 = c.Tnoscat * Fd3;
+            Fdir = Fd3;
+          } else {
+            const SwDif2 d = sw_dif2(t, w0, g0, etab);
+            Rdif = d.Rdif;
+            Tdif = d.Tdif;
+          }
+          const f2 denom = rcp2(1.0f - Rdif * alb);
+          Fdn = (Tdif * Fdn + Rdif * src + Sdn) * denom;
           const f2 up = Fdn * alb + src;
           put(up, Fdn, Fdir, r);
         }

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "librrtmgpnn.so"))
+# RRTMGPNN_LIB: another build of the same library (tools/solver_variants.sh variants under a profiler)
+LIB_PATH = os.environ.get("RRTMGPNN_LIB") or os.path.normpath(os.path.join(_HERE, "..", "librrtmgpnn.so"))
 
 c_int, c_float, c_ll, c_vp, c_char_p = ctypes.c_int, ctypes.c_float, ctypes.c_longlong, ctypes.c_void_p, ctypes.c_char_p
 P = ctypes.POINTER
@@ -20,6 +21,7 @@ SIGNATURES = {
     "rrtmgpnn_context_create": (c_int, [c_int, c_vp, P(c_vp)]),
     "rrtmgpnn_context_destroy": (c_int, [c_vp]),
     "rrtmgpnn_context_set_stream": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_context_set_sw_kernel": (c_int, [c_vp, c_int]),
     "rrtmgpnn_context_stream": (c_vp, [c_vp]),
     "rrtmgpnn_context_synchronize": (c_int, [c_vp]),
     "rrtmgpnn_malloc": (c_int, [c_vp, c_ll, P(c_vp)]),

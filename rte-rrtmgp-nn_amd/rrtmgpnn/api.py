@@ -55,12 +55,22 @@ class Context:
     def synchronize(self):
         check(_lib.lib().rrtmgpnn_context_synchronize(self.h), "context_synchronize")
 
+    def set_sw_kernel(self, mode):
+        """0: SW two-stream kernel by problem size (default); 1 / 2: one / two g-points per lane (bit-identical)."""
+        check(_lib.lib().rrtmgpnn_context_set_sw_kernel(self.h, int(mode)), "context_set_sw_kernel")
+
     def __del__(self):
         try:
             if getattr(self, "h", None):
                 _lib.lib().rrtmgpnn_context_destroy(self.h)
         except Exception:
             pass
+
+
+def set_sw_kernel_default(mode):
+    """The SW two-stream kernel of every context not set itself: 0 by problem size (the default), 1 / 2 one /
+    two g-points per lane (bit-identical fluxes; tests force each)."""
+    check(_lib.lib().rrtmgpnn_context_set_sw_kernel(None, int(mode)), "context_set_sw_kernel")
 
 
 def context(device=None):

@@ -202,7 +202,7 @@ def _allsky_prob(rfmip, ncol):
 
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("lut", [True, False])
-def test_allsky_step_bitwise_vs_oracle(dev, orc, rfmip, fused, lut):
+def test_allsky_step_bitwise_vs_oracle(dev, orc, rfmip, fused, lut, sw_kernel):
     from rrtmgpnn import data
     from rrtmgpnn.pipeline import ClearSkyStep
     prob = _allsky_prob(rfmip, 240)
@@ -254,7 +254,7 @@ def test_allsky_graph_replay_matches_eager(dev, rfmip):
 
 @pytest.mark.parametrize("top_at_1", [True, False])
 @pytest.mark.parametrize("nmus", [1, 3])
-def test_fused_increment_solvers_match_increment_then_solve(dev, rfmip, top_at_1, nmus):
+def test_fused_increment_solvers_match_increment_then_solve(dev, rfmip, top_at_1, nmus, sw_kernel):
     """rrtmgpnn_{lw_solver_noscat_planck,sw_solver_2stream}_inc == increment_bybnd followed by the plain solver,
     bit for bit, in both orientations (and for LW with several angles); the inputs are left untouched."""
     from rrtmgpnn import _lib, data

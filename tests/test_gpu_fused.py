@@ -68,7 +68,7 @@ def test_fused_lw_solver_matches_oracle(dev, orc, rfmip, nmus, top_at_1):
 
 
 @pytest.mark.parametrize("top_at_1", [True, False])
-def test_sw_null_g_equals_zero_g(dev, top_at_1):
+def test_sw_null_g_equals_zero_g(dev, top_at_1, sw_kernel):
     from rrtmgpnn import _lib
     from rrtmgpnn._lib import check
     from rrtmgpnn.api import context

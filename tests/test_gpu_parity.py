@@ -148,7 +148,7 @@ def test_lw_solver_matches_oracle(dev, orc, nmus, top_at_1):
 
 
 @pytest.mark.parametrize("flip", [False, True])
-def test_sw_solver_matches_reference_fixture(dev, flip):
+def test_sw_solver_matches_reference_fixture(dev, flip, sw_kernel):
     from rrtmgpnn import api, rbin
     import os
     g = rbin.read(os.path.join(os.path.dirname(__file__), "golden", "rfmip8_reference.rbin"))
@@ -171,7 +171,7 @@ def test_sw_solver_matches_reference_fixture(dev, flip):
     assert_flux(fl.flux_dn_dir.cpu().numpy(), g["sw_flux_dir" + suf], "sw dir")
 
 
-def test_sw_solver_with_scattering_and_diffuse_inc(dev, orc):
+def test_sw_solver_with_scattering_and_diffuse_inc(dev, orc, sw_kernel):
     """g != 0 and a diffuse incident flux exercise branches the clear-sky NN path never reaches."""
     from rrtmgpnn import api
     rng = np.random.default_rng(5)
@@ -219,7 +219,7 @@ def _check_pipeline(got, ref, usecol):
         assert_flux(g, r, k)
 
 
-def test_full_rfmip_clear_sky_lw_sw(dev, orc, rfmip, models):
+def test_full_rfmip_clear_sky_lw_sw(dev, orc, rfmip, models, sw_kernel):
     """C3 (all 1800 RFMIP columns): the benchmarked step vs the oracle, plus heating-rate agreement."""
     from rrtmgpnn.pipeline import ClearSkyStep
     step = ClearSkyStep(rfmip, device=0)
@@ -282,7 +282,7 @@ def test_sw_tsi_linearity(dev, rfmip):
 
 
 @pytest.mark.parametrize("nlay,ncol", [(2, 3), (137, 50), (60, 1)])
-def test_pipeline_shapes_vs_oracle(dev, orc, models, nlay, ncol):
+def test_pipeline_shapes_vs_oracle(dev, orc, models, nlay, ncol, sw_kernel):
     from rrtmgpnn import data
     from rrtmgpnn.pipeline import ClearSkyStep
     if nlay == 60:

@@ -2,6 +2,8 @@
 # Bench + rocprofv3 kernel-trace summary + PMC HBM traffic for each config given (default: c3 c4), one GPU box call.
 # Each config's artefacts land in gpurun_out/<config>/; PMC traffic is merged into gpurun_out/pmc_traffic.json.
 # Stops at the first failing GPU step (every step has its own time limit).
+# The kernel trace runs with --no-overlap: bench.py times each stage alone on its stream, and per-kernel durations
+# only agree with those when the LW and SW chains do not share the chip (overlapped, both stretch).
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -13,7 +15,7 @@ for cfg in ${CONFIGS:-c3 c4}; do
   timeout -k 10 300 python bench.py --config $cfg --steps $STEPS --warmup 5 ${BENCH_ARGS:-} > $o/bench.json 2> $o/bench.err || exit $?
   head -c 400 $o/bench.json; echo
   echo "== $cfg rocprofv3 kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --no-overlap ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg rocprofv3 --pmc $c"
     timeout -k 10 300 rocprofv3 --pmc $c -d $o/pmc_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > $o/pmc_$c.log 2>&1 || exit $?

@@ -81,5 +81,7 @@ for v in names:
     if first is None:
         first, same = res, "ref"
     else:
-        same = "bitwise" if all(np.array_equal(x, y) for x, y in zip(res, first)) else "DIFFERS"
+        bad = [(i, float(np.nanmax(np.abs(x - y)))) for i, (x, y) in enumerate(zip(res, first))
+               if not np.array_equal(x, y)]
+        same = "bitwise" if not bad else "DIFFERS " + ",".join("%d:%.2g" % b for b in bad)
     print("%-10s [%s] " % (v, same) + " | ".join(line), flush=True)

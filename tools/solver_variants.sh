@@ -22,4 +22,4 @@ wait
 for n in "${names[@]}"; do
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $B/lib_$n.so $B/common_*.o $B/nn_$n.o $B/rte_$n.o $B/swx2_$n.o -ldl
 done
-python3 tools/solver_variants.py $B ${CONFIG:-c3} "${names[@]}"
+[ -n "${BUILD_ONLY:-}" ] || python3 tools/solver_variants.py $B ${CONFIG:-c3} "${names[@]}"
