@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
                     help="auto: the reference's own Fortran (oracle/_ref) when built, else the C restatement")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "pmc_sq.json"),
+                    help="committed SQ counters per config/stage (tools/profile_configs.sh): valu_busy")
     return ap.parse_args()
 
 
@@ -212,6 +214,11 @@ def main():
             best = (name, kind, amount)
     roof = None
     stage_roofs = {}
+    try:  # share of the chip's VALU issue slots each stage used, from the committed SQ counter pass
+        with open(args.sq_json) as f:
+            sq = json.load(f).get(args.config, {})
+    except (OSError, ValueError):
+        sq = {}
     for name, ms in stages.items():
         kind, amount, k2, a2 = stage_work(name, step)
         if amount <= 0:
@@ -224,6 +231,8 @@ def main():
         else:
             ach = amount / (ms * 1e-3) / 1e9
             stage_roofs[name] = {"bound": "hbm", "achieved_gbs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)}
+        if sq.get(name, {}).get("valu_busy") is not None:
+            stage_roofs[name]["valu_busy"] = sq[name]["valu_busy"]
     if best is not None:
         name, kind, amount = best
         ms = stages[name]
@@ -248,6 +257,10 @@ def main():
             roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_per_launch": amount,
                     "avg_launch_ms": round(ms, 4)}
+            if traffic:
+                roof["actual_gbs"] = round(traffic / (ms * 1e-3) / 1e9, 1)  # PMC bytes / launch time
+        if roof is not None and sq.get(name, {}).get("valu_busy") is not None:
+            roof["valu_busy"] = sq[name]["valu_busy"]  # the solvers' binding limit: VALU issue
 
     # ---- final flux all-gather over RCCL (outside the timed region) ----
     gather_ms = None

@@ -1,6 +1,7 @@
 #!/bin/bash
-# Bench + rocprofv3 kernel-trace summary + PMC HBM traffic for each config given (default: c3 c4), one GPU box call.
-# Each config's artefacts land in gpurun_out/<config>/; PMC traffic is merged into gpurun_out/pmc_traffic.json.
+# Bench + rocprofv3 kernel-trace summary + PMC HBM traffic + SQ issue counters for each config given (default: c3 c4),
+# one GPU box call.  Each config's artefacts land in gpurun_out/<config>/; PMC traffic is merged into
+# gpurun_out/pmc_traffic.json, the SQ counters (valu_busy etc.) into gpurun_out/pmc_sq.json.
 # Stops at the first failing GPU step (every step has its own time limit).
 # The kernel trace runs with --no-overlap: bench.py times each stage alone on its stream, and per-kernel durations
 # only agree with those when the LW and SW chains do not share the chip (overlapped, both stretch).
@@ -8,12 +9,10 @@ set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 STEPS=${STEPS:-30}
+SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
 for cfg in ${CONFIGS:-c3 c4}; do
   o=gpurun_out/$cfg
   mkdir -p $o
-  echo "== $cfg bench"
-  timeout -k 10 300 python bench.py --config $cfg --steps $STEPS --warmup 5 ${BENCH_ARGS:-} > $o/bench.json 2> $o/bench.err || exit $?
-  head -c 400 $o/bench.json; echo
   echo "== $cfg rocprofv3 kernel trace"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --no-overlap ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
   for c in FETCH_SIZE WRITE_SIZE; do
@@ -21,5 +20,12 @@ for cfg in ${CONFIGS:-c3 c4}; do
     timeout -k 10 300 rocprofv3 --pmc $c -d $o/pmc_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > $o/pmc_$c.log 2>&1 || exit $?
   done
   python3 tools/pmc_traffic.py $o/pmc_FETCH_SIZE $o/pmc_WRITE_SIZE $cfg gpurun_out/pmc_traffic.json > $o/pmc_traffic.txt || exit $?
+  echo "== $cfg rocprofv3 --pmc SQ counters"
+  timeout -k 10 300 rocprofv3 --pmc $SQ -d $o/pmc_SQ -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > $o/pmc_SQ.log 2>&1 || exit $?
+  python3 tools/pmc_counters.py $o/pmc_SQ gpurun_out/pmc_sq.json $cfg > $o/pmc_sq.txt || exit $?
+  # the bench line last, so its roofline carries this build's PMC traffic and SQ figures
+  echo "== $cfg bench"
+  timeout -k 10 300 python bench.py --config $cfg --steps $STEPS --warmup 5 --traffic-json gpurun_out/pmc_traffic.json --sq-json gpurun_out/pmc_sq.json ${BENCH_ARGS:-} > $o/bench.json 2> $o/bench.err || exit $?
+  head -c 400 $o/bench.json; echo
 done
 exit 0

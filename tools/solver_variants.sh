@@ -14,7 +14,7 @@ for f in $COMMON; do /opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/$f -o $B/com
 names=()
 for spec in "$@"; do
   n=${spec%%:*}; d=${spec#*:}; names+=($n)
-  /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_rte.hip -o $B/rte_$n.o &
+  /opt/rocm/bin/hipcc $FLAGS -fno-slp-vectorize $d -x hip -c $PKG/csrc/kernels_rte.hip -o $B/rte_$n.o &  # as the Makefile
   /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_nn.hip -o $B/nn_$n.o &
   /opt/rocm/bin/hipcc $FLAGS $d -x hip -c $PKG/csrc/kernels_sw_x2.hip -o $B/swx2_$n.o &
 done
