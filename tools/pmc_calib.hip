@@ -78,7 +78,51 @@ __global__ void __launch_bounds__(256) column_kernel(float *__restrict__ a, int 
   if (s == 12345.678f) out[0] = s;
 }
 
+// VALU issue calibration: 8 independent fma chains per lane, NIT iterations (8 * NIT v_fma per wave, no memory).
+// Built with -fno-slp-vectorize so float stays v_fma_f32; pk2 (two floats per value) is v_pk_fma_f32.
+typedef float pk2 __attribute__((ext_vector_type(2)));
+template <typename T, typename S>
+__global__ void __launch_bounds__(256) fma_kernel(S *__restrict__ out, int nit, S a_, S b_)
+{
+  const T a = a_, b = b_;
+  T x0 = (S)threadIdx.x, x1 = x0 + (S)1, x2 = x0 + (S)2, x3 = x0 + (S)3, x4 = x0 + (S)4, x5 = x0 + (S)5,
+    x6 = x0 + (S)6, x7 = x0 + (S)7;
+  for (int i = 0; i < nit; i++) {
+    x0 = x0 * a + b; x1 = x1 * a + b; x2 = x2 * a + b; x3 = x3 * a + b;
+    x4 = x4 * a + b; x5 = x5 * a + b; x6 = x6 * a + b; x7 = x7 * a + b;
+  }
+  const T s = ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + (x6 + x7));
+  if constexpr (sizeof(T) == sizeof(S)) {
+    if (s == (S)12345.678) out[0] = s;
+  } else {
+    if (s.x == (S)12345.678) out[0] = s.x + s.y;
+  }
+}
+
 extern "C" {
+// returns the kernel time in ms (hipEvents); dbl: v_fma_f64 instead of v_fma_f32
+// returns the kernel time in ms (hipEvents); kind 0 v_fma_f32, 1 v_fma_f64, 2 v_pk_fma_f32
+float calib_fma(int kind, void *out, int blocks, int nit)
+{
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  if (kind == 1)
+    hipLaunchKernelGGL((fma_kernel<double, double>), dim3(blocks), dim3(256), 0, 0, (double *)out, nit, 0.999, 1e-3);
+  else if (kind == 2)
+    hipLaunchKernelGGL((fma_kernel<pk2, float>), dim3(blocks), dim3(256), 0, 0, (float *)out, nit, 0.999f, 1e-3f);
+  else
+    hipLaunchKernelGGL((fma_kernel<float, float>), dim3(blocks), dim3(256), 0, 0, (float *)out, nit, 0.999f, 1e-3f);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.0f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms;
+}
+
 int calib_read(int width, const void *in, size_t bytes, float *out)
 {
   const dim3 grid(4096), block(256);

@@ -3,6 +3,8 @@
 
 usage: pmc_calib.py run <lib.so>                  (the GPU program: run it under rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE)
        pmc_calib.py parse <fetch_dir> <write_dir> [out.json]
+       pmc_calib.py valu <lib.so>                 (fma_kernel<float/double>: run under rocprofv3 --pmc SQ_* counters;
+                                                   prints the hipEvent times and v_fma rates)
 Prints, per calibration kernel, counter bytes (KiB * 1024, no correction) / true bytes moved.  Buffers exceed the
 256 MiB Infinity Cache so the counted traffic is HBM traffic (MI355X_MICROARCH.md, HBM and L3 sections).
 """
@@ -73,8 +75,30 @@ def parse(fdir, wdir, out=None):
             fh.write(txt)
 
 
+FMA_BLOCKS, FMA_NIT = 256 * 16, 4096
+
+
+def valu(lib):
+    import torch
+    L = ctypes.CDLL(lib)
+    L.calib_fma.restype = ctypes.c_float
+    out = torch.zeros(2, dtype=torch.float64, device="cuda")
+    res = {}
+    for kind, name, per in ((0, "v_fma_f32", 1), (1, "v_fma_f64", 1), (2, "v_pk_fma_f32", 2)):
+        L.calib_fma(kind, ctypes.c_void_p(out.data_ptr()), FMA_BLOCKS, 16)  # warm
+        ms = L.calib_fma(kind, ctypes.c_void_p(out.data_ptr()), FMA_BLOCKS, FMA_NIT)
+        waves = FMA_BLOCKS * 4
+        insts = 8 * FMA_NIT * waves
+        res[name] = {"ms": round(ms, 4), "wave_insts": insts, "cycles_per_inst_per_simd_at_2.4GHz":
+                     round(ms * 1e-3 * 2.4e9 * 1024 / insts, 2),
+                     "tflops": round(2 * 64 * per * insts / (ms * 1e-3) / 1e12, 1)}
+    print(json.dumps(res))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2])
+    elif sys.argv[1] == "valu":
+        valu(sys.argv[2])
     else:
         parse(*sys.argv[2:])
