@@ -193,7 +193,7 @@ __device__ __forceinline__ float act_out(int act, float x)
 //   K1S = ceil(nx/4), H1T = ceil(h1/16), H2T = ceil(h2/16), NGT = ceil(ny/16)
 //   L1 [H1T][K1S][64]        lane(i,q): W1[k=4t+q][u(i)]         u(i) = 16mo + 4(i&3) + (i>>2)
 //   L2 [H2T][4*H1T][64]      lane(i,q): W2[k=16m+4t+q][u(i)]
-//   L3 [NGT][4*H2T][64]      lane(j,q): W3[k=16m+4t+q][g=16go+j]
+//   L3 [NGT][4*H2T][64]      lane(i,q): W3[k=16m+4t+q][g=16go+i]   (the A operand: rows are g-points)
 //   B1 [H1T*16], B2 [H2T*16] bias by PHYSICAL row R: b[16m + 4(R&3) + (R>>2)]
 //   B3, STD, MEAN [NGT*16]   by g
 // ------------------------------------------------------------------------------------------
@@ -281,6 +281,7 @@ struct MlpArgs {
   int ngpt;    // g-points of the physical outputs
   int ngt;     // output g-tiles per network (NGT)
   int imgA_floats, imgB_floats;
+  int vec4;    // outputs may be stored 16 bytes at a time (ngpt % 4 == 0, 16-byte aligned arrays)
   int actA[3], actB[3];
   long long nbatch;
 };
@@ -333,7 +334,7 @@ __device__ __forceinline__ floatx4 mlp_out_tile(const float *__restrict__ img, i
   for (int m = 0; m < H2T; m++)
 #pragma unroll
     for (int t = 0; t < 4; t++)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(h2[m][t], img[l3 + (go * 4 * H2T + 4 * m + t) * 64 + lane], acc, 0, 0,
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(img[l3 + (go * 4 * H2T + 4 * m + t) * 64 + lane], h2[m][t], acc, 0, 0,
                                                  0);
   return acc;
 }
@@ -387,97 +388,107 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
       static_assert(BK == AK, "paired networks share their inputs");
       mlp_hidden<BK, BH1, BH2, ACTS>(imgB, NGT, xv, lane, a.actB[0], a.actB[1], hB);
     }
-    // Per-lane sample rows of the output tile: s = s0 + 4q + r
-    float cd[4];
-    if constexpr (MODE != MLP_PLAIN && MODE != MLP_LW_BOTH) {
+    // Layer 3 runs with the weights as the A operand (rows = g-points) and the hidden activations as B
+    // (columns = samples): lane (j, q) holds g = 16go + 4q + r, r = 0..3, of sample s0 + j, so each lane
+    // stores 16 contiguous bytes per output array.  Same k-ordered chains as the oracle, same bits.
+    const long long s = s0 + j;
+    const bool sok = s < a.nbatch;
+    float cd = 0.0f;
+    if constexpr (MODE != MLP_PLAIN) cd = sok ? a.col_dry[s] : 0.0f;
+    // 4 consecutive g of one sample: one 16-byte store when the row allows it, else element by element
+    auto put4 = [&](float *out, int row, int gc, const floatx4 &v) {
+      if (!sok) return;
+      float *p = out + (size_t)s * row + gc;
+      if (a.vec4 && gc + 3 < row) {
+        *(floatx4 *)p = v;
+      } else {
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        long long s = s0 + 4 * q + r;
-        cd[r] = s < a.nbatch ? a.col_dry[s] : 0.0f;
+        for (int r = 0; r < 4; r++)
+          if (gc + r < row) p[r] = v[r];
       }
-    } else if constexpr (MODE == MLP_LW_BOTH) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        long long s = s0 + 4 * q + r;
-        cd[r] = s < a.nbatch ? a.col_dry[s] : 0.0f;
-      }
-    }
+    };
 #pragma unroll kGoUnroll
     for (int go = 0; go < NGT; go++) {
-      const int g = 16 * go + j;
-      floatx4 yA = mlp_out_tile<AH2>(imgA, LA.l3, go, hA, lane);
-      const float bA = imgA[LA.b3 + g];
+      const int g0 = 16 * go + 4 * q;
+      const floatx4 yA = mlp_out_tile<AH2>(imgA, LA.l3, go, hA, lane);
+      const floatx4 bA = *(const floatx4 *)&imgA[LA.b3 + g0];
       if constexpr (MODE == MLP_PLAIN) {
-        const int ny = ngpt;
+        floatx4 o;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          long long s = s0 + 4 * q + r;
-          if (s < a.nbatch && g < ny) a.out0[(size_t)s * ny + g] = act_out<ACTS>(a.actA[2], yA[r] + bA);
-        }
+        for (int r = 0; r < 4; r++) o[r] = act_out<ACTS>(a.actA[2], yA[r] + bA[r]);
+        put4(a.out0, ngpt, g0, o);
       } else if constexpr (MODE == MLP_LW_BOTH) {
         // single model, outputs [0,ngpt) -> tau, [ngpt, 2 ngpt) -> pfrac (mo_gas_optics_kernels.F90:754-766)
-        const float sd = imgA[LA.sd + g], mn = imgA[LA.mn + g];
+        const floatx4 sd = *(const floatx4 *)&imgA[LA.sd + g0], mn = *(const floatx4 *)&imgA[LA.mn + g0];
+        floatx4 tau, pf;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-          long long s = s0 + 4 * q + r;
-          if (s >= a.nbatch) continue;
-          float y = yA[r] + bA;
-          if (g < ngpt) {
-            float t = sd * y;
-            t = t + mn;
-            a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];
-          } else if (g < 2 * ngpt) {
-            a.out1[(size_t)s * ngpt + (g - ngpt)] = y * y;
+          const float y = yA[r] + bA[r];
+          float t = sd[r] * y;
+          t = t + mn[r];
+          tau[r] = pow8(t) * cd;
+          pf[r] = y * y;
+        }
+        if (a.vec4 && g0 + 3 < ngpt) {
+          put4(a.out0, ngpt, g0, tau);
+        } else if (a.vec4 && g0 >= ngpt) {
+          put4(a.out1, ngpt, g0 - ngpt, pf);
+        } else if (sok) {  // a 4-group straddling the tau / pfrac boundary or the end
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int g = g0 + r;
+            if (g < ngpt) a.out0[(size_t)s * ngpt + g] = tau[r];
+            else if (g < 2 * ngpt) a.out1[(size_t)s * ngpt + (g - ngpt)] = pf[r];
           }
         }
       } else {
-        const float sdA = imgA[LA.sd + g], mnA = imgA[LA.mn + g];
+        const floatx4 sdA = *(const floatx4 *)&imgA[LA.sd + g0], mnA = *(const floatx4 *)&imgA[LA.mn + g0];
         if constexpr (MODE == MLP_SW_ABS) {
+          floatx4 tau;
 #pragma unroll
           for (int r = 0; r < 4; r++) {
-            long long s = s0 + 4 * q + r;
-            if (s >= a.nbatch || g >= ngpt) continue;
-            float t = sdA * (yA[r] + bA);
-            t = t + mnA;
-            a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];
+            float t = sdA[r] * (yA[r] + bA[r]);
+            t = t + mnA[r];
+            tau[r] = pow8(t) * cd;
           }
+          put4(a.out0, ngpt, g0, tau);
         } else {
-          floatx4 yB = mlp_out_tile<BH2>(imgB, LB.l3, go, hB, lane);
-          const float bB = imgB[LB.b3 + g];
+          const floatx4 yB = mlp_out_tile<BH2>(imgB, LB.l3, go, hB, lane);
+          const floatx4 bB = *(const floatx4 *)&imgB[LB.b3 + g0];
           if constexpr (MODE == MLP_LW_PAIR) {
+            floatx4 tau, pf;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-              long long s = s0 + 4 * q + r;
-              if (s >= a.nbatch || g >= ngpt) continue;
-              float t = sdA * (yA[r] + bA);
-              t = t + mnA;
-              float p = yB[r] + bB;
-#ifdef RRTMGPNN_ABL_MLP_NOSTORE  // ablation only: stores skipped unless the value is a nan
-              if (t != t || p != p) {
-#else
-              {
+              float t = sdA[r] * (yA[r] + bA[r]);
+              t = t + mnA[r];
+              const float p = yB[r] + bB[r];
+              tau[r] = pow8(t) * cd;
+              pf[r] = p * p;
+            }
+#ifdef RRTMGPNN_ABL_MLP_NOSTORE  // ablation only: stores skipped unless a value is a nan
+            if (tau[0] != tau[0] || pf[0] != pf[0])
 #endif
-                a.out0[(size_t)s * ngpt + g] = pow8(t) * cd[r];  // tau
-                a.out1[(size_t)s * ngpt + g] = p * p;            // pfrac
-              }
+            {
+              put4(a.out0, ngpt, g0, tau);  // tau
+              put4(a.out1, ngpt, g0, pf);   // pfrac
             }
           } else {  // MLP_SW_PAIR
-            const float sdB = imgB[LB.sd + g], mnB = imgB[LB.mn + g];
+            const floatx4 sdB = *(const floatx4 *)&imgB[LB.sd + g0], mnB = *(const floatx4 *)&imgB[LB.mn + g0];
+            floatx4 tot, ssa;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-              long long s = s0 + 4 * q + r;
-              if (s >= a.nbatch || g >= ngpt) continue;
-              float ta = sdA * (yA[r] + bA);
-              ta = ta + mnA;
-              float vabs = pow8(ta) * cd[r];
-              float tr = sdB * (yB[r] + bB);
-              tr = tr + mnB;
-              float vray = pow8(tr) * cd[r];
-              float tot = vabs + vray;
-              a.out0[(size_t)s * ngpt + g] = tot;          // tau = tau_abs + tau_ray
-              a.out1[(size_t)s * ngpt + g] = vray / tot;   // ssa
-              if (a.out2) a.out2[(size_t)s * ngpt + g] = 0.0f;  // g
+              float ta = sdA[r] * (yA[r] + bA[r]);
+              ta = ta + mnA[r];
+              const float vabs = pow8(ta) * cd;
+              float tr = sdB[r] * (yB[r] + bB[r]);
+              tr = tr + mnB[r];
+              const float vray = pow8(tr) * cd;
+              tot[r] = vabs + vray;
+              ssa[r] = vray / tot[r];
             }
+            put4(a.out0, ngpt, g0, tot);  // tau = tau_abs + tau_ray
+            put4(a.out1, ngpt, g0, ssa);  // ssa
+            if (a.out2) put4(a.out2, ngpt, g0, floatx4{0.0f, 0.0f, 0.0f, 0.0f});  // g
           }
         }
       }
@@ -555,6 +566,8 @@ int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, c
   a.imgA = A->d_packed; a.imgA_floats = A->packed_floats;
   a.imgB = paired ? B->d_packed : nullptr; a.imgB_floats = paired ? B->packed_floats : 0;
   a.nx = A->dims[0]; a.ngpt = ngpt; a.ngt = A->ngt; a.nbatch = nbatch;
+  auto al16 = [](const float *p) { return ((uintptr_t)p & 15) == 0; };
+  a.vec4 = (ngpt % 4 == 0) && al16(out0) && (!out1 || al16(out1)) && (!out2 || al16(out2));
   for (int i = 0; i < 3; i++) { a.actA[i] = A->act[i]; a.actB[i] = paired ? B->act[i] : 0; }
 
 #define TRY_PAIR(AK, AH1, AH2, BK, BH1, BH2, MODE) \
