@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
+    ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2],
+                    help="SW solver: 0 the library's choice, 1 / 2 g-points per lane (rrtmgpnn_context_set_sw_kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
@@ -134,6 +136,9 @@ def main():
         prob = data.synthetic_problem(125000, 137, seed=20251015 + rank)
         workload = "C5 shard: 125000 synthetic columns x 137 layers per GPU, clear-sky LW+SW"
         data_desc = "synthetic columns interpolated from RFMIP profiles (PCG64 seed 20251015+rank)"
+    if args.sw_kernel:
+        from rrtmgpnn import api
+        api.set_sw_kernel_default(args.sw_kernel)
     step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap)
     ncol, nlay = step.ncol, step.nlay
 

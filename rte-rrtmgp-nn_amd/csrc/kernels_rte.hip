@@ -298,8 +298,8 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
               pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
               pi[p] = ld_inc(ln);
             }
-            const float T = ref_expf_nb(-t, etab);
-            const float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+            const float T = solver_exp_neg(-t, etab);
+            const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
             const float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
             I = T * I + S;
             put(fac * I, r, 0, top_at_1 ? l + 1 : l, acc);
@@ -336,8 +336,8 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
               pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pi[p] = ld_inc(ln);
               if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * ln);
             }
-            const float T = ref_expf_nb(-t, etab);
-            const float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
+            const float T = solver_exp_neg(-t, etab);
+            const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
             const float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
             U = T * U + S;
             put(fac * U, r, 1, top_at_1 ? l : l + 1, acc);
@@ -449,7 +449,7 @@ __device__ __forceinline__ SwDif sw_dif(float tau, float w0, float g, const uint
   d.gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
   d.gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
   d.k = sqrt_rn_normal(fmaxf((d.gamma1 - d.gamma2) * (d.gamma1 + d.gamma2), k_min));
-  d.emk = ref_expf_nb(-tau * d.k, etab);
+  d.emk = solver_exp_neg(-tau * d.k, etab);
   d.em2k = d.emk * d.emk;
   d.RT = rcp_rn_normal(d.k * (1.0f + d.em2k) + d.gamma1 * (1.0f - d.em2k));
   d.Rdif = d.RT * d.gamma2 * (1.0f - d.em2k);
@@ -461,6 +461,8 @@ struct SwCoef {
   float Rdif, Tdif, Sup, Sdn, Tnoscat;
 };
 
+// kG0: g is the literal 0 (the NN path), so gamma3 = (2 - 3 mu0 0)/4 = 0.5 and gamma4 = 0.5 exactly (mu0 finite).
+template <bool kG0 = false>
 __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, float mu0, float mu0_inv, float dir_inc,
                                                const uint64_t *etab)
 {
@@ -468,8 +470,8 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   SwCoef c;
   const SwDif d = sw_dif(tau, w0, g, etab);
   const float gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
-  float Tnoscat = ref_expf_nb(-tau * mu0_inv, etab);
-  float gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
+  float Tnoscat = solver_exp_neg(-tau * mu0_inv, etab);
+  float gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? 0.5f : (2.0f - 3.0f * mu0 * g) * .25f;
   float gamma4 = 1.0f - gamma3;
   float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
@@ -478,7 +480,7 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   c.Tdif = d.Tdif;
   float k_mu = k * mu0, k_mu2 = k_mu * k_mu, k_g3 = k * gamma3, k_g4 = k * gamma4;
   float dd = (fabsf(1.0f - k_mu2) >= eps) ? (1.0f - k_mu2) : eps;
-  float RT = w0 * d.RT / dd;
+  float RT = solver_div(w0 * d.RT, dd);
   float Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
                      k2e * (gamma3 - alpha2 * mu0) * Tnoscat);
   float Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
@@ -506,6 +508,9 @@ __device__ __forceinline__ void inc_2str(float &t1, float &w1, float &g1, float 
 // kInc: the atmosphere is incremented by band-resolved two-stream properties (tau, ssa, g)_bnd as it is read
 // (clouds%increment(atmos) fused).  Pass 1 needs only tau + tau_bnd; pass 2 forms the full increment and
 // parks (tau, ssa, g) in three workspace planes that pass 3 reads in place of the inputs.
+//
+// One column per block: packing two 224-g-point columns into 7 full waves (as the two-per-lane kernel does) was
+// measured slower here (C3 0.312 vs 0.288 ms): its 72 VGPRs allow 7 waves per SIMD, and this kernel wants 8.
 template <bool kHasG, bool kInc, int kPF>
 __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1,
                                             const float *__restrict__ inc_flux, const float *__restrict__ inc_dif,
@@ -519,29 +524,32 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 {
   static_assert(kRingSw % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nlev = nlay + 1;
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
-  const int nlev = nlay + 1;
+  const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
   float *ring = smem + kExpTabFloats;                // [3][kRingSw][ngpt]: up, dif, dir
+  float *part = ring + (size_t)3 * kRingSw * ngpt;   // [3][nlev][4]: up, dn, dir
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   load_exp_table(etab);
   __syncthreads();
-  float *part = ring + (size_t)3 * kRingSw * ngpt;   // [3][nlev][4]: up, dn, dir
-  const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
-  const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
+  const uint32_t row = 4u * (uint32_t)ngpt;
+  const uint32_t vL = 4u * (uint32_t)gc, vV = vL;  // g-point in the VGPR offset (layer and level arrays alike)
   const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol, plane = (size_t)ngpt * nlev * ncol;
-  const ColArr Ttau(tau, cl, row * nlay), Tssa(ssa, cl, row * nlay), Tg(kHasG ? gg : tau, cl, row * nlay);
-  const ColArr WA(ws, cv, row * nlev), WB(ws + plane, cv, row * nlev), WS(ws + 2 * plane, cv, row * nlev),
-      WD(ws + 3 * plane, cv, row * nlev);
+  const uint32_t bL = row * nlay, bV = row * nlev;
+  const ColArr Ttau(tau, cl, bL), Tssa(ssa, cl, bL), Tg(kHasG ? gg : tau, cl, bL);
+  const ColArr WA(ws, cv, bV), WB(ws + plane, cv, bV), WS(ws + 2 * plane, cv, bV), WD(ws + 3 * plane, cv, bV);
   // kInc: incremented (tau, ssa, g) planes (ngpt, nlay, ncol) after the four level planes
   const size_t lplane = (size_t)ngpt * nlay * ncol;
   float *wi = ws + 4 * plane;
-  const ColArr WT(wi, cl, row * nlay), WW(wi + lplane, cl, row * nlay), WG(wi + 2 * lplane, cl, row * nlay);
+  const ColArr WT(wi, cl, bL), WW(wi + lplane, cl, bL), WG(wi + 2 * lplane, cl, bL);
   // band-resolved increments: this lane's band in the VGPR offset, the layer in the SGPR offset
   const size_t cb = (size_t)bands.nbnd * nlay * icol;
-  const uint32_t brow = 4u * (uint32_t)bands.nbnd, vb = kInc ? 4u * (uint32_t)band_of(bands, gc) : 0u;
-  const ColArr Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, brow * nlay), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, brow * nlay),
-      Bg(kInc ? g_bnd : tau, kInc ? cb : 0, brow * nlay);
+  const uint32_t brow = 4u * (uint32_t)bands.nbnd;
+  const uint32_t vb = kInc ? 4u * (uint32_t)band_of(bands, gc) : 0u;
+  const uint32_t bB = kInc ? brow * nlay : 0u;
+  const ColArr Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, bB), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, bB),
+      Bg(kInc ? g_bnd : tau, kInc ? cb : 0, bB);
   auto ld_bnd = [&](const ColArr &a, int l) { return kInc ? a.ld(vb, brow * (uint32_t)l) : 0.0f; };
   const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
   // "layer l spans levels l (top side) and l+1" when top_at_1, else l+1 (top) and l
@@ -549,19 +557,20 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
   auto lay_of_down = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };  // j-th layer from the top
   auto lay_of_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };    // j-th layer from the surface
-  auto ld_g = [&](uint32_t soff) { return kHasG ? Tg.ld(vg, soff) : 0.0f; };
+  auto ld_g = [&](uint32_t soff) { return kHasG ? Tg.ld(vL, soff) : 0.0f; };
+  const size_t gcol = (size_t)gc + (size_t)ngpt * icol;  // this lane's (g, col) in (ngpt, ncol) arrays
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
-  const float Ftop = on ? inc_flux[g + (size_t)ngpt * icol] * mu0 : 0.0f;
+  const float Ftop = on ? inc_flux[gcol] * mu0 : 0.0f;
 
   // ---- pass 1: direct beam (only tau is read) ----
   float Fd = Ftop;
-  if (on) WA.st(Fd, vg, row * top);
+  if (on) WA.st(Fd, vV, row * top);
   {
     float pt[kPF], pi[kPF];
 #pragma unroll
     for (int p = 0; p < kPF; p++) {
       const int l = lay_of_down(min(p, nlay - 1));
-      pt[p] = Ttau.ld(vg, row * l);
+      pt[p] = Ttau.ld(vL, row * l);
       pi[p] = ld_bnd(Bt, l);
     }
     for (int j0 = 0; j0 < nlay; j0 += kPF) {
@@ -573,27 +582,27 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
           const float t = kInc ? pt[p] + pi[p] : pt[p];  // tau12 of the increment
           {
             const int ln = lay_of_down(min(j + kPF, nlay - 1));
-            pt[p] = Ttau.ld(vg, row * ln);
+            pt[p] = Ttau.ld(vL, row * ln);
             pi[p] = ld_bnd(Bt, ln);
           }
-          Fd = ref_expf_nb(-t * mu0_inv, etab) * Fd;
-          if (on) WA.st(Fd, vg, row * lev_below(l));
+          Fd = solver_exp_neg(-t * mu0_inv, etab) * Fd;
+          if (on) WA.st(Fd, vV, row * lev_below(l));
         }
       }
     }
   }
   // ---- pass 2: bottom -> top adding (albedo, src) ----
-  float alb_b = on ? alb_dif[g + (size_t)ngpt * icol] : 0.0f;  // albedo at the level below
-  float src_b = on ? Fd * alb_dir[g + (size_t)ngpt * icol] : 0.0f;
+  float alb_b = on ? alb_dif[gcol] : 0.0f;  // albedo at the level below
+  float src_b = on ? Fd * alb_dir[gcol] : 0.0f;
   if (on) {
-    WB.st(alb_b, vg, row * sfcl);
-    WS.st(src_b, vg, row * sfcl);
+    WB.st(alb_b, vV, row * sfcl);
+    WS.st(src_b, vV, row * sfcl);
   }
   {
     float pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load2 = [&](int p, int l) {
       const uint32_t s = row * l;
-      pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(l));
+      pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s); pf[p] = WA.ld(vV, row * lev_above(l));
       if constexpr (kInc) {
         qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
@@ -611,21 +620,21 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
           if constexpr (kInc) {
             inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);
             if (kSwIncPark && on) {
-              WT.st(t, vg, row * l);
-              WW.st(w0, vg, row * l);
-              WG.st(g0, vg, row * l);
+              WT.st(t, vL, row * l);
+              WW.st(w0, vL, row * l);
+              WG.st(g0, vL, row * l);
             }
           }
           load2(p, lay_of_up(min(j + kPF, nlay - 1)));
-          SwCoef c = sw_two_stream(t, w0, g0, mu0, mu0_inv, Fin, etab);
-          const float denom = rcp_rn_normal(1.0f - c.Rdif * alb_b);
-          const float alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
-          const float src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+          SwCoef cf = sw_two_stream<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fin, etab);
+          const float denom = rcp_rn_normal(1.0f - cf.Rdif * alb_b);
+          const float alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
+          const float src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
           if (on) {
             const uint32_t sa = row * lev_above(l);
-            WB.st(alb, vg, sa);
-            WS.st(src, vg, sa);
-            WD.st(c.Sdn, vg, row * l);
+            WB.st(alb, vV, sa);
+            WS.st(src, vV, sa);
+            WD.st(cf.Sdn, vV, row * l);
           }
           alb_b = alb;
           src_b = src;
@@ -647,7 +656,7 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 #endif
   };
   const int dl_dn = top_at_1 ? 1 : -1;
-  float Fdn = (on && inc_dif) ? inc_dif[g + (size_t)ngpt * icol] : 0.0f;
+  float Fdn = (on && inc_dif) ? inc_dif[gcol] : 0.0f;
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0);  // Eq 12 at the top; alb_b/src_b hold the top level's values
   flush(1, top, 1);
   {
@@ -655,15 +664,15 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
     auto load = [&](int p, int l) {
       const uint32_t s = row * l, sb = row * lev_below(l);
       if constexpr (kInc && kSwIncPark) {
-        pt[p] = WT.ld(vg, s); pw[p] = WW.ld(vg, s); pg[p] = WG.ld(vg, s);
+        pt[p] = WT.ld(vL, s); pw[p] = WW.ld(vL, s); pg[p] = WG.ld(vL, s);
       } else {
-        pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s);
+        pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s);
       }
       if constexpr (kInc && !kSwIncPark) {
         qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
-      pd[p] = WD.ld(vg, s);
-      pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb); pf[p] = WA.ld(vg, sb);
+      pd[p] = WD.ld(vV, s);
+      pa[p] = WB.ld(vV, sb); ps[p] = WS.ld(vV, sb); pf[p] = WA.ld(vV, sb);
     };
 #pragma unroll
     for (int p = 0; p < kPF; p++) load(p, lay_of_down(min(p, nlay - 1)));
@@ -695,15 +704,15 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 }
 
 template <bool kHasG, bool kInc>
-static void sw_launch(rrtmgpnn_context *ctx, size_t lds, int threads, int ngpt, int nlay, int ncol, int top_at_1,
-                      const float *inc_flux, const float *inc_flux_dif, const float *tau, const float *ssa,
-                      const float *g, const float *mu0, const float *alb_dir, const float *alb_dif,
+static void sw_launch(rrtmgpnn_context *ctx, size_t lds, int threads, int ngpt, int nlay, int ncol,
+                      int top_at_1, const float *inc_flux, const float *inc_flux_dif, const float *tau,
+                      const float *ssa, const float *g, const float *mu0, const float *alb_dir, const float *alb_dif,
                       const BandArgs &bands, const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws,
                       float *flux_up, float *flux_dn, float *flux_dir)
 {
   hipLaunchKernelGGL((sw_2stream_kernel<kHasG, kInc, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream,
-                     ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, bands,
-                     tau_bnd, ssa_bnd, g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
+                     ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
+                     alb_dir, alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
 }
 
 int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
@@ -726,23 +735,23 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (x2)
     return launch_sw_2stream_x2(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
                                 alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
-  int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRingSw * ngpt + (size_t)3 * (nlay + 1) * 4);
+  const int threads = (ngpt + 63) / 64 * 64;
+  const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kRingSw * ngpt + (size_t)3 * (nlay + 1) * 4);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
   const BandArgs nob{};
   const BandArgs &b = inc ? *bands : nob;
   if (inc && g)
-    sw_launch<true, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
-                          alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
+    sw_launch<true, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
+                          mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
   else if (inc)
-    sw_launch<false, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
-                           alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
+    sw_launch<false, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
+                           mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
   else if (g)
-    sw_launch<true, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
-                           alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
+    sw_launch<true, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
+                           mu0, alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
   else
-    sw_launch<false, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
-                            alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
+    sw_launch<false, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
+                            mu0, alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
   RRTMGPNN_LAUNCH_CHECK("sw_2stream_kernel");
   return RRTMGPNN_OK;
 }

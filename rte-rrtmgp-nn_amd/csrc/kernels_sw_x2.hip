@@ -19,9 +19,10 @@ __device__ __forceinline__ f2 vmax(f2 a, f2 b) { return __builtin_elementwise_ma
 __device__ __forceinline__ f2 vmin(f2 a, f2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ f2 splat(float x) { return (f2){x, x}; }
 
+// x <= 0 everywhere it is called (exp of -tau*k and -tau/mu0)
 __device__ __forceinline__ f2 exp2v(f2 x, const uint64_t *etab)
 {
-  return (f2){ref_expf_nb(x.x, etab), ref_expf_nb(x.y, etab)};
+  return (f2){solver_exp_neg(x.x, etab), solver_exp_neg(x.y, etab)};
 }
 
 // sqrt_rn_normal (libm_ref.hpp) with the correction fmas paired
@@ -48,6 +49,20 @@ __device__ __forceinline__ f2 rcp2(f2 b)
   return vfma(vfma(-b, q, one), r, q);
 }
 
+// solver_div (rte_device.hpp) with the Newton fmas paired
+__device__ __forceinline__ f2 div2(f2 a, f2 b)
+{
+#if RRTMGPNN_FASTOPS
+  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  r = vfma(vfma(-b, r, splat(1.0f)), r, r);
+  f2 q = a * r;
+  q = vfma(vfma(-b, q, a), r, q);
+  return vfma(vfma(-b, q, a), r, q);
+#else
+  return a / b;
+#endif
+}
+
 struct SwDif2 {
   f2 gamma1, gamma2, k, emk, em2k, RT, Rdif, Tdif;
 };
@@ -72,6 +87,7 @@ struct SwCoef2 {
 };
 
 // sw_two_stream of kernels_rte.hip, term by term
+template <bool kG0 = false>
 __device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0, float mu0_inv, f2 dir_inc,
                                                  const uint64_t *etab)
 {
@@ -80,7 +96,7 @@ __device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0
   const SwDif2 d = sw_dif2(tau, w0, g, etab);
   const f2 gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
   const f2 Tnoscat = exp2v(-tau * mu0_inv, etab);
-  const f2 gamma3 = (2.0f - 3.0f * mu0 * g) * .25f;
+  const f2 gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? splat(0.5f) : (2.0f - 3.0f * mu0 * g) * .25f;  // g == 0: exactly 0.5
   const f2 gamma4 = 1.0f - gamma3;
   const f2 alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   const f2 alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
@@ -92,7 +108,7 @@ __device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0
   f2 dd;
   dd.x = (fabsf(omk.x) >= eps) ? omk.x : eps;
   dd.y = (fabsf(omk.y) >= eps) ? omk.y : eps;
-  const f2 RT = w0 * d.RT / dd;
+  const f2 RT = div2(w0 * d.RT, dd);
   f2 Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
                   k2e * (gamma3 - alpha2 * mu0) * Tnoscat);
   f2 Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
@@ -155,8 +171,8 @@ constexpr bool kSw2Recomp = RRTMGPNN_SW2_RECOMP != 0;
 constexpr int kSw2Ring = 6;
 
 template <bool kHasG, bool kInc, int kPF>
-__global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
-    sw_2stream_x2_kernel(int ngpt, int nlay, int ncol, int top_at_1, const float *__restrict__ inc_flux,
+__global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
+    sw_2stream_x2_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
                          const float *__restrict__ ssa, const float *__restrict__ gg, const float *__restrict__ mu0p,
                          const float *__restrict__ alb_dir, const float *__restrict__ alb_dif, BandArgs bands,
@@ -166,29 +182,36 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
 {
   static_assert(kSw2Ring % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int icol = blockIdx.x, g = 2 * threadIdx.x;  // this lane's g-points: g, g + 1
-  const bool on = g < ngpt;
-  const int nlev = nlay + 1;
-  float *ring = smem + kExpTabFloats;                // [3][kSw2Ring][ngpt]: up, dif, dir
+  // `ncb` columns per block (as sw_2stream_kernel): lane t works on column c = t / (ngpt/2), g-points g, g + 1
+  const int nlev = nlay + 1, lanes = ngpt / 2;
+  const int icol0 = blockIdx.x * ncb, nc = min(ncb, ncol - icol0);
+  const int craw = (int)threadIdx.x / lanes;
+  const bool on = craw < nc;
+  const int c = on ? craw : nc - 1;
+  const int g = 2 * ((int)threadIdx.x - craw * lanes);
+  const int gc = on ? g : ngpt - 2;
+  const int icol = icol0 + c;
+  float *ring = smem + kExpTabFloats + (size_t)c * 3 * kSw2Ring * ngpt;  // this column's [3][kSw2Ring][ngpt]
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   load_exp_table(etab);
   __syncthreads();
-  float *part = ring + (size_t)3 * kSw2Ring * ngpt;  // [3][nlev][4]: up, dn, dir
-  const int gc = on ? g : ngpt - 2;
-  const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
-  const size_t cl = (size_t)ngpt * nlay * icol, cv = (size_t)ngpt * nlev * icol, plane = (size_t)ngpt * nlev * ncol;
-  const ColArr2 Ttau(tau, cl, row * nlay), Tssa(ssa, cl, row * nlay), Tg(kHasG ? gg : tau, cl, row * nlay);
-  const ColArr2 WA(ws, cv, row * nlev), WB(ws + plane, cv, row * nlev), WS(ws + 2 * plane, cv, row * nlev),
-      WD(ws + 3 * plane, cv, row * nlev);
+  const uint32_t row = 4u * (uint32_t)ngpt;
+  const uint32_t vL = 4u * (uint32_t)gc + (uint32_t)c * row * nlay, vV = 4u * (uint32_t)gc + (uint32_t)c * row * nlev;
+  const size_t cl = (size_t)ngpt * nlay * icol0, cv = (size_t)ngpt * nlev * icol0, plane = (size_t)ngpt * nlev * ncol;
+  const uint32_t bL = (uint32_t)nc * row * nlay, bV = (uint32_t)nc * row * nlev;
+  const ColArr2 Ttau(tau, cl, bL), Tssa(ssa, cl, bL), Tg(kHasG ? gg : tau, cl, bL);
+  const ColArr2 WA(ws, cv, bV), WB(ws + plane, cv, bV), WS(ws + 2 * plane, cv, bV), WD(ws + 3 * plane, cv, bV);
   const size_t lplane = (size_t)ngpt * nlay * ncol;
   float *wi = ws + 4 * plane;
-  const ColArr2 WT(wi, cl, row * nlay), WW(wi + lplane, cl, row * nlay), WG(wi + 2 * lplane, cl, row * nlay);
+  const ColArr2 WT(wi, cl, bL), WW(wi + lplane, cl, bL), WG(wi + 2 * lplane, cl, bL);
   // band-resolved increments: one band offset per g-point of the pair
-  const size_t cb = (size_t)bands.nbnd * nlay * icol;
-  const uint32_t brow = 4u * (uint32_t)bands.nbnd;
-  const uint32_t vb0 = kInc ? 4u * (uint32_t)band_of(bands, gc) : 0u, vb1 = kInc ? 4u * (uint32_t)band_of(bands, gc + 1) : 0u;
-  const ColArr2 Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, brow * nlay), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, brow * nlay),
-      Bg(kInc ? g_bnd : tau, kInc ? cb : 0, brow * nlay);
+  const size_t cb = (size_t)bands.nbnd * nlay * icol0;
+  const uint32_t brow = 4u * (uint32_t)bands.nbnd, vbc = (uint32_t)c * brow * nlay;
+  const uint32_t vb0 = kInc ? 4u * (uint32_t)band_of(bands, gc) + vbc : 0u,
+                 vb1 = kInc ? 4u * (uint32_t)band_of(bands, gc + 1) + vbc : 0u;
+  const uint32_t bB = kInc ? (uint32_t)nc * brow * nlay : 0u;
+  const ColArr2 Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, bB), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, bB),
+      Bg(kInc ? g_bnd : tau, kInc ? cb : 0, bB);
   auto ld_bnd = [&](const ColArr2 &a, int l) {
     return kInc ? (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)} : splat(0.0f);
   };
@@ -197,20 +220,20 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
   auto lev_below = [&](int l) { return top_at_1 ? l + 1 : l; };
   auto lay_of_down = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
   auto lay_of_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
-  auto ld_g = [&](uint32_t soff) { return kHasG ? Tg.ld(vg, soff) : splat(0.0f); };
+  auto ld_g = [&](uint32_t soff) { return kHasG ? Tg.ld(vL, soff) : splat(0.0f); };
   auto ld_col = [&](const float *p) { return on ? *(const f2 *)(p + gc + (size_t)ngpt * icol) : splat(0.0f); };
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   const f2 Ftop = ld_col(inc_flux) * mu0;
 
   // ---- pass 1: direct beam ----
   f2 Fd = Ftop;
-  if (on) WA.st(Fd, vg, row * top);
+  if (on) WA.st(Fd, vV, row * top);
   {
     f2 pt[kPF], pi[kPF];
 #pragma unroll
     for (int p = 0; p < kPF; p++) {
       const int l = lay_of_down(min(p, nlay - 1));
-      pt[p] = Ttau.ld(vg, row * l);
+      pt[p] = Ttau.ld(vL, row * l);
       pi[p] = ld_bnd(Bt, l);
     }
     for (int j0 = 0; j0 < nlay; j0 += kPF) {
@@ -222,11 +245,11 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
           const f2 t = kInc ? pt[p] + pi[p] : pt[p];
           {
             const int ln = lay_of_down(min(j + kPF, nlay - 1));
-            pt[p] = Ttau.ld(vg, row * ln);
+            pt[p] = Ttau.ld(vL, row * ln);
             pi[p] = ld_bnd(Bt, ln);
           }
           Fd = exp2v(-t * mu0_inv, etab) * Fd;
-          if (on) WA.st(Fd, vg, row * lev_below(l));
+          if (on) WA.st(Fd, vV, row * lev_below(l));
         }
       }
     }
@@ -235,14 +258,14 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
   f2 alb_b = ld_col(alb_dif);
   f2 src_b = Fd * ld_col(alb_dir);
   if (on) {
-    WB.st(alb_b, vg, row * sfcl);
-    WS.st(src_b, vg, row * sfcl);
+    WB.st(alb_b, vV, row * sfcl);
+    WS.st(src_b, vV, row * sfcl);
   }
   {
     f2 pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load2 = [&](int p, int l) {
       const uint32_t s = row * l;
-      pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s); pf[p] = WA.ld(vg, row * lev_above(l));
+      pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s); pf[p] = WA.ld(vV, row * lev_above(l));
       if constexpr (kInc) {
         qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
@@ -260,21 +283,21 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
           if constexpr (kInc) {
             inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
             if (on) {
-              WT.st(t, vg, row * l);
-              WW.st(w0, vg, row * l);
-              WG.st(g0, vg, row * l);
+              WT.st(t, vL, row * l);
+              WW.st(w0, vL, row * l);
+              WG.st(g0, vL, row * l);
             }
           }
           load2(p, lay_of_up(min(j + kPF, nlay - 1)));
-          const SwCoef2 c = sw_two_stream2(t, w0, g0, mu0, mu0_inv, Fin, etab);
-          const f2 denom = rcp2(1.0f - c.Rdif * alb_b);
-          const f2 alb = c.Rdif + c.Tdif * c.Tdif * alb_b * denom;
-          const f2 src = c.Sup + c.Tdif * denom * (src_b + alb_b * c.Sdn);
+          const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fin, etab);
+          const f2 denom = rcp2(1.0f - cf.Rdif * alb_b);
+          const f2 alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
+          const f2 src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
           if (on) {
             const uint32_t sa = row * lev_above(l);
-            WB.st(alb, vg, sa);
-            WS.st(src, vg, sa);
-            if constexpr (!kSw2Recomp) WD.st(c.Sdn, vg, row * l);
+            WB.st(alb, vV, sa);
+            WS.st(src, vV, sa);
+            if constexpr (!kSw2Recomp) WD.st(cf.Sdn, vV, row * l);
           }
           alb_b = alb;
           src_b = src;
@@ -290,7 +313,10 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
       *(f2 *)&ring[((size_t)2 * kSw2Ring + r) * ngpt + g] = dir;
     }
   };
-  auto flush = [&](int n, int lev0, int dl) { ring_flush<kSw2Ring>(ring, part, 3, n, lev0, dl, ngpt, nlev, true); };
+  auto flush = [&](int n, int lev0, int dl) {
+    ring_flush_sw<kSw2Ring>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
+                            flux_dir);
+  };
   const int dl_dn = top_at_1 ? 1 : -1;
   f2 Fdn = inc_dif ? ld_col(inc_dif) : splat(0.0f);
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0);
@@ -300,14 +326,14 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
     auto load = [&](int p, int l) {
       const uint32_t s = row * l, sb = row * lev_below(l);
       if constexpr (kInc) {
-        pt[p] = WT.ld(vg, s); pw[p] = WW.ld(vg, s); pg[p] = WG.ld(vg, s);
+        pt[p] = WT.ld(vL, s); pw[p] = WW.ld(vL, s); pg[p] = WG.ld(vL, s);
       } else {
-        pt[p] = Ttau.ld(vg, s); pw[p] = Tssa.ld(vg, s); pg[p] = ld_g(s);
+        pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s);
       }
-      pa[p] = WB.ld(vg, sb); ps[p] = WS.ld(vg, sb);
+      pa[p] = WB.ld(vV, sb); ps[p] = WS.ld(vV, sb);
       if constexpr (!kSw2Recomp) {
-        pd[p] = WD.ld(vg, s);
-        pf[p] = WA.ld(vg, sb);
+        pd[p] = WD.ld(vV, s);
+        pf[p] = WA.ld(vV, sb);
       }
     };
     f2 Fd3 = Ftop;  // kSw2Recomp: the direct beam again, top down, exactly as pass 1 formed it
@@ -324,11 +350,11 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
           load(p, lay_of_down(min(j + kPF, nlay - 1)));
           if constexpr (kSw2Recomp) {
             // pass 2's coefficients from the same inputs (same bits), the beam from pass 1's recurrence
-            const SwCoef2 c = sw_two_stream2(t, w0, g0, mu0, mu0_inv, Fd3, etab);
-            Rdif = c.Rdif;
-            Tdif = c.Tdif;
-            Sdn = c.Sdn;
-            Fd3 = c.Tnoscat * Fd3;
+            const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fd3, etab);
+            Rdif = cf.Rdif;
+            Tdif = cf.Tdif;
+            Sdn = cf.Sdn;
+            Fd3 = cf.Tnoscat * Fd3;
             Fdir = Fd3;
           } else {
             const SwDif2 d = sw_dif2(t, w0, g0, etab);
@@ -344,11 +370,6 @@ __global__ void __launch_bounds__(128, RRTMGPNN_SW2_WAVES)
       flush(min(kSw2Ring, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
     }
   }
-  for (int l = threadIdx.x; l < nlev; l += blockDim.x) {
-    flux_up[l + (size_t)nlev * icol] = combine4(part + 4 * l);
-    flux_dn[l + (size_t)nlev * icol] = combine4(part + (size_t)nlev * 4 + 4 * l);
-    flux_dir[l + (size_t)nlev * icol] = combine4(part + (size_t)2 * nlev * 4 + 4 * l);
-  }
 }
 
 // ngpt even and <= 256; workspace as launch_sw_2stream's (the fused increment parks tau, ssa, g)
@@ -358,31 +379,36 @@ int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
                          float *flux_dn, float *flux_dir)
 {
-  const int threads = (ngpt / 2 + 63) / 64 * 64;
-  const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)3 * kSw2Ring * ngpt + (size_t)3 * (nlay + 1) * 4);
-  if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
+#ifndef RRTMGPNN_SW_NCB
+#define RRTMGPNN_SW_NCB 0
+#endif
+  const int ncb = RRTMGPNN_SW_NCB > 0 && RRTMGPNN_SW_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SW_NCB : columns_per_block(ngpt / 2);
+  const int threads = (ncb * (ngpt / 2) + 63) / 64 * 64;
+  const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * kSw2Ring * ngpt);
+  if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: LDS ring exceeds 160 KiB");
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
-  const dim3 grid(ncol), block(threads);
+  const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
   constexpr int PF = RRTMGPNN_SW2_PF;
-  if (bands && g)
-    hipLaunchKernelGGL((sw_2stream_x2_kernel<true, true, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
-                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd,
-                       g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
-  else if (bands)
-    hipLaunchKernelGGL((sw_2stream_x2_kernel<false, true, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
-                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd,
-                       g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
-  else if (g)
-    hipLaunchKernelGGL((sw_2stream_x2_kernel<true, false, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
-                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, nullptr, nullptr,
-                       nullptr, (float *)ws, flux_up, flux_dn, flux_dir);
-  else
-    hipLaunchKernelGGL((sw_2stream_x2_kernel<false, false, PF>), grid, block, lds, ctx->stream, ngpt, nlay, ncol,
-                       top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir, alb_dif, b, nullptr, nullptr,
-                       nullptr, (float *)ws, flux_up, flux_dn, flux_dir);
-  RRTMGPNN_LAUNCH_CHECK("sw_2stream_x2_kernel");
-  return RRTMGPNN_OK;
+  // rings past 64 KiB (4 columns of 224 g-points: 64.5 KiB) need the dynamic-LDS limit raised, once for all four
+  // instantiations (so later calls, and hipGraph captures of them, make no attribute call)
+  static bool lds_raised = false;
+  if (lds > 64 * 1024 && !lds_raised) {
+    const void *ks[4] = {(const void *)sw_2stream_x2_kernel<true, true, PF>, (const void *)sw_2stream_x2_kernel<false, true, PF>,
+                         (const void *)sw_2stream_x2_kernel<true, false, PF>, (const void *)sw_2stream_x2_kernel<false, false, PF>};
+    for (const void *k : ks) RRTMGPNN_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    lds_raised = true;
+  }
+  auto go = [&](auto kern, const float *tb, const float *sb, const float *gb) -> int {
+    hipLaunchKernelGGL(kern, grid, block, lds, ctx->stream, ngpt, nlay, ncol, top_at_1, ncb, inc_flux, inc_flux_dif,
+                       tau, ssa, g, mu0, alb_dir, alb_dif, b, tb, sb, gb, (float *)ws, flux_up, flux_dn, flux_dir);
+    RRTMGPNN_LAUNCH_CHECK("sw_2stream_x2_kernel");
+    return RRTMGPNN_OK;
+  };
+  if (bands && g) return go(sw_2stream_x2_kernel<true, true, PF>, tau_bnd, ssa_bnd, g_bnd);
+  if (bands) return go(sw_2stream_x2_kernel<false, true, PF>, tau_bnd, ssa_bnd, g_bnd);
+  if (g) return go(sw_2stream_x2_kernel<true, false, PF>, nullptr, nullptr, nullptr);
+  return go(sw_2stream_x2_kernel<false, false, PF>, nullptr, nullptr, nullptr);
 }
 
 }  // namespace rrtmgpnn

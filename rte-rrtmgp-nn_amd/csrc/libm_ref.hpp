@@ -107,6 +107,40 @@ __device__ __forceinline__ float rcp_rn_normal(float b)
   return fmaf(fmaf(-b, q, 1.0f), r, q);
 }
 
+// Correctly rounded a / b for operands and quotient in the normal range (|a| >= 2^-100, |b| and |a/b| in
+// [2^-126, 2^126]; a == 0 also gives the IEEE result): the compiler's division sequence -- reciprocal, one Newton
+// step, quotient, two residual corrections -- without v_div_scale and v_div_fixup, which leave operands and
+// result untouched in that range, so the bits are those of a / b (3 of 11 instructions fewer).
+__device__ __forceinline__ float div_rn_normal(float a, float b)
+{
+  float r = __builtin_amdgcn_rcpf(b);
+  r = fmaf(fmaf(-b, r, 1.0f), r, r);
+  float q = a * r;
+  q = fmaf(fmaf(-b, q, a), r, q);
+  return fmaf(fmaf(-b, q, a), r, q);
+}
+
+// ref_expf_nb for x <= 0 (the solvers' exp(-tau*D), exp(-tau/mu0), exp(-k*tau) with tau >= 0): only glibc's
+// underflow case can occur, so the overflow select is dropped.  For 0 < x <= 0x1.62e42ep6 the main path is
+// still glibc's; only a larger x (a negative tau below -88/D) would return a finite value where glibc gives inf.
+__device__ __forceinline__ float ref_expf_neg(float x, const uint64_t *tab)
+{
+  const double InvLn2N = 0x1.71547652b82fep+0 * 32, SHIFT = 0x1.8p+52;
+  const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+               C2 = 0x1.62e42ff0c52d6p-1 / 32;
+  const double xd = (double)x;
+  double kd = __fma_rn(InvLn2N, xd, SHIFT);
+  const uint64_t ki = f64_as_u64(kd);
+  kd -= SHIFT;
+  const double r = __fma_rn(InvLn2N, xd, -kd);
+  const double s = u64_as_f64(tab[ki % 32] + (ki << 47));
+  const double z = __fma_rn(C0, r, C1), r2 = r * r;
+  double y = __fma_rn(C2, r, 1.0);
+  y = __fma_rn(z, r2, y);
+  const float res = (float)(y * s);
+  return (x < -0x1.9fe368p6f) ? 0.0f : res;
+}
+
 // Copy the exp table into LDS (call with all threads of the block; a __syncthreads() must follow).
 __device__ __forceinline__ void load_exp_table(uint64_t *lds_tab)
 {

@@ -22,6 +22,29 @@ __device__ __forceinline__ int band_of(const BandArgs &b, int g)
 
 static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS
 
+// RRTMGPNN_FASTOPS (default 1; 0 for tools/solver_variants.sh A/B runs): the solvers' divisions whose operands stay
+// in the normal range use div_rn_normal, and their exps of non-positive arguments ref_expf_neg (libm_ref.hpp).
+// Same bits either way; fewer instructions per layer step.
+#ifndef RRTMGPNN_FASTOPS
+#define RRTMGPNN_FASTOPS 1
+#endif
+__device__ __forceinline__ float solver_div(float a, float b)
+{
+#if RRTMGPNN_FASTOPS
+  return div_rn_normal(a, b);
+#else
+  return a / b;
+#endif
+}
+__device__ __forceinline__ float solver_exp_neg(float x, const uint64_t *tab)
+{
+#if RRTMGPNN_FASTOPS
+  return ref_expf_neg(x, tab);
+#else
+  return ref_expf_nb(x, tab);
+#endif
+}
+
 
 // Gauss-Jacobi quadrature of the LW no-scattering solvers (secants and weights, nmus <= 4)
 struct LwAngles {
@@ -86,6 +109,67 @@ __device__ __forceinline__ void ring_flush(const float *ring, float *part, int n
 
 __device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]) + p[2]) + p[3]; }
 
+// The SW solvers' flush for blocks that hold `ncb` columns: ring [ncb][3][R][ngpt] (up, dif, dir of column c at
+// ring + c*3*R*ngpt).  Each (column, quantity, level) thread forms the level's complete ordered sum -- the same
+// partials and the same ((p0 + p1) + p2) + p3 as ring_flush + combine4 -- and stores it straight to the flux
+// array: up, dn (= dif + dir, dn_mode) and dir.  Columns at or past ncol (the grid's last block) store nothing.
+template <int R>
+__device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n, int lev0, int dl, int ngpt, int nlev,
+                                              int icol0, int ncol, float *o_up, float *o_dn, float *o_dir)
+{
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 3 * ncb * n) {
+    const int c = t / (3 * n), rem = t - c * 3 * n, q = rem / n, s = rem - q * n;
+    const float *rc = ring + (size_t)c * 3 * R * ngpt;
+    const float *r = rc + ((size_t)q * R + s) * ngpt;
+    const float *r2 = rc + ((size_t)2 * R + s) * ngpt;
+    const bool dn = q == 1;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    if ((ngpt & 3) == 0) {
+      const float4 *r4 = (const float4 *)r, *q4 = (const float4 *)r2;
+      const int n4 = ngpt >> 2;
+      if (dn) {
+#pragma unroll 4
+        for (int m = 0; m < n4; m++) {
+          const float4 a = r4[m], b = q4[m];
+          s0 = (s0 + a.x) + b.x; s1 = (s1 + a.y) + b.y; s2 = (s2 + a.z) + b.z; s3 = (s3 + a.w) + b.w;
+        }
+      } else {
+#pragma unroll 4
+        for (int m = 0; m < n4; m++) {
+          const float4 a = r4[m];
+          s0 = s0 + a.x; s1 = s1 + a.y; s2 = s2 + a.z; s3 = s3 + a.w;
+        }
+      }
+    } else {
+      if (dn) for (int i = 0; i < ngpt; i++) s0 = s0 + (r[i] + r2[i]);
+      else    for (int i = 0; i < ngpt; i++) s0 = s0 + r[i];
+    }
+    const int icol = icol0 + c;
+    if (icol < ncol) {
+      float *o = q == 0 ? o_up : (q == 1 ? o_dn : o_dir);
+      o[lev0 + s * dl + (size_t)nlev * icol] = ((s0 + s1) + s2) + s3;
+    }
+  }
+  __syncthreads();
+}
+
+// Columns per block for a solver whose column occupies `lanes` lanes: the count (1, 2 or 4, at most 512 lanes)
+// that leaves the fewest idle lanes in the block's last wave -- the two-per-lane SW kernel's 112 lanes per column
+// (224 g-points): 4 columns = 448 lanes = 7 full waves instead of 2 waves with 16 idle lanes each (C4 -5 %).
+inline int columns_per_block(int lanes)
+{
+  int best = 1;
+  double best_waste = 1e30;
+  for (int k = 1; k <= 4; k *= 2) {
+    if (k * lanes > 512) break;
+    const double waste = (double)((k * lanes + 63) / 64 * 64) / (k * lanes);
+    if (waste < best_waste - 1e-9) { best = k; best_waste = waste; }
+  }
+  return best;
+}
+
 // ------------------------------------------------------------------------------------------
 // Column-local addressing.  Every solver array is (ngpt, n, ncol) with the column block uniform per
 // workgroup, so each array gets a per-column buffer descriptor built from wave-uniform values: a
@@ -96,8 +180,7 @@ struct ColArr {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ ColArr() = default;
   __device__ __forceinline__ ColArr(const float *base, size_t col_off, uint32_t bytes)
-      : r(__builtin_amdgcn_make_buffer_rsrc((void *)(base + col_off), 0, (int)bytes, 0x00020000)) {}
-  __device__ __forceinline__ float ld(uint32_t voff, uint32_t soff) const
+      : r(__builtin_amdgcn_make_buffer_rsrc((void *)(base + col_off), 0, (int)bytes, 0x00020000)) {}  __device__ __forceinline__ float ld(uint32_t voff, uint32_t soff) const
   {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
   }

@@ -33,10 +33,14 @@ def bind(L):
 
 
 for v in names:
-    L = ctypes.CDLL(os.path.join(B, "lib_%s.so" % v))
+    # "name@k": variant `name` with the SW solver forced to k g-points per lane (default: by problem size)
+    lib, _, swk = v.partition("@")
+    L = ctypes.CDLL(os.path.join(B, "lib_%s.so" % lib))
     bind(L)
     h = _lib.c_vp()
     assert L.rrtmgpnn_context_create(0, None, h) == 0
+    if swk or os.environ.get("SW_KERNEL"):
+        L.rrtmgpnn_context_set_sw_kernel(h, int(swk or os.environ["SW_KERNEL"]))
     line, res = [], []
     for tag, st in steps.items():
         # the networks are loaded through the variant library too (its packed MLP images)
@@ -69,7 +73,7 @@ for v in names:
             if name not in SHOW[tag]:
                 continue
             best = 1e9
-            for _ in range(2):
+            for _ in range(int(os.environ.get("REPS", "2"))):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(20):

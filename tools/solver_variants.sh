@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/.."
 PKG=rte-rrtmgp-nn_amd
-B=${TMPDIR:-/tmp}/rrtmgpnn_var
+B=${VAR_DIR:-${TMPDIR:-/tmp}/rrtmgpnn_var}
 rm -rf $B; mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off"
 # sources without tuning knobs are built once
