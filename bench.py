@@ -238,6 +238,10 @@ def main():
             stage_roofs[name] = {"bound": "hbm", "achieved_gbs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)}
         if sq.get(name, {}).get("valu_busy") is not None:
             stage_roofs[name]["valu_busy"] = sq[name]["valu_busy"]
+        if kind == "flop" and sq.get(name, {}).get("mfma_busy") is not None:
+            stage_roofs[name]["mfma_busy"] = sq[name]["mfma_busy"]  # rocprof matrix-core utilisation (pmc_counters.py)
+            if sq[name].get("mfma_flop"):
+                stage_roofs[name]["mfma_flop_counter"] = sq[name]["mfma_flop"]
     if best is not None:
         name, kind, amount = best
         ms = stages[name]

@@ -169,6 +169,10 @@ __device__ __forceinline__ float activate(int act, float x)
   }
 }
 
+#ifndef RRTMGPNN_MLP_FASTDIV
+#define RRTMGPNN_MLP_FASTDIV 1
+#endif
+
 // Compile-time activation sets of the fused kernel: ACTS == 1 is the shipped models' softsign,
 // softsign, linear (Appendix A of SURVEY.md), inlined straight-line; ACTS == 0 dispatches on the
 // runtime codes (any other combination).
@@ -177,6 +181,12 @@ __device__ __forceinline__ float act_hidden(int act, float x)
 {
 #ifdef RRTMGPNN_ABL_MLP_CHEAP_ACT  // ablation only: breaks parity
   if constexpr (ACTS == 1) return x * 0.5f;
+#endif
+#if RRTMGPNN_MLP_FASTDIV
+  // softsign with the division sequence minus v_div_scale/v_div_fixup (libm_ref.hpp div_rn_normal): exact for
+  // |x| < 2^126 -- below 2^-24, |x| + 1 rounds to 1 and the quotient is x itself; above, both operands and the
+  // quotient are normal
+  if constexpr (ACTS == 1) return div_rn_normal(x, fabsf(x) + 1.0f);
 #endif
   if constexpr (ACTS == 1) return x / (fabsf(x) + 1.0f);  // softsign (mod_activation.F90:107-128)
   else return activate(act, x);
@@ -348,8 +358,22 @@ __device__ __forceinline__ floatx4 mlp_out_tile(const float *__restrict__ img, i
 #define RRTMGPNN_MLP_GO_UNROLL 1
 #endif
 constexpr int kMlpThreads = RRTMGPNN_MLP_THREADS, kGoUnroll = RRTMGPNN_MLP_GO_UNROLL;
+// Compile-time output g-tile count for the shipped pairs (LW 16, SW 14): the output loop unrolls completely and the
+// next tile's inputs are loaded before this tile's stores, so the wait for them (vmcnt counts loads and stores
+// together, in order) no longer drains the stores.  0 compiles the runtime-count loop only.
+#ifndef RRTMGPNN_MLP_NGT_CT
+#define RRTMGPNN_MLP_NGT_CT 1
+#endif
+// output tiles unrolled per loop trip when NGTC > 0 (tools/solver_variants.sh: LW 4 -5 % C3 / -7 % C4 against the
+// runtime loop, full unrolling spills; SW 2 -9 % at C4)
+#ifndef RRTMGPNN_MLP_CT_UNROLL_LW
+#define RRTMGPNN_MLP_CT_UNROLL_LW 4
+#endif
+#ifndef RRTMGPNN_MLP_CT_UNROLL_SW
+#define RRTMGPNN_MLP_CT_UNROLL_SW 2
+#endif
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS>
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0>
 __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -364,22 +388,32 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
   const float *imgB = lds + a.imgA_floats;
   const int lane = threadIdx.x & 63, j = lane & 15, q = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;
-  const int NGT = a.ngt, nx = a.nx, ngpt = a.ngpt;
+  const int NGT = NGTC > 0 ? NGTC : a.ngt, nx = a.nx, ngpt = a.ngpt;
   const ImgLayout LA = img_layout(AK, AH1, AH2, NGT);
   const ImgLayout LB = img_layout(BK, BH1, BH2, NGT);
   const long long ntiles = (a.nbatch + 15) / 16;
 
-  for (long long tile = (long long)blockIdx.x * nwaves + wave; tile < ntiles; tile += (long long)gridDim.x * nwaves) {
-    const long long s0 = tile * 16;
-    // Layer-1 B operand: x[sample s0+j][k = 4t+q]
-    float xv[AK];
-    {
-      const long long s = s0 + j;
+  const long long tstride = (long long)gridDim.x * nwaves;
+  // Layer-1 B operand: x[sample s0+j][k = 4t+q]
+  auto load_x = [&](long long tl, float (&xv)[AK]) {
+    const long long s = tl * 16 + j;
 #pragma unroll
-      for (int t = 0; t < AK; t++) {
-        int k = 4 * t + q;
-        xv[t] = (s < a.nbatch && k < nx) ? a.x[(size_t)s * nx + k] : 0.0f;
-      }
+    for (int t = 0; t < AK; t++) {
+      int k = 4 * t + q;
+      xv[t] = (s < a.nbatch && k < nx) ? a.x[(size_t)s * nx + k] : 0.0f;
+    }
+  };
+  float xn[AK];  // NGTC: the next tile's inputs, loaded before this tile's stores
+  if constexpr (NGTC > 0) load_x((long long)blockIdx.x * nwaves + wave, xn);
+  for (long long tile = (long long)blockIdx.x * nwaves + wave; tile < ntiles; tile += tstride) {
+    const long long s0 = tile * 16;
+    float xv[AK];
+    if constexpr (NGTC > 0) {
+#pragma unroll
+      for (int t = 0; t < AK; t++) xv[t] = xn[t];
+      load_x(tile + tstride, xn);
+    } else {
+      load_x(tile, xv);
     }
     floatx4 hA[AH2];
     mlp_hidden<AK, AH1, AH2, ACTS>(imgA, NGT, xv, lane, a.actA[0], a.actA[1], hA);
@@ -407,8 +441,7 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
           if (gc + r < row) p[r] = v[r];
       }
     };
-#pragma unroll kGoUnroll
-    for (int go = 0; go < NGT; go++) {
+    auto out_tile = [&](int go) {
       const int g0 = 16 * go + 4 * q;
       const floatx4 yA = mlp_out_tile<AH2>(imgA, LA.l3, go, hA, lane);
       const floatx4 bA = *(const floatx4 *)&imgA[LA.b3 + g0];
@@ -492,14 +525,24 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
           }
         }
       }
+    };
+    if constexpr (NGTC > 0 && MODE == MLP_LW_PAIR) {
+#pragma unroll RRTMGPNN_MLP_CT_UNROLL_LW
+      for (int go = 0; go < NGTC; go++) out_tile(go);
+    } else if constexpr (NGTC > 0) {
+#pragma unroll RRTMGPNN_MLP_CT_UNROLL_SW
+      for (int go = 0; go < NGTC; go++) out_tile(go);
+    } else {
+#pragma unroll kGoUnroll
+      for (int go = 0; go < NGT; go++) out_tile(go);
     }
   }
 }
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS>
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0>
 static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
 {
-  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS>;
+  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS, NGTC>;
   size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
   // Raise the dynamic-LDS limit once per instantiation (kept out of the per-call path so the launch
@@ -528,8 +571,18 @@ static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
   auto std_acts = [](const int *act) {
     return act[0] == RRTMGPNN_ACT_SOFTSIGN && act[1] == RRTMGPNN_ACT_SOFTSIGN && act[2] == RRTMGPNN_ACT_LINEAR;
   };
-  if (std_acts(a.actA) && (!pair || std_acts(a.actB)))
+  if (std_acts(a.actA) && (!pair || std_acts(a.actB))) {
+    // the shipped pairs' output tile counts compiled in: LW g256 (16 tiles), SW g224 (14)
+    constexpr bool lw = MODE == MLP_LW_PAIR && AK == 5 && AH1 == 4 && AH2 == 4 && BH1 == 1 && BH2 == 1;
+    constexpr bool sw = MODE == MLP_SW_PAIR && AK == 2 && AH1 == 1 && AH2 == 1 && BH1 == 1 && BH2 == 1;
+    if constexpr (RRTMGPNN_MLP_NGT_CT && lw) {
+      if (a.ngt == 16) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16>(ctx, a);
+    }
+    if constexpr (RRTMGPNN_MLP_NGT_CT && sw) {
+      if (a.ngt == 14) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 14>(ctx, a);
+    }
     return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1>(ctx, a);
+  }
   return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 0>(ctx, a);
 }
 

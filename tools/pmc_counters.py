@@ -53,6 +53,15 @@ def main():
             r["valu_busy"] = round(4.0 * r["SQ_ACTIVE_INST_VALU"] / (r["SQ_BUSY_CYCLES"] / N_SE * N_SIMD), 4)
         if r.get("SQ_INSTS_VALU") and r.get("SQ_WAVES"):
             r["valu_insts_per_wave"] = round(r["SQ_INSTS_VALU"] / r["SQ_WAVES"], 1)
+        # MFMA pass: MOPS count multiply-adds / 512 per the counter description, so flops = MOPS * 512;
+        # SQ_VALU_MFMA_BUSY_CYCLES sums the matrix pipes' busy cycles over all SIMDs (MI355X_MICROARCH.md), so its
+        # share of (kernel cycles x 1024 SIMDs) is the chip's matrix-core utilisation
+        if r.get("SQ_INSTS_VALU_MFMA_MOPS_F32") is not None:
+            r["mfma_flop"] = r["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512.0
+        if r.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and r.get("SQ_BUSY_CYCLES"):
+            r["mfma_busy"] = round(r["SQ_VALU_MFMA_BUSY_CYCLES"] / (r["SQ_BUSY_CYCLES"] / N_SE * N_SIMD), 4)
+            if r.get("SQ_INSTS_MFMA"):
+                r["mfma_busy_cycles_per_inst"] = round(r["SQ_VALU_MFMA_BUSY_CYCLES"] / r["SQ_INSTS_MFMA"], 2)
     txt = json.dumps(res, indent=1, sort_keys=True)
     print(txt)
     if len(sys.argv) > 3:
@@ -61,7 +70,9 @@ def main():
                 allres = json.load(fh)
         except (OSError, ValueError):
             allres = {}
-        allres[sys.argv[3]] = res
+        cfg = allres.setdefault(sys.argv[3], {})
+        for st, r in res.items():  # merge: passes of different counter sets add to the same stage entry
+            cfg.setdefault(st, {}).update(r)
         allres["_note"] = ("per-launch SQ counters (rocprofv3 --pmc, one pass) by stage; valu_busy = share of the chip's "
                            "VALU issue slots used (tools/pmc_counters.py)")
         with open(sys.argv[2], "w") as fh:

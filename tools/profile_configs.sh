@@ -9,6 +9,7 @@ set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 STEPS=${STEPS:-30}
+MFMA="SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_BUSY_CYCLES SQ_WAVES"
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
 for cfg in ${CONFIGS:-c3 c4}; do
   o=gpurun_out/$cfg
@@ -23,6 +24,9 @@ for cfg in ${CONFIGS:-c3 c4}; do
   echo "== $cfg rocprofv3 --pmc SQ counters"
   timeout -k 10 300 rocprofv3 --pmc $SQ -d $o/pmc_SQ -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > $o/pmc_SQ.log 2>&1 || exit $?
   python3 tools/pmc_counters.py $o/pmc_SQ gpurun_out/pmc_sq.json $cfg > $o/pmc_sq.txt || exit $?
+  echo "== $cfg rocprofv3 --pmc MFMA counters"
+  timeout -k 10 300 rocprofv3 --pmc $MFMA -d $o/pmc_MFMA -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > $o/pmc_MFMA.log 2>&1 || exit $?
+  python3 tools/pmc_counters.py $o/pmc_MFMA gpurun_out/pmc_sq.json $cfg > $o/pmc_mfma.txt || exit $?
   # the bench line last, so its roofline carries this build's PMC traffic and SQ figures
   echo "== $cfg bench"
   timeout -k 10 300 python bench.py --config $cfg --steps $STEPS --warmup 5 --traffic-json gpurun_out/pmc_traffic.json --sq-json gpurun_out/pmc_sq.json ${BENCH_ARGS:-} > $o/bench.json 2> $o/bench.err || exit $?
