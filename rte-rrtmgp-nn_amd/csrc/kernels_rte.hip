@@ -184,7 +184,7 @@ __host__ __device__ constexpr size_t lw_btab_floats(int nbnd, int nlay) { return
 // kInc: tau is incremented by a band-resolved absorption optical depth tau_bnd (nbnd, nlay, ncol) as it is
 // read -- inc_1scalar_by_1scalar_bybnd (rte/kernels/mo_optical_props_kernels.F90:358-372), tau + tau_bnd(band),
 // the same single add -- so clouds%increment(atmos) never makes a pass over the g-point array.
-template <bool kFused, bool kInc, int kPF>
+template <bool kFused, bool kInc, int kPF, bool kMulti>
 __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top_at_1, LwAngles ang,
                                            const float *__restrict__ inc_flux, const float *__restrict__ tau,
                                            const float *__restrict__ lay, const float *__restrict__ lev,
@@ -200,10 +200,11 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   const int gc = on ? g : ngpt - 1;  // clamped g-point for unconditional loads
   const int nlev = nlay + 1;
   const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
-  // nmus > 1 (lw_solver_noscat_GaussQuad :383-412): g-point fluxes are summed over angles first, then
-  // reduced with sum_broadband's plain sequential sum; ws holds the per-g accumulators (2, nlev, ngpt).
-  const bool multi = ang.nmus > 1;
-  float *wcol = multi ? ws + (size_t)2 * nlev * ngpt * icol : nullptr;
+  // kMulti (nmus > 1, lw_solver_noscat_GaussQuad :383-412): g-point fluxes are summed over angles first, then
+  // reduced with sum_broadband's plain sequential sum; ws holds the per-g accumulators (2, nlev, ngpt).  A
+  // template parameter, so the nmus = 1 kernel's layer loop holds no global memory access besides its loads and
+  // the compiler's vmcnt waits keep the prefetch distance (a runtime branch merged both paths into vmcnt(0)).
+  float *wcol = kMulti ? ws + (size_t)2 * nlev * ngpt * icol : nullptr;
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   float *btab = smem + kExpTabFloats;                        // fused: [nbnd][2*nlay+1] + [nbnd]
   const int brow = 2 * nlay + 1;
@@ -242,9 +243,9 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   const float e = on ? emis[g + (size_t)ngpt * icol] : 0.0f;
   const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
-  // stage one level's value: slot r of the ring, or (nmus > 1) the per-g accumulator of plane q
+  // stage one level's value: slot r of the ring, or (kMulti) the per-g accumulator of plane q
   auto put = [&](float v, int r, int q, int level, bool acc) {
-    if (multi) {
+    if constexpr (kMulti) {
       if (on) {
         float *w = wcol + ((size_t)q * nlev + level) * ngpt + g;
         *w = acc ? *w + v : v;
@@ -255,7 +256,7 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   };
   auto flush = [&](float *pq, int n, int lev0, int dl) {
 #ifndef RRTMGPNN_ABL_NO_BARRIER
-    if (!multi) ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
+    if constexpr (!kMulti) ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
 #endif
   };
   // layer source and the level source on the side given by `li` (lev index, 0..nlay)
@@ -272,7 +273,7 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     const float D = ang.D[imu];
     // radiance -> flux factor inside the broadband sum; with nmus == 1 and ngpt % 4 != 0 the reference
     // sums plain radiances (quirk B-5, mo_rte_solver_kernels.F90:287-320)
-    const float fac = (multi || (ngpt & 3) == 0) ? 2.0f * kPi * ang.w[imu] : 1.0f;
+    const float fac = (kMulti || (ngpt & 3) == 0) ? 2.0f * kPi * ang.w[imu] : 1.0f;
     const bool acc = imu > 0;
     float I = inc / (2.0f * kPi * ang.w[imu]);
     put(fac * I, 0, 0, top, acc);
@@ -286,25 +287,28 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
         const int l = lay_dn(min(p, nlay - 1));
         pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pv[p] = lev_ld(l + 1); pi[p] = ld_inc(l);
       }
+      // Every step issues its prefetch loads unconditionally (clamped to the last layer); only the arithmetic of
+      // the last chunk's steps past nlay is skipped, by a uniform branch holding no memory access, so the
+      // compiler's vmcnt waits see the same loads on every path and keep the prefetch distance.
+      auto step = [&](int j, int r) {
+        const int p = r % kPF, l = lay_dn(min(j, nlay - 1));
+        const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
+        {
+          const int ln = lay_dn(min(j + kPF, nlay - 1));
+          pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
+          pi[p] = ld_inc(ln);
+        }
+        if (j < nlay) {
+          const float T = solver_exp_neg(-t, etab);
+          const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
+          const float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
+          I = T * I + S;
+          put(fac * I, r, 0, top_at_1 ? l + 1 : l, acc);
+        }
+      };
       for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
-        for (int r = 0; r < kRing; r++) {
-          const int j = j0 + r, p = r % kPF;
-          if (j < nlay) {
-            const int l = lay_dn(j);
-            const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
-            {
-              const int ln = lay_dn(min(j + kPF, nlay - 1));
-              pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
-              pi[p] = ld_inc(ln);
-            }
-            const float T = solver_exp_neg(-t, etab);
-            const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
-            const float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
-            I = T * I + S;
-            put(fac * I, r, 0, top_at_1 ? l + 1 : l, acc);
-          }
-        }
+        for (int r = 0; r < kRing; r++) step(j0 + r, r);
         flush(pdn, min(kRing, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     }
@@ -322,32 +326,32 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
         pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
         if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * l);
       }
+      auto step = [&](int j, int r) {
+        const int p = r % kPF, l = lay_up(min(j, nlay - 1));
+        // fused: lev(l) = pfrac(l) * B(tlev(l)) (l < nlay), from the layer's own pfrac
+        const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l);
+        const float lvup = lev_src(kFused ? py[p] : pv[p], l);
+        {
+          const int ln = lay_up(min(j + kPF, nlay - 1));
+          pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pi[p] = ld_inc(ln);
+          if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * ln);
+        }
+        if (j < nlay) {
+          const float T = solver_exp_neg(-t, etab);
+          const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
+          const float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
+          U = T * U + S;
+          put(fac * U, r, 1, top_at_1 ? l : l + 1, acc);
+        }
+      };
       for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
-        for (int r = 0; r < kRing; r++) {
-          const int j = j0 + r, p = r % kPF;
-          if (j < nlay) {
-            const int l = lay_up(j);
-            // fused: lev(l) = pfrac(l) * B(tlev(l)) (l < nlay), from the layer's own pfrac
-            const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l);
-            const float lvup = lev_src(kFused ? py[p] : pv[p], l);
-            {
-              const int ln = lay_up(min(j + kPF, nlay - 1));
-              pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pi[p] = ld_inc(ln);
-              if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * ln);
-            }
-            const float T = solver_exp_neg(-t, etab);
-            const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
-            const float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
-            U = T * U + S;
-            put(fac * U, r, 1, top_at_1 ? l : l + 1, acc);
-          }
-        }
+        for (int r = 0; r < kRing; r++) step(j0 + r, r);
         flush(pup, min(kRing, nlay - j0), sfcl - dl_dn * (j0 + 1), -dl_dn);
       }
     }
   }
-  if (multi) {
+  if constexpr (kMulti) {
     __syncthreads();
     for (int t = g; t < 2 * nlev; t += blockDim.x) {
       const float *w = wcol + (size_t)t * ngpt;
@@ -386,10 +390,15 @@ static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, i
     int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
     if (rc) return rc;
   }
-  hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF>), dim3(ncol),
-                     dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac,
-                     kFused ? lay_or_pfrac : lev_source, sfc_emis, sfc_source, pl, bands, tau_bnd, (float *)ws,
-                     flux_up, flux_dn);
+  constexpr int PF = kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF;
+  if (nmus > 1)
+    hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, PF, true>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
+                       nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac, kFused ? lay_or_pfrac : lev_source,
+                       sfc_emis, sfc_source, pl, bands, tau_bnd, (float *)ws, flux_up, flux_dn);
+  else
+    hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, PF, false>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
+                       nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac, kFused ? lay_or_pfrac : lev_source,
+                       sfc_emis, sfc_source, pl, bands, tau_bnd, (float *)ws, flux_up, flux_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_noscat_kernel");
   return RRTMGPNN_OK;
 }
@@ -563,8 +572,14 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   const float Ftop = on ? inc_flux[gcol] * mu0 : 0.0f;
 
   // ---- pass 1: direct beam (only tau is read) ----
+  // Straight-line layer steps: the prefetch loads and the stores are issued on every step, the stores of idle
+  // lanes (g >= ngpt) and of the steps past nlay at an out-of-range buffer offset (dropped by the hardware), and
+  // only arithmetic sits under the uniform `j < nlay` branch.  So every path issues the same memory operations and
+  // the compiler's vmcnt waits (loads and stores share the counter) keep the prefetch distance instead of
+  // draining to vmcnt(0) at each merge.
+  const uint32_t vVs = on ? vV : kBufOOB, vLs = on ? vL : kBufOOB;
   float Fd = Ftop;
-  if (on) WA.st(Fd, vV, row * top);
+  WA.st(Fd, vVs, row * top);
   {
     float pt[kPF], pi[kPF];
 #pragma unroll
@@ -577,27 +592,23 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
-        if (j < nlay) {
-          const int l = lay_of_down(j);
-          const float t = kInc ? pt[p] + pi[p] : pt[p];  // tau12 of the increment
-          {
-            const int ln = lay_of_down(min(j + kPF, nlay - 1));
-            pt[p] = Ttau.ld(vL, row * ln);
-            pi[p] = ld_bnd(Bt, ln);
-          }
-          Fd = solver_exp_neg(-t * mu0_inv, etab) * Fd;
-          if (on) WA.st(Fd, vV, row * lev_below(l));
+        const int l = lay_of_down(min(j, nlay - 1));
+        const float t = kInc ? pt[p] + pi[p] : pt[p];  // tau12 of the increment
+        {
+          const int ln = lay_of_down(min(j + kPF, nlay - 1));
+          pt[p] = Ttau.ld(vL, row * ln);
+          pi[p] = ld_bnd(Bt, ln);
         }
+        if (j < nlay) Fd = solver_exp_neg(-t * mu0_inv, etab) * Fd;
+        WA.st(Fd, j < nlay ? vVs : kBufOOB, row * lev_below(l));
       }
     }
   }
   // ---- pass 2: bottom -> top adding (albedo, src) ----
   float alb_b = on ? alb_dif[gcol] : 0.0f;  // albedo at the level below
   float src_b = on ? Fd * alb_dir[gcol] : 0.0f;
-  if (on) {
-    WB.st(alb_b, vV, row * sfcl);
-    WS.st(src_b, vV, row * sfcl);
-  }
+  WB.st(alb_b, vVs, row * sfcl);
+  WS.st(src_b, vVs, row * sfcl);
   {
     float pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load2 = [&](int p, int l) {
@@ -613,32 +624,33 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
-        if (j < nlay) {
-          const int l = lay_of_up(j);
-          float t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : 0.0f;
-          const float Fin = pf[p];
-          if constexpr (kInc) {
-            inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);
-            if (kSwIncPark && on) {
-              WT.st(t, vL, row * l);
-              WW.st(w0, vL, row * l);
-              WG.st(g0, vL, row * l);
-            }
+        const int l = lay_of_up(min(j, nlay - 1));
+        const uint32_t vs = j < nlay ? vVs : kBufOOB, vls = j < nlay ? vLs : kBufOOB;
+        float t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : 0.0f;
+        const float Fin = pf[p];
+        if constexpr (kInc) {
+          inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);
+          if (kSwIncPark) {
+            WT.st(t, vls, row * l);
+            WW.st(w0, vls, row * l);
+            WG.st(g0, vls, row * l);
           }
-          load2(p, lay_of_up(min(j + kPF, nlay - 1)));
+        }
+        load2(p, lay_of_up(min(j + kPF, nlay - 1)));
+        float alb = alb_b, src = src_b, Sdn = 0.0f;
+        if (j < nlay) {
           SwCoef cf = sw_two_stream<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fin, etab);
           const float denom = rcp_rn_normal(1.0f - cf.Rdif * alb_b);
-          const float alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
-          const float src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
-          if (on) {
-            const uint32_t sa = row * lev_above(l);
-            WB.st(alb, vV, sa);
-            WS.st(src, vV, sa);
-            WD.st(cf.Sdn, vV, row * l);
-          }
-          alb_b = alb;
-          src_b = src;
+          alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
+          src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
+          Sdn = cf.Sdn;
         }
+        const uint32_t sa = row * lev_above(l);
+        WB.st(alb, vs, sa);
+        WS.st(src, vs, sa);
+        WD.st(Sdn, vs, row * l);
+        alb_b = alb;
+        src_b = src;
       }
     }
   }
@@ -680,11 +692,11 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 #pragma unroll
       for (int r = 0; r < kRingSw; r++) {
         const int j = j0 + r, p = r % kPF;
+        float t = pt[p], w0 = pw[p], g0 = kHasG || (kInc && kSwIncPark) ? pg[p] : 0.0f;
+        const float Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
+        if constexpr (kInc && !kSwIncPark) inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);  // pass 2's increment again
+        load(p, lay_of_down(min(j + kPF, nlay - 1)));
         if (j < nlay) {
-          float t = pt[p], w0 = pw[p], g0 = kHasG || (kInc && kSwIncPark) ? pg[p] : 0.0f;
-          const float Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
-          if constexpr (kInc && !kSwIncPark) inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);  // pass 2's increment again
-          load(p, lay_of_down(min(j + kPF, nlay - 1)));
           // R_dif, T_dif exactly as pass 2 computed them (same inputs, same expressions -> same bits)
           const SwDif d = sw_dif(t, w0, (kHasG || kInc) ? g0 : 0.0f, etab);
           const float denom = rcp_rn_normal(1.0f - d.Rdif * alb);

@@ -226,8 +226,11 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
   const f2 Ftop = ld_col(inc_flux) * mu0;
 
   // ---- pass 1: direct beam ----
+  // Straight-line layer steps as in sw_2stream_kernel: memory operations on every step (idle lanes and steps past
+  // nlay store at kBufOOB), arithmetic alone under the uniform `j < nlay` branch.
+  const uint32_t vVs = on ? vV : kBufOOB, vLs = on ? vL : kBufOOB;
   f2 Fd = Ftop;
-  if (on) WA.st(Fd, vV, row * top);
+  WA.st(Fd, vVs, row * top);
   {
     f2 pt[kPF], pi[kPF];
 #pragma unroll
@@ -240,27 +243,23 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
-        if (j < nlay) {
-          const int l = lay_of_down(j);
-          const f2 t = kInc ? pt[p] + pi[p] : pt[p];
-          {
-            const int ln = lay_of_down(min(j + kPF, nlay - 1));
-            pt[p] = Ttau.ld(vL, row * ln);
-            pi[p] = ld_bnd(Bt, ln);
-          }
-          Fd = exp2v(-t * mu0_inv, etab) * Fd;
-          if (on) WA.st(Fd, vV, row * lev_below(l));
+        const int l = lay_of_down(min(j, nlay - 1));
+        const f2 t = kInc ? pt[p] + pi[p] : pt[p];
+        {
+          const int ln = lay_of_down(min(j + kPF, nlay - 1));
+          pt[p] = Ttau.ld(vL, row * ln);
+          pi[p] = ld_bnd(Bt, ln);
         }
+        if (j < nlay) Fd = exp2v(-t * mu0_inv, etab) * Fd;
+        WA.st(Fd, j < nlay ? vVs : kBufOOB, row * lev_below(l));
       }
     }
   }
   // ---- pass 2: bottom -> top adding ----
   f2 alb_b = ld_col(alb_dif);
   f2 src_b = Fd * ld_col(alb_dir);
-  if (on) {
-    WB.st(alb_b, vV, row * sfcl);
-    WS.st(src_b, vV, row * sfcl);
-  }
+  WB.st(alb_b, vVs, row * sfcl);
+  WS.st(src_b, vVs, row * sfcl);
   {
     f2 pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load2 = [&](int p, int l) {
@@ -276,32 +275,31 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
+        const int l = lay_of_up(min(j, nlay - 1));
+        const uint32_t vs = j < nlay ? vVs : kBufOOB, vls = j < nlay ? vLs : kBufOOB;
+        f2 t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : splat(0.0f);
+        const f2 Fin = pf[p];
+        if constexpr (kInc) {
+          inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
+          WT.st(t, vls, row * l);
+          WW.st(w0, vls, row * l);
+          WG.st(g0, vls, row * l);
+        }
+        load2(p, lay_of_up(min(j + kPF, nlay - 1)));
+        f2 alb = alb_b, src = src_b, Sdn = splat(0.0f);
         if (j < nlay) {
-          const int l = lay_of_up(j);
-          f2 t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : splat(0.0f);
-          const f2 Fin = pf[p];
-          if constexpr (kInc) {
-            inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
-            if (on) {
-              WT.st(t, vL, row * l);
-              WW.st(w0, vL, row * l);
-              WG.st(g0, vL, row * l);
-            }
-          }
-          load2(p, lay_of_up(min(j + kPF, nlay - 1)));
           const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fin, etab);
           const f2 denom = rcp2(1.0f - cf.Rdif * alb_b);
-          const f2 alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
-          const f2 src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
-          if (on) {
-            const uint32_t sa = row * lev_above(l);
-            WB.st(alb, vV, sa);
-            WS.st(src, vV, sa);
-            if constexpr (!kSw2Recomp) WD.st(cf.Sdn, vV, row * l);
-          }
-          alb_b = alb;
-          src_b = src;
+          alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
+          src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
+          Sdn = cf.Sdn;
         }
+        const uint32_t sa = row * lev_above(l);
+        WB.st(alb, vs, sa);
+        WS.st(src, vs, sa);
+        if constexpr (!kSw2Recomp) WD.st(Sdn, vs, row * l);
+        alb_b = alb;
+        src_b = src;
       }
     }
   }
@@ -343,11 +341,11 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
 #pragma unroll
       for (int r = 0; r < kSw2Ring; r++) {
         const int j = j0 + r, p = r % kPF;
+        const f2 t = pt[p], w0 = pw[p], g0 = (kHasG || kInc) ? pg[p] : splat(0.0f);
+        const f2 alb = pa[p], src = ps[p];
+        f2 Rdif, Tdif, Sdn = kSw2Recomp ? splat(0.0f) : pd[p], Fdir = kSw2Recomp ? splat(0.0f) : pf[p];
+        load(p, lay_of_down(min(j + kPF, nlay - 1)));
         if (j < nlay) {
-          const f2 t = pt[p], w0 = pw[p], g0 = (kHasG || kInc) ? pg[p] : splat(0.0f);
-          const f2 alb = pa[p], src = ps[p];
-          f2 Rdif, Tdif, Sdn = kSw2Recomp ? splat(0.0f) : pd[p], Fdir = kSw2Recomp ? splat(0.0f) : pf[p];
-          load(p, lay_of_down(min(j + kPF, nlay - 1)));
           if constexpr (kSw2Recomp) {
             // pass 2's coefficients from the same inputs (same bits), the beam from pass 1's recurrence
             const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fd3, etab);

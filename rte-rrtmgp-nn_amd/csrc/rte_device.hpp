@@ -176,6 +176,11 @@ inline int columns_per_block(int lanes)
 // load is `buffer_load v, voff=g*4, s_rsrc, soff=layer*ngpt*4` -- no per-lane 64-bit address math,
 // the layer offset lives in an SGPR.
 // ------------------------------------------------------------------------------------------
+// A buffer offset past every solver array's range: raw buffer stores there are dropped, loads return 0 (the
+// range check covers the VGPR offset; the SGPR layer offset is added past it), so idle lanes and padding steps
+// can issue the same stores as the others without a branch.
+static constexpr uint32_t kBufOOB = 0x7ffff000u;
+
 struct ColArr {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ ColArr() = default;
