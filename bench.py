@@ -194,21 +194,38 @@ def main():
     pcie = {"value": round(ncol / (io_ms * 1e-3), 1), "unit": "columns/s", "ms_per_step": round(io_ms, 4),
             "bytes_per_step": io_bytes, "note": "per GPU; pinned host buffers, H2D inputs + step + D2H fluxes"}
 
-    # ---- per-stage kernel times, HIP events on the context's stream (eager launches) ----
-    stages = {}
+    # ---- per-stage kernel times: HIP events around every launch of `reps` whole steps issued eagerly, each launch on
+    # the stream it runs on.  stages_ms (the rooflines): the launches serialised -- each kernel has the chip to
+    # itself, in its place in the step (after the kernel that produced its inputs), as in the graph replays of
+    # `bench.py --no-overlap`, whose rocprofv3 --kernel-trace averages they match.  stages_overlapped_ms: the step's
+    # own concurrency (LW and SW chains overlapped, as the timed region runs); there the events also hold the time a
+    # launch waits for CUs the other chain occupies ----
     reps = max(3, min(20, args.steps))
-    torch.cuda.synchronize(dev)
-    for name, fn, cargs in step.calls:
-        s = step.stream_for(name)  # each stage alone on its own stream (no overlap while timing stages)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(s):
-            fn(*cargs)  # warm
-            ev0.record(s)
-            for _ in range(reps):
-                fn(*cargs)
-            ev1.record(s)
-        ev1.synchronize()
-        stages[name] = ev0.elapsed_time(ev1) / reps  # ms per launch
+
+    def time_stages(serial):
+        step.step()  # warm the eager path
+        torch.cuda.synchronize(dev)
+        timing = {}
+        prev = None  # serial: every launch waits for the one before it, across steps too
+        for _ in range(reps):
+            if serial:
+                for name, fn, cargs in step.calls:
+                    s = step.stream_for(name)
+                    if prev is not None:
+                        s.wait_event(prev)
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record(s)
+                    fn(*cargs)
+                    ev1.record(s)
+                    timing.setdefault(name, []).append((ev0, ev1))
+                    prev = ev1
+            else:
+                step.step(timing)
+        torch.cuda.synchronize(dev)
+        return {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
+
+    stages = time_stages(True)
+    stages_ov = time_stages(False) if step.overlap else None
     # dominant kernel and its roofline
     best = None
     for name, ms in stages.items():
@@ -265,7 +282,9 @@ def main():
             ach = amount / (ms * 1e-3) / 1e9
             roof = {"kernel": name, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "algorithmic_per_launch": amount,
-                    "avg_launch_ms": round(ms, 4)}
+                    "avg_launch_ms": round(ms, 4),
+                    "timing": "HIP events around each launch, whole steps with the launches serialised (the kernel "
+                              "alone on the chip; rocprofv3 trace of bench.py --no-overlap)"}
             if traffic:
                 roof["actual_gbs"] = round(traffic / (ms * 1e-3) / 1e9, 1)  # PMC bytes / launch time
         if roof is not None and sq.get(name, {}).get("valu_busy") is not None:
@@ -307,6 +326,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+            "stages_overlapped_ms": None if stages_ov is None else {k: round(v, 4) for k, v in stages_ov.items()},
             "stage_roofline": stage_roofs,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             "host_resident": pcie,

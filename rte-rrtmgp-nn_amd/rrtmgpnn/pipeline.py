@@ -25,6 +25,8 @@ clouds=(lwp, iwp, rel, rei) makes it the all-sky step of examples/all-sky/rrtmgp
 :219), added to the LW absorption optical depth by band (1scl increment), and for SW delta-scaled and
 added as a two-stream increment; the SW solver then sees a non-zero asymmetry parameter.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -35,6 +37,11 @@ from .api import GAUSS_DS, GAUSS_WTS, Context
 
 # calls of the SW chain (issued on the second stream when overlapping)
 SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver"}
+
+
+# issue order of the fused step (stable sort; names not listed keep their place at the end)
+FUSED_ORDER = ["get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", "predict_nn_lw", "lw_solver",
+               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver"]
 
 
 def _t(a, dev):
@@ -204,16 +211,27 @@ class ClearSkyStep:
                  (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
+        if fused and os.environ.get("RRTMGPNN_STEP_ORDER", "") != "class":
+            # the small kernels that do not depend on a network's output go first in their chain, ahead of the big
+            # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW
+            # solver held while the LW solver, which needs it, could not start
+            order = {n: i for i, n in enumerate(FUSED_ORDER)}
+            self.calls.sort(key=lambda c: order.get(c[0], len(order)))
         # overlap: the SW chain runs on a second context/stream, forked after col_dry (which both streams read)
         # and joined at the end of the step -- the VALU-bound SW solver shares the CUs with the MFMA-bound LW
         # network and the LW solver instead of running after them
         self.overlap = overlap
         self.ctx2 = None
         if overlap:
-            self.ctx2 = Context(device, torch.cuda.Stream(self.dev))
+            self.ctx2 = Context(device, self._sw_stream())
             self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
+
+    def _sw_stream(self):
+        # default priority: a high-priority SW stream (critical path) was measured 25 % slower at C3 -- it takes every
+        # CU first and the chains stop overlapping (tools/ab_prio.sh)
+        return torch.cuda.Stream(self.dev)
 
     def stream_for(self, name):
         """The torch stream a call of `self.calls` is issued on."""
@@ -235,11 +253,20 @@ class ClearSkyStep:
                 except Exception:
                     pass
 
-    def step(self):
+    def step(self, timing=None):
+        """Issue one step.  timing: a dict name -> list; each launch is then bracketed by timing events recorded on
+        the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended."""
         for name, fn, args in self.calls:
+            if timing is not None:
+                s = self.stream_for(name)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
             rc = fn(*args)
             if rc:
                 check(rc, name)
+            if timing is not None:
+                e1.record(s)
+                timing.setdefault(name, []).append((e0, e1))
             if self.overlap and name == "get_col_dry":
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
@@ -256,7 +283,7 @@ class ClearSkyStep:
         old = self.ctx.stream
         if self.overlap:
             old2 = self.ctx2.stream
-            self.ctx2.use_stream(torch.cuda.Stream(self.dev))
+            self.ctx2.use_stream(self._sw_stream())
         with torch.cuda.stream(s):
             self.ctx.use_stream(s)
             with torch.cuda.graph(g, stream=s):

@@ -3,8 +3,9 @@
 # one GPU box call.  Each config's artefacts land in gpurun_out/<config>/; PMC traffic is merged into
 # gpurun_out/pmc_traffic.json, the SQ counters (valu_busy etc.) into gpurun_out/pmc_sq.json.
 # Stops at the first failing GPU step (every step has its own time limit).
-# The kernel trace runs with --no-overlap: bench.py times each stage alone on its stream, and per-kernel durations
-# only agree with those when the LW and SW chains do not share the chip (overlapped, both stretch).
+# The kernel trace runs the bench line's own command (LW and SW chains overlapped, as bench.py times its stages),
+# so its per-kernel averages are comparable with the line's roofline; a second trace with --no-overlap gives each
+# kernel's time with the chip to itself (prof_iso).
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -15,7 +16,8 @@ for cfg in ${CONFIGS:-c3 c4}; do
   o=gpurun_out/$cfg
   mkdir -p $o
   echo "== $cfg rocprofv3 kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --no-overlap ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof_iso -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --no-overlap ${BENCH_ARGS:-} > $o/prof_iso.log 2>&1 || exit $?
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg rocprofv3 --pmc $c"
     timeout -k 10 300 rocprofv3 --pmc $c -d $o/pmc_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > $o/pmc_$c.log 2>&1 || exit $?
