@@ -735,11 +735,10 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
   const bool inc = bands != nullptr;
-  // two g-points per lane (kernels_sw_x2.hip) halves the waves: worth it only once they still fill the chip
-  // (C4, 10k columns: -3 %), not at C3's 1800 columns (+5 %, the SW chain then starves the overlapped LW chain)
-  const long long x2_waves = (long long)ncol * ((ngpt / 2 + 63) / 64);
+  // two g-points per lane (kernels_sw_x2.hip, 4 columns per 7-wave block) whenever ngpt is even: alone 7 % faster at
+  // C3 and the whole step 1.8 % (C3) / 2 % (C4) faster than one g-point per lane (tools/cmp_sw_kernel.sh)
   const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
-  const bool x2 = kSwX2 && (ngpt % 2) == 0 && (mode == 2 || (mode == 0 && x2_waves >= 8LL * 4 * ctx->num_cus));
+  const bool x2 = kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc && (kSwIncPark || x2) ? 3 * (size_t)ngpt * nlay * ncol : 0);
   int rc = ctx->workspace(sizeof(float) * nws, &ws);

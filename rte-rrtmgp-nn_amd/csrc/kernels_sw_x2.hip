@@ -168,7 +168,10 @@ struct ColArr2 {
 #define RRTMGPNN_SW2_RECOMP 1
 #endif
 constexpr bool kSw2Recomp = RRTMGPNN_SW2_RECOMP != 0;
-constexpr int kSw2Ring = 6;
+#ifndef RRTMGPNN_SW2_RING
+#define RRTMGPNN_SW2_RING 6
+#endif
+constexpr int kSw2Ring = RRTMGPNN_SW2_RING;
 
 template <bool kHasG, bool kInc, int kPF>
 __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)

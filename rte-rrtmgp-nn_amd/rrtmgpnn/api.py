@@ -56,7 +56,7 @@ class Context:
         check(_lib.lib().rrtmgpnn_context_synchronize(self.h), "context_synchronize")
 
     def set_sw_kernel(self, mode):
-        """0: SW two-stream kernel by problem size (default); 1 / 2: one / two g-points per lane (bit-identical)."""
+        """0: SW two-stream kernel by ngpt (two g-points per lane when even; default); 1 / 2: one / two (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_sw_kernel(self.h, int(mode)), "context_set_sw_kernel")
 
     def __del__(self):
@@ -68,7 +68,7 @@ class Context:
 
 
 def set_sw_kernel_default(mode):
-    """The SW two-stream kernel of every context not set itself: 0 by problem size (the default), 1 / 2 one /
+    """The SW two-stream kernel of every context not set itself: 0 by ngpt (the default), 1 / 2 one /
     two g-points per lane (bit-identical fluxes; tests force each)."""
     check(_lib.lib().rrtmgpnn_context_set_sw_kernel(None, int(mode)), "context_set_sw_kernel")
 
