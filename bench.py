@@ -110,10 +110,13 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; with more ranks than GPUs (rehearsing the N-rank path on a smaller box) ranks share
+    # devices round-robin, and RRTMGPNN_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    backend = os.environ.get("RRTMGPNN_DIST_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", world_size=world, rank=rank,
-                                device_id=torch.device("cuda", local))
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, init_method="env://", world_size=world, rank=rank, **kw)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
