@@ -43,7 +43,7 @@ struct rrtmgpnn_context {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int num_cus = 256;
-  int sw_kernel = -1;  // SW two-stream kernel: 0 by problem size, 1 / 2 g-points per lane, -1 the library default
+  int sw_kernel = -1;  // SW two-stream kernel: 0 by ngpt, 1 / 2 g-points per lane, -1 the library default
   void *ws = nullptr;
   size_t ws_bytes = 0;
   int workspace(size_t bytes, void **out);

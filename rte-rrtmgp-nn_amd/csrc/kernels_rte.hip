@@ -36,16 +36,6 @@ __device__ __forceinline__ float wave_sum(float v)
 // and also writes lev_source(:,nlay+1) (ilay == nlay-1) and the surface sources (ilay == sfc_lay-1)
 // from its in-register pfrac, before pfrac is overwritten with lay_source (no cross-block race).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float interp1d(float val, float offset, float delta, int ntemp, const float *__restrict__ t)
-{
-  float val0 = (val - offset) / delta;
-  int iv = (int)val0;  // Fortran int(): truncation
-  float frac = val0 - (float)iv;
-  int index = min(ntemp - 1, max(1, iv + 1));
-  float lo = t[index - 1], hi = t[index];
-  return lo + frac * (hi - lo);
-}
-
 constexpr int kPlanckLayers = 4;  // layers per block: independent loads in flight per lane
 
 __global__ void planck_source_kernel(int ncol, int nlay, int ngpt, int ntemp, const float *__restrict__ tlay,
@@ -171,15 +161,6 @@ static constexpr int kSwMaxG = RRTMGPNN_SW_WAVES > 0 ? 256 : 1024;
 // LDS: etab | [fused: B [nbnd][2*nlay+1], Bsfc[nbnd]] | ring [kRing][ngpt] | part [2][nlev][4]
 // ------------------------------------------------------------------------------------------
 
-
-struct LwPlanck {
-  const float *tlay, *tlev, *tsfc, *totplnk;
-  int ntemp, sfc_lay;
-  float tmin, tdelta;
-};
-
-// fused Planck table size in floats, padded so the ring that follows stays 16-byte aligned
-__host__ __device__ constexpr size_t lw_btab_floats(int nbnd, int nlay) { return ((size_t)nbnd * (2 * nlay + 2) + 3) & ~(size_t)3; }
 
 // kInc: tau is incremented by a band-resolved absorption optical depth tau_bnd (nbnd, nlay, ncol) as it is
 // read -- inc_1scalar_by_1scalar_bybnd (rte/kernels/mo_optical_props_kernels.F90:358-372), tau + tau_bnd(band),

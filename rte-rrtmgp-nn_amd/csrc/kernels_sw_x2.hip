@@ -6,62 +6,12 @@
 // v_pk_fma_f32 (two IEEE operations each, so the same bits as the scalar kernel), loads and stores move 8
 // bytes per lane, and half as many lanes walk the column.  The glibc-exact exps (double precision), the IEEE
 // divisions and the selects stay per element.  Used when ngpt is even.
-#include "rte_device.hpp"
+#include "x2_device.hpp"
 
 namespace rrtmgpnn {
-
-typedef float f2 __attribute__((ext_vector_type(2)));
+using namespace x2;
 
 namespace {
-
-__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 vmax(f2 a, f2 b) { return __builtin_elementwise_max(a, b); }
-__device__ __forceinline__ f2 vmin(f2 a, f2 b) { return __builtin_elementwise_min(a, b); }
-__device__ __forceinline__ f2 splat(float x) { return (f2){x, x}; }
-
-// x <= 0 everywhere it is called (exp of -tau*k and -tau/mu0)
-__device__ __forceinline__ f2 exp2v(f2 x, const uint64_t *etab)
-{
-  return (f2){solver_exp_neg(x.x, etab), solver_exp_neg(x.y, etab)};
-}
-
-// sqrt_rn_normal (libm_ref.hpp) with the correction fmas paired
-__device__ __forceinline__ f2 sqrt2(f2 x)
-{
-  const f2 s = (f2){__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
-  const f2 sm = (f2){__uint_as_float(__float_as_uint(s.x) - 1u), __uint_as_float(__float_as_uint(s.y) - 1u)};
-  const f2 sp = (f2){__uint_as_float(__float_as_uint(s.x) + 1u), __uint_as_float(__float_as_uint(s.y) + 1u)};
-  const f2 em = vfma(-sm, s, x), ep = vfma(-sp, s, x);
-  f2 r;
-  r.x = (ep.x > 0.0f) ? sp.x : ((em.x <= 0.0f) ? sm.x : s.x);
-  r.y = (ep.y > 0.0f) ? sp.y : ((em.y <= 0.0f) ? sm.y : s.y);
-  return r;
-}
-
-// rcp_rn_normal (libm_ref.hpp) with the Newton fmas paired
-__device__ __forceinline__ f2 rcp2(f2 b)
-{
-  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
-  const f2 one = splat(1.0f);
-  r = vfma(vfma(-b, r, one), r, r);
-  f2 q = r;
-  q = vfma(vfma(-b, q, one), r, q);
-  return vfma(vfma(-b, q, one), r, q);
-}
-
-// solver_div (rte_device.hpp) with the Newton fmas paired
-__device__ __forceinline__ f2 div2(f2 a, f2 b)
-{
-#if RRTMGPNN_FASTOPS
-  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
-  r = vfma(vfma(-b, r, splat(1.0f)), r, r);
-  f2 q = a * r;
-  q = vfma(vfma(-b, q, a), r, q);
-  return vfma(vfma(-b, q, a), r, q);
-#else
-  return a / b;
-#endif
-}
 
 struct SwDif2 {
   f2 gamma1, gamma2, k, emk, em2k, RT, Rdif, Tdif;
@@ -131,26 +81,6 @@ __device__ __forceinline__ void inc_2str2(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, 
   w1 = tauscat12 / vmax(splat(eps), tau12);
   t1 = tau12;
 }
-
-// 8-byte column-local loads and stores (g-point pair at byte offset voff, layer at soff)
-struct ColArr2 {
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ ColArr2(const float *base, size_t col_off, uint32_t bytes)
-      : r(__builtin_amdgcn_make_buffer_rsrc((void *)(base + col_off), 0, (int)bytes, 0x00020000)) {}
-  __device__ __forceinline__ f2 ld(uint32_t voff, uint32_t soff) const
-  {
-    return __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
-  }
-  __device__ __forceinline__ float ld1(uint32_t voff, uint32_t soff) const
-  {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-  }
-  __device__ __forceinline__ void st(f2 v, uint32_t voff, uint32_t soff) const
-  {
-    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, voff, soff, 0);
-  }
-};
 
 }  // namespace
 

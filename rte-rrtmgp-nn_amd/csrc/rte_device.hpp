@@ -46,6 +46,27 @@ __device__ __forceinline__ float solver_exp_neg(float x, const uint64_t *tab)
 }
 
 
+// interpolate1D of compute_Planck_source_nn (rrtmgp/kernels/mo_gas_optics_kernels.F90:1024-1043)
+__device__ __forceinline__ float interp1d(float val, float offset, float delta, int ntemp, const float *__restrict__ t)
+{
+  float val0 = (val - offset) / delta;
+  int iv = (int)val0;  // Fortran int(): truncation
+  float frac = val0 - (float)iv;
+  int index = min(ntemp - 1, max(1, iv + 1));
+  float lo = t[index - 1], hi = t[index];
+  return lo + frac * (hi - lo);
+}
+
+// Planck inputs of the LW solvers that form the sources in-kernel from the Planck fraction
+struct LwPlanck {
+  const float *tlay, *tlev, *tsfc, *totplnk;
+  int ntemp, sfc_lay;
+  float tmin, tdelta;
+};
+
+// fused Planck table size in floats, padded so the ring that follows stays 16-byte aligned
+__host__ __device__ constexpr size_t lw_btab_floats(int nbnd, int nlay) { return ((size_t)nbnd * (2 * nlay + 2) + 3) & ~(size_t)3; }
+
 // Gauss-Jacobi quadrature of the LW no-scattering solvers (secants and weights, nmus <= 4)
 struct LwAngles {
   float D[4], w[4];

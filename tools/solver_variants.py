@@ -33,7 +33,7 @@ def bind(L):
 
 
 for v in names:
-    # "name@k": variant `name` with the SW solver forced to k g-points per lane (default: by problem size)
+    # "name@s": variant `name` with the SW solver forced to s g-points per lane (0: the library's choice)
     lib, _, swk = v.partition("@")
     L = ctypes.CDLL(os.path.join(B, "lib_%s.so" % lib))
     bind(L)
