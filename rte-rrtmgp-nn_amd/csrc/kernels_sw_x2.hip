@@ -84,8 +84,16 @@ __device__ __forceinline__ void inc_2str2(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, 
 
 }  // namespace
 
+// layers of inputs in flight per lane: 3 for the NN path's g = NULL kernel (C3 -1.5 %, C4 -2 %, no spill), 2 for the
+// kernels that also read g (3 spilled there) and for the fused cloud increment (RRTMGPNN_SW2_PF_INC)
 #ifndef RRTMGPNN_SW2_PF
 #define RRTMGPNN_SW2_PF 2
+#endif
+#ifndef RRTMGPNN_SW2_PF_NOG
+#define RRTMGPNN_SW2_PF_NOG 3
+#endif
+#ifndef RRTMGPNN_SW2_PF_INC
+#define RRTMGPNN_SW2_PF_INC 2
 #endif
 #ifndef RRTMGPNN_SW2_WAVES
 #define RRTMGPNN_SW2_WAVES 4
@@ -320,13 +328,13 @@ int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
   const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
-  constexpr int PF = RRTMGPNN_SW2_PF;
+  constexpr int PF = RRTMGPNN_SW2_PF, PFN = RRTMGPNN_SW2_PF_NOG, PFI = RRTMGPNN_SW2_PF_INC;
   // rings past 64 KiB (4 columns of 224 g-points: 64.5 KiB) need the dynamic-LDS limit raised, once for all four
   // instantiations (so later calls, and hipGraph captures of them, make no attribute call)
   static bool lds_raised = false;
   if (lds > 64 * 1024 && !lds_raised) {
-    const void *ks[4] = {(const void *)sw_2stream_x2_kernel<true, true, PF>, (const void *)sw_2stream_x2_kernel<false, true, PF>,
-                         (const void *)sw_2stream_x2_kernel<true, false, PF>, (const void *)sw_2stream_x2_kernel<false, false, PF>};
+    const void *ks[4] = {(const void *)sw_2stream_x2_kernel<true, true, PF>, (const void *)sw_2stream_x2_kernel<false, true, PFI>,
+                         (const void *)sw_2stream_x2_kernel<true, false, PF>, (const void *)sw_2stream_x2_kernel<false, false, PFN>};
     for (const void *k : ks) RRTMGPNN_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lds_raised = true;
   }
@@ -337,9 +345,9 @@ int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     return RRTMGPNN_OK;
   };
   if (bands && g) return go(sw_2stream_x2_kernel<true, true, PF>, tau_bnd, ssa_bnd, g_bnd);
-  if (bands) return go(sw_2stream_x2_kernel<false, true, PF>, tau_bnd, ssa_bnd, g_bnd);
+  if (bands) return go(sw_2stream_x2_kernel<false, true, PFI>, tau_bnd, ssa_bnd, g_bnd);
   if (g) return go(sw_2stream_x2_kernel<true, false, PF>, nullptr, nullptr, nullptr);
-  return go(sw_2stream_x2_kernel<false, false, PF>, nullptr, nullptr, nullptr);
+  return go(sw_2stream_x2_kernel<false, false, PFN>, nullptr, nullptr, nullptr);
 }
 
 }  // namespace rrtmgpnn
