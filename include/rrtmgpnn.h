@@ -109,6 +109,22 @@ int rrtmgpnn_predict_nn_lw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, 
 int rrtmgpnn_predict_nn_sw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs,
                            const float *nn_inputs, const float *col_dry,
                            const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g);
+/* Fused gas optics, NN path (MI355X): compute_nn_inputs + get_col_dry + predict_nn_lw in one kernel.  The network
+ * inputs and the dry-air column amounts are formed per sample inside the MLP kernel with the expressions of
+ * rrtmgpnn_compute_nn_inputs and rrtmgpnn_get_col_dry, so nn_inputs and col_dry never touch HBM; tau and pfrac are
+ * bit-identical to the three separate calls (gas_optics_int's NN branch, rrtmgp/mo_gas_optics_rrtmgp.F90:342-391).
+ * Arguments as those calls' (gas_conc / gas_ndims HOST arrays; vmr_h2o the h2o vmr get_col_dry reads).  Networks
+ * without an in-kernel instance run the three kernels (nn_inputs and col_dry in the context workspace). */
+int rrtmgpnn_gas_optics_lw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
+                              const float *tlay, const float *plev, const float *vmr_h2o,
+                              const float *const *gas_conc, const int *gas_ndims,
+                              const rrtmgpnn_network *const *nets, int nnets, float *tau, float *pfrac);
+/* The same for the shortwave: compute_nn_inputs + get_col_dry + predict_nn_sw (gas_optics_ext's NN branch,
+ * mo_gas_optics_rrtmgp.F90:433-602); ssa / g as rrtmgpnn_predict_nn_sw. */
+int rrtmgpnn_gas_optics_sw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
+                              const float *tlay, const float *plev, const float *vmr_h2o,
+                              const float *const *gas_conc, const int *gas_ndims,
+                              const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g);
 /* Generic MLP forward (network_type%output_sgemm_flat, neural/mod_network.F90:273-354):
  * out(ny, nbatch) = net(x(nx, nbatch)), last-layer activation applied, no post-processing. */
 int rrtmgpnn_network_forward(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch,

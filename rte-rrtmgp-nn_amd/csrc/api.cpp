@@ -427,6 +427,101 @@ int rrtmgpnn_predict_nn_lw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, 
   return fail(RRTMGPNN_ERR_ARGUMENT, "predict_nn_lw: nnets must be 1 or 2");
 }
 
+// Fused gas optics (NN path): the inputs of compute_nn_inputs and get_col_dry are formed inside the MLP kernel.
+static int fused_inputs(const char *who, const rrtmgpnn_network *net, int ninputs, int nlay, const float *play,
+                        const float *tlay, const float *plev, const float *vmr_h2o, const float *const *gas_conc,
+                        const int *gas_ndims, MlpInputs &in)
+{
+  if (!net || !play || !tlay || !plev || !vmr_h2o || !gas_conc || !gas_ndims || nlay < 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, std::string(who) + ": bad argument");
+  if (ninputs != net->dims[0] || ninputs < 4 || ninputs > kMaxInputs)
+    return fail(RRTMGPNN_ERR_ARGUMENT, std::string(who) + ": ninputs does not match the network");
+  if (!gas_conc[2] || !gas_conc[3] || gas_ndims[2] != 2 || gas_ndims[3] != 2)
+    return fail(RRTMGPNN_ERR_ARGUMENT, std::string(who) + ": inputs 3 (h2o) and 4 (o3) must be 2-D (nlay,ncol)");
+  in = MlpInputs{};
+  in.play = play; in.tlay = tlay; in.plev = plev; in.h2o = vmr_h2o; in.nlay = nlay;
+  for (int k = 0; k < ninputs; k++) {
+    in.gas.p[k] = k >= 2 ? gas_conc[k] : nullptr;
+    in.gas.nd[k] = k >= 2 ? gas_ndims[k] : 0;
+    if (k >= 2 && in.gas.p[k] && (in.gas.nd[k] < 0 || in.gas.nd[k] > 2))
+      return fail(RRTMGPNN_ERR_ARGUMENT, std::string(who) + ": gas_ndims must be 0, 1 or 2");
+    in.mn[k] = net->in_min[k];
+    in.mx[k] = net->in_max[k];
+  }
+  return RRTMGPNN_OK;
+}
+
+// no in-kernel-input instance for these networks: compute_nn_inputs + get_col_dry into the context workspace, then
+// the MLP on them (the same kernels as the separate entries)
+static int fused_fallback(rrtmgpnn_context *ctx, int ncol, int nlay, const MlpInputs &in, int ninputs,
+                          const float **x, const float **col_dry)
+{
+  const size_t N = (size_t)ncol * nlay;
+  void *ws = nullptr;
+  if (int rc = ctx->workspace(sizeof(float) * N * (ninputs + 1), &ws)) return rc;
+  float *xw = (float *)ws, *cw = xw + N * ninputs;
+  std::vector<float> mm(2 * ninputs);
+  for (int k = 0; k < ninputs; k++) { mm[k] = in.mn[k]; mm[ninputs + k] = in.mx[k]; }
+  if (int rc = launch_nn_inputs(ctx, ncol, nlay, ninputs, in.play, in.tlay, in.gas, mm.data(), xw)) return rc;
+  if (int rc = launch_col_dry(ctx, ncol, nlay, in.h2o, in.plev, cw)) return rc;
+  *x = xw;
+  *col_dry = cw;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_gas_optics_lw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
+                              const float *tlay, const float *plev, const float *vmr_h2o,
+                              const float *const *gas_conc, const int *gas_ndims,
+                              const rrtmgpnn_network *const *nets, int nnets, float *tau, float *pfrac)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!nets || !nets[0] || !tau || !pfrac || ncol < 0 || ngpt < 1 || (nnets != 1 && nnets != 2))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_lw_nn: bad argument");
+  MlpInputs in;
+  if (int rc = fused_inputs("gas_optics_lw_nn", nets[0], ninputs, nlay, play, tlay, plev, vmr_h2o, gas_conc, gas_ndims,
+                            in))
+    return rc;
+  if (ncol == 0) return RRTMGPNN_OK;
+  const long long N = (long long)ncol * nlay;
+  if (nnets == 2) {
+    const rrtmgpnn_network *A = nets[0], *B = nets[1];
+    if (!B || B->dims[0] != ninputs || A->dims[A->nlayers] != ngpt || B->dims[B->nlayers] != ngpt)
+      return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_lw_nn: network sizes do not match (ninputs, ngpt)");
+    if (!A->has_out_scaling()) return fail(RRTMGPNN_ERR_ARGUMENT, "output_sgemm_tau: NN output scaling coefficients missing");
+    const int rc = launch_mlp(ctx, MLP_LW_PAIR, A, B, N, ngpt, nullptr, nullptr, tau, pfrac, nullptr, &in);
+    if (rc != RRTMGPNN_ERR_UNSUPPORTED) return rc;
+  }
+  const float *x = nullptr, *cd = nullptr;
+  if (int rc = fused_fallback(ctx, ncol, nlay, in, ninputs, &x, &cd)) return rc;
+  return rrtmgpnn_predict_nn_lw(ctx, ncol, nlay, ngpt, ninputs, x, cd, nets, nnets, tau, pfrac);
+}
+
+int rrtmgpnn_gas_optics_sw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
+                              const float *tlay, const float *plev, const float *vmr_h2o,
+                              const float *const *gas_conc, const int *gas_ndims,
+                              const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!nets || !nets[0] || !tau || ncol < 0 || ngpt < 1) return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_sw_nn: bad argument");
+  MlpInputs in;
+  if (int rc = fused_inputs("gas_optics_sw_nn", nets[0], ninputs, nlay, play, tlay, plev, vmr_h2o, gas_conc, gas_ndims,
+                            in))
+    return rc;
+  if (ncol == 0) return RRTMGPNN_OK;
+  const long long N = (long long)ncol * nlay;
+  const rrtmgpnn_network *A = nets[0], *B = ssa ? nets[1] : nullptr;
+  if (ssa) {
+    if (!B || B->dims[0] != ninputs || A->dims[A->nlayers] != ngpt || B->dims[B->nlayers] != ngpt ||
+        !A->has_out_scaling() || !B->has_out_scaling())
+      return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_sw_nn: absorption / Rayleigh networks missing or inconsistent");
+    const int rc = launch_mlp(ctx, MLP_SW_PAIR, A, B, N, ngpt, nullptr, nullptr, tau, ssa, g, &in);
+    if (rc != RRTMGPNN_ERR_UNSUPPORTED) return rc;
+  }
+  const float *x = nullptr, *cd = nullptr;
+  if (int rc = fused_fallback(ctx, ncol, nlay, in, ninputs, &x, &cd)) return rc;
+  return rrtmgpnn_predict_nn_sw(ctx, ncol, nlay, ngpt, ninputs, x, cd, nets, tau, ssa, g);
+}
+
 int rrtmgpnn_predict_nn_sw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *nn_inputs,
                            const float *col_dry, const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g)
 {

@@ -105,9 +105,16 @@ int launch_col_dry(rrtmgpnn_context *ctx, int ncol, int nlay, const float *h2o, 
 int launch_tlev(rrtmgpnn_context *ctx, int ncol, int nlay, const float *play, const float *plev, const float *tlay,
                 float *tlev);
 enum MlpMode { MLP_PLAIN = 0, MLP_LW_PAIR = 1, MLP_SW_PAIR = 2, MLP_SW_ABS = 3, MLP_LW_BOTH = 4 };
+// state the MLP kernel forms its inputs from (fused gas optics): compute_nn_inputs + get_col_dry in-kernel
+struct MlpInputs {
+  const float *play, *tlay, *plev, *h2o;
+  int nlay;
+  GasArgs gas;
+  float mn[kMaxInputs], mx[kMaxInputs];
+};
 int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
                long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
-               float *out2);
+               float *out2, const MlpInputs *in = nullptr);
 int launch_mlp_generic(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch, const float *x,
                        float *out);
 int pack_network(rrtmgpnn_network *net);

@@ -84,19 +84,25 @@ __global__ void __launch_bounds__(kInThreads) nn_inputs_kernel(int ncol, int nla
   for (int i = threadIdx.x; i < nx * ns; i += kInThreads) dst[i] = st[i];
 }
 
+// get_col_dry for one (layer, column): h2o vmr v and the layer's two level pressures (shared by col_dry_kernel and
+// the MLP kernel's in-kernel form, so both give the same bits)
+__device__ __forceinline__ float col_dry_of(float v, float p_a, float p_b)
+{
+  const float m_dry = 0.028964f, m_h2o = 0.018016f, avogad = 6.02214076e23f, grav = 9.80665f;
+  float delta_plev = fabsf(p_a - p_b);
+  float fact = 1.0f / (1.0f + v);
+  float m_air = (m_dry + m_h2o * v) * fact;
+  return 10.0f * delta_plev * avogad * fact / (1000.0f * m_air * 100.0f * grav);
+}
+
 __global__ void col_dry_kernel(int ncol, int nlay, const float *__restrict__ h2o, const float *__restrict__ plev,
                                float *__restrict__ col_dry)
 {
   long long s = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= (long long)ncol * nlay) return;
   int icol = (int)(s / nlay), ilev = (int)(s % nlay);
-  const float m_dry = 0.028964f, m_h2o = 0.018016f, avogad = 6.02214076e23f, grav = 9.80665f;
   const float *pl = plev + (size_t)(nlay + 1) * icol;
-  float v = h2o[s];
-  float delta_plev = fabsf(pl[ilev] - pl[ilev + 1]);
-  float fact = 1.0f / (1.0f + v);
-  float m_air = (m_dry + m_h2o * v) * fact;
-  col_dry[s] = 10.0f * delta_plev * avogad * fact / (1000.0f * m_air * 100.0f * grav);
+  col_dry[s] = col_dry_of(h2o[s], pl[ilev], pl[ilev + 1]);
 }
 
 __global__ void tlev_kernel(int ncol, int nlay, const float *__restrict__ play, const float *__restrict__ plev,
@@ -294,6 +300,11 @@ struct MlpArgs {
   int vec4;    // outputs may be stored 16 bytes at a time (ngpt % 4 == 0, 16-byte aligned arrays)
   int actA[3], actB[3];
   long long nbatch;
+  // in-kernel inputs (MlpInputs, the fused gas-optics entries): x and col_dry formed per sample from the state
+  const float *play, *tlay, *plev, *h2o;
+  int nlay;
+  GasArgs gas;
+  NnInArgs sc;
 };
 
 __device__ __forceinline__ float pow8(float t)
@@ -373,7 +384,11 @@ constexpr int kMlpThreads = RRTMGPNN_MLP_THREADS, kGoUnroll = RRTMGPNN_MLP_GO_UN
 #define RRTMGPNN_MLP_CT_UNROLL_SW 2
 #endif
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0>
+// XIN: the inputs are formed in-kernel (compute_nn_inputs + get_col_dry per sample, the expressions of
+// nn_inputs_kernel and col_dry_kernel) instead of read from nn_inputs / col_dry arrays.  Lane (j, q) needs inputs
+// k = 4t + q of sample s0 + j: the raw state values are loaded a tile ahead (with the next tile's prefetch) and
+// turned into inputs at the tile's start.
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0, bool XIN = false>
 __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -394,33 +409,88 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
   const long long ntiles = (a.nbatch + 15) / 16;
 
   const long long tstride = (long long)gridDim.x * nwaves;
-  // Layer-1 B operand: x[sample s0+j][k = 4t+q]
-  auto load_x = [&](long long tl, float (&xv)[AK]) {
+  // Layer-1 B operand: x[sample s0+j][k = 4t+q].  XIN: raw[t] holds the state value input k is formed from
+  // (t = 0: tlay, play, h2o or o3 by q; t > 0: gas 4t+q), raw[AK..AK+2] = h2o, p(lev ilay), p(lev ilay+1) for col_dry.
+  constexpr int NR = XIN ? AK + 3 : AK;
+  auto load_x = [&](long long tl, float (&xv)[NR]) {
     const long long s = tl * 16 + j;
+    if constexpr (XIN) {
+      const bool ok = s < a.nbatch;
+      const long long sc = ok ? s : 0;
+      const int ilay = (int)(sc % a.nlay);
+      const long long icol = sc / a.nlay;
+      // inputs 3, 4 (h2o, o3) are 2-D; constant indices keep the pointers in SGPRs (a lane index would spill them)
+      const float *p0 = q == 0 ? a.tlay : (q == 1 ? a.play : (q == 2 ? a.gas.p[2] : a.gas.p[3]));
+      xv[0] = (ok && q < nx) ? p0[sc] : 0.0f;
 #pragma unroll
-    for (int t = 0; t < AK; t++) {
-      int k = 4 * t + q;
-      xv[t] = (s < a.nbatch && k < nx) ? a.x[(size_t)s * nx + k] : 0.0f;
+      for (int t = 1; t < AK; t++) {
+        const int k = 4 * t + q;
+        const float *pk = a.gas.p[4 * t];
+        int nd = a.gas.nd[4 * t];
+#pragma unroll
+        for (int r = 1; r < 4; r++)
+          if (q == r) { pk = a.gas.p[4 * t + r]; nd = a.gas.nd[4 * t + r]; }
+        const long long idx = nd == 0 ? 0 : (nd == 1 ? (long long)ilay : sc);
+        xv[t] = (ok && k < nx && pk) ? pk[idx] : 0.0f;
+      }
+      const float *pl = a.plev + (size_t)(a.nlay + 1) * icol;
+      xv[AK] = ok ? a.h2o[sc] : 0.0f;
+      xv[AK + 1] = ok ? pl[ilay] : 0.0f;
+      xv[AK + 2] = ok ? pl[ilay + 1] : 1.0f;
+    } else {
+#pragma unroll
+      for (int t = 0; t < AK; t++) {
+        int k = 4 * t + q;
+        xv[t] = (s < a.nbatch && k < nx) ? a.x[(size_t)s * nx + k] : 0.0f;
+      }
     }
   };
-  float xn[AK];  // NGTC: the next tile's inputs, loaded before this tile's stores
+  // XIN: compute_nn_inputs (nn_inputs_kernel's expressions) from the raw values, in place; returns col_dry
+  auto form_x = [&](float (&xv)[NR]) -> float {
+    if constexpr (XIN) {
+      const float r0 = xv[0];
+      const float v0 = q == 1 ? ref_logf(r0) : (q >= 2 ? sqrtf(sqrtf(r0)) : r0);
+      float mn = a.sc.mn[0], mx = a.sc.mx[0];
+#pragma unroll
+      for (int r = 1; r < 4; r++)
+        if (q == r) { mn = a.sc.mn[r]; mx = a.sc.mx[r]; }
+      xv[0] = q < nx ? (v0 - mn) / (mx - mn) : 0.0f;
+#pragma unroll
+      for (int t = 1; t < AK; t++) {
+        const int k = 4 * t + q;
+        float mnk = a.sc.mn[4 * t], mxk = a.sc.mx[4 * t];
+#pragma unroll
+        for (int r = 1; r < 4; r++)
+          if (q == r && 4 * t + r < kMaxInputs) { mnk = a.sc.mn[4 * t + r]; mxk = a.sc.mx[4 * t + r]; }
+        xv[t] = k < nx ? (xv[t] - mnk) / (mxk - mnk) : 0.0f;
+      }
+      return col_dry_of(xv[AK], xv[AK + 1], xv[AK + 2]);
+    } else {
+      return 0.0f;
+    }
+  };
+  float xn[NR];  // NGTC: the next tile's inputs, loaded before this tile's stores
   if constexpr (NGTC > 0) load_x((long long)blockIdx.x * nwaves + wave, xn);
   for (long long tile = (long long)blockIdx.x * nwaves + wave; tile < ntiles; tile += tstride) {
     const long long s0 = tile * 16;
-    float xv[AK];
+    float xv[NR];
     if constexpr (NGTC > 0) {
 #pragma unroll
-      for (int t = 0; t < AK; t++) xv[t] = xn[t];
+      for (int t = 0; t < NR; t++) xv[t] = xn[t];
       load_x(tile + tstride, xn);
     } else {
       load_x(tile, xv);
     }
+    const float cd_in = form_x(xv);
+    float x1[AK];
+#pragma unroll
+    for (int t = 0; t < AK; t++) x1[t] = xv[t];
     floatx4 hA[AH2];
-    mlp_hidden<AK, AH1, AH2, ACTS>(imgA, NGT, xv, lane, a.actA[0], a.actA[1], hA);
+    mlp_hidden<AK, AH1, AH2, ACTS>(imgA, NGT, x1, lane, a.actA[0], a.actA[1], hA);
     floatx4 hB[BH2];
     if constexpr (MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) {
       static_assert(BK == AK, "paired networks share their inputs");
-      mlp_hidden<BK, BH1, BH2, ACTS>(imgB, NGT, xv, lane, a.actB[0], a.actB[1], hB);
+      mlp_hidden<BK, BH1, BH2, ACTS>(imgB, NGT, x1, lane, a.actB[0], a.actB[1], hB);
     }
     // Layer 3 runs with the weights as the A operand (rows = g-points) and the hidden activations as B
     // (columns = samples): lane (j, q) holds g = 16go + 4q + r, r = 0..3, of sample s0 + j, so each lane
@@ -428,7 +498,8 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
     const long long s = s0 + j;
     const bool sok = s < a.nbatch;
     float cd = 0.0f;
-    if constexpr (MODE != MLP_PLAIN) cd = sok ? a.col_dry[s] : 0.0f;
+    if constexpr (XIN) cd = sok ? cd_in : 0.0f;
+    else if constexpr (MODE != MLP_PLAIN) cd = sok ? a.col_dry[s] : 0.0f;
     // 4 consecutive g of one sample: one 16-byte store when the row allows it, else element by element
     auto put4 = [&](float *out, int row, int gc, const floatx4 &v) {
       if (!sok) return;
@@ -539,10 +610,10 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
   }
 }
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0>
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0, bool XIN = false>
 static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
 {
-  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS, NGTC>;
+  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS, NGTC, XIN>;
   size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
   // Raise the dynamic-LDS limit once per instantiation (kept out of the per-call path so the launch
@@ -576,13 +647,17 @@ static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
     constexpr bool lw = MODE == MLP_LW_PAIR && AK == 5 && AH1 == 4 && AH2 == 4 && BH1 == 1 && BH2 == 1;
     constexpr bool sw = MODE == MLP_SW_PAIR && AK == 2 && AH1 == 1 && AH2 == 1 && BH1 == 1 && BH2 == 1;
     if constexpr (RRTMGPNN_MLP_NGT_CT && lw) {
+      if (a.ngt == 16 && a.play) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16, true>(ctx, a);
       if (a.ngt == 16) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16>(ctx, a);
     }
     if constexpr (RRTMGPNN_MLP_NGT_CT && sw) {
+      if (a.ngt == 14 && a.play) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 14, true>(ctx, a);
       if (a.ngt == 14) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 14>(ctx, a);
     }
+    if (a.play) return RRTMGPNN_ERR_UNSUPPORTED;  // no in-kernel-input instance: the caller runs the three kernels
     return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1>(ctx, a);
   }
+  if (a.play) return RRTMGPNN_ERR_UNSUPPORTED;
   return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 0>(ctx, a);
 }
 
@@ -606,7 +681,8 @@ static bool shape_is(const rrtmgpnn_network *n, int k, int h1, int h2)
 }
 
 int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
-               long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1, float *out2)
+               long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1, float *out2,
+               const MlpInputs *in)
 {
   if (nbatch <= 0) return RRTMGPNN_OK;
   if (!A || !A->d_packed) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: network has no MFMA image (needs 3 layers)");
@@ -619,6 +695,12 @@ int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, c
   a.imgA = A->d_packed; a.imgA_floats = A->packed_floats;
   a.imgB = paired ? B->d_packed : nullptr; a.imgB_floats = paired ? B->packed_floats : 0;
   a.nx = A->dims[0]; a.ngpt = ngpt; a.ngt = A->ngt; a.nbatch = nbatch;
+  if (in) {  // fused gas optics: x and col_dry formed in-kernel (returns RRTMGPNN_ERR_UNSUPPORTED, no error set,
+             // when no such instance exists for the shape; the caller then runs the separate kernels)
+    a.play = in->play; a.tlay = in->tlay; a.plev = in->plev; a.h2o = in->h2o; a.nlay = in->nlay;
+    a.gas = in->gas;
+    for (int k = 0; k < kMaxInputs; k++) { a.sc.mn[k] = in->mn[k]; a.sc.mx[k] = in->mx[k]; }
+  }
   auto al16 = [](const float *p) { return ((uintptr_t)p & 15) == 0; };
   a.vec4 = (ngpt % 4 == 0) && al16(out0) && (!out1 || al16(out1)) && (!out2 || al16(out2));
   for (int i = 0; i < 3; i++) { a.actA[i] = A->act[i]; a.actB[i] = paired ? B->act[i] : 0; }

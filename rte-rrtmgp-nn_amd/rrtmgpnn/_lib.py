@@ -40,6 +40,10 @@ SIGNATURES = {
     "rrtmgpnn_interpolate_tlev": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_predict_nn_lw": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, P(c_vp), c_int, c_vp, c_vp]),
     "rrtmgpnn_predict_nn_sw": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, P(c_vp), c_vp, c_vp, c_vp]),
+    "rrtmgpnn_gas_optics_lw_nn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, P(c_vp), P(c_int),
+                                          P(c_vp), c_int, c_vp, c_vp]),
+    "rrtmgpnn_gas_optics_sw_nn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, P(c_vp), P(c_int),
+                                          P(c_vp), c_vp, c_vp, c_vp]),
     "rrtmgpnn_network_forward": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),
     "rrtmgpnn_compute_planck_source_nn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                                   P(c_int), c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -124,15 +124,25 @@ class ClearSkyStep:
         self._Ds, self._W = float_array(GAUSS_DS[nmus]), float_array(GAUSS_WTS[nmus])
         self.nmus = nmus
         c = self.ctx.h
-        self.calls = [
-            ("get_col_dry", L.rrtmgpnn_get_col_dry, (c, ncol, nlay, p(self.gases["h2o"]), p(self.plev), p(self.col_dry))),
-            ("nn_inputs_lw", L.rrtmgpnn_compute_nn_inputs,
-             (c, ncol, nlay, self.nx_lw, p(self.play), p(self.tlay), self._g_lw, self._nd_lw, self.lw_nets[0],
-              p(self.x_lw))),
-            ("predict_nn_lw", L.rrtmgpnn_predict_nn_lw,
-             (c, ncol, nlay, self.ng_lw, self.nx_lw, p(self.x_lw), p(self.col_dry), self._nets_lw, len(self.lw_nets),
-              p(self.tau_lw), p(self.lay_src))),
-        ]
+        if fused:
+            # compute_nn_inputs + get_col_dry + predict_nn_lw in one kernel (rrtmgpnn_gas_optics_lw_nn): the network
+            # inputs and column amounts are formed in-kernel and never stored (same bits as the three calls)
+            self.calls = [
+                ("predict_nn_lw", L.rrtmgpnn_gas_optics_lw_nn,
+                 (c, ncol, nlay, self.ng_lw, self.nx_lw, p(self.play), p(self.tlay), p(self.plev), p(self.gases["h2o"]),
+                  self._g_lw, self._nd_lw, self._nets_lw, len(self.lw_nets), p(self.tau_lw), p(self.lay_src))),
+            ]
+        else:
+            self.calls = [
+                ("get_col_dry", L.rrtmgpnn_get_col_dry,
+                 (c, ncol, nlay, p(self.gases["h2o"]), p(self.plev), p(self.col_dry))),
+                ("nn_inputs_lw", L.rrtmgpnn_compute_nn_inputs,
+                 (c, ncol, nlay, self.nx_lw, p(self.play), p(self.tlay), self._g_lw, self._nd_lw, self.lw_nets[0],
+                  p(self.x_lw))),
+                ("predict_nn_lw", L.rrtmgpnn_predict_nn_lw,
+                 (c, ncol, nlay, self.ng_lw, self.nx_lw, p(self.x_lw), p(self.col_dry), self._nets_lw,
+                  len(self.lw_nets), p(self.tau_lw), p(self.lay_src))),
+            ]
         if fused:
             # compute_Planck_source_nn fused into the LW solver (sources formed in-kernel from pfrac); all-sky:
             # the cloud increment by band is added as tau is read (rrtmgpnn_lw_solver_noscat_planck_inc)
@@ -176,14 +186,21 @@ class ClearSkyStep:
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
         g_sw = None if fused else p(self.g_sw)
-        self.calls += [
-            ("nn_inputs_sw", L.rrtmgpnn_compute_nn_inputs,
-             (c, ncol, nlay, self.nx_sw, p(self.play), p(self.tlay), self._g_sw, self._nd_sw, self.sw_nets[0],
-              p(self.x_sw))),
-            ("predict_nn_sw", L.rrtmgpnn_predict_nn_sw,
-             (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.x_sw), p(self.col_dry), self._nets_sw, p(self.tau_sw),
-              p(self.ssa_sw), g_sw)),
-        ]
+        if fused:
+            self.calls += [
+                ("predict_nn_sw", L.rrtmgpnn_gas_optics_sw_nn,
+                 (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.play), p(self.tlay), p(self.plev), p(self.gases["h2o"]),
+                  self._g_sw, self._nd_sw, self._nets_sw, p(self.tau_sw), p(self.ssa_sw), g_sw)),
+            ]
+        else:
+            self.calls += [
+                ("nn_inputs_sw", L.rrtmgpnn_compute_nn_inputs,
+                 (c, ncol, nlay, self.nx_sw, p(self.play), p(self.tlay), self._g_sw, self._nd_sw, self.sw_nets[0],
+                  p(self.x_sw))),
+                ("predict_nn_sw", L.rrtmgpnn_predict_nn_sw,
+                 (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.x_sw), p(self.col_dry), self._nets_sw, p(self.tau_sw),
+                  p(self.ssa_sw), g_sw)),
+            ]
         if self.allsky:  # clouds%delta_scale(); clouds%increment(atmos) before rte_sw (rrtmgp_allsky.F90:420-433)
             self.calls += [
                 ("cloud_optics_sw", L.rrtmgpnn_cloud_optics_compute,
@@ -217,7 +234,8 @@ class ClearSkyStep:
             # solver held while the LW solver, which needs it, could not start
             order = {n: i for i, n in enumerate(FUSED_ORDER)}
             self.calls.sort(key=lambda c: order.get(c[0], len(order)))
-        # overlap: the SW chain runs on a second context/stream, forked after col_dry (which both streams read)
+        # overlap: the SW chain runs on a second context/stream, forked after col_dry (which both streams read; the
+        # fused step, whose chains form col_dry each in their network kernel, forks at its start)
         # and joined at the end of the step -- the VALU-bound SW solver shares the CUs with the MFMA-bound LW
         # network and the LW solver instead of running after them
         self.overlap = overlap
@@ -256,6 +274,10 @@ class ClearSkyStep:
     def step(self, timing=None):
         """Issue one step.  timing: a dict name -> list; each launch is then bracketed by timing events recorded on
         the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended."""
+        fork_after = "get_col_dry" if any(n == "get_col_dry" for n, _, _ in self.calls) else None
+        if self.overlap and fork_after is None:  # fused step: the chains share no kernel; fork at the start
+            self._fork.record(self.ctx.stream)
+            self.ctx2.stream.wait_event(self._fork)
         for name, fn, args in self.calls:
             if timing is not None:
                 s = self.stream_for(name)
@@ -267,7 +289,7 @@ class ClearSkyStep:
             if timing is not None:
                 e1.record(s)
                 timing.setdefault(name, []).append((e0, e1))
-            if self.overlap and name == "get_col_dry":
+            if self.overlap and name == fork_after:
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
         if self.overlap:

@@ -106,6 +106,56 @@ def test_fused_step_equals_class_sequence(dev, rfmip):
         np.testing.assert_array_equal(res[0][k], res[1][k], err_msg=k)
 
 
+@pytest.mark.parametrize("ncol", [1, 37, 1800])
+def test_fused_gas_optics_equals_separate_calls(dev, rfmip, ncol):
+    """rrtmgpnn_gas_optics_{lw,sw}_nn (network inputs and col_dry formed inside the MLP kernel) == compute_nn_inputs +
+    get_col_dry + predict_nn_{lw,sw}, bit for bit; the LW g128 'both' model (no in-kernel instance) takes the
+    fallback through the context workspace and matches too."""
+    from rrtmgpnn import _lib, data
+    from rrtmgpnn._lib import check, ptr_array
+    from rrtmgpnn.pipeline import ClearSkyStep
+    prob = subset(rfmip, np.arange(ncol) * 7 % 1800)
+    st = ClearSkyStep(prob, device=0, fused=False, overlap=False)
+    L, c, p = _lib.lib(), st.ctx.h, (lambda t: t.data_ptr())
+    nl, nc = st.nlay, st.ncol
+    for name in ("get_col_dry", "nn_inputs_lw", "predict_nn_lw", "nn_inputs_sw", "predict_nn_sw"):
+        fn, args = next((f, a) for n, f, a in st.calls if n == name)
+        check(fn(*args), name)
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)]
+    got = [torch.full_like(t, float("nan")) for t in ref]
+    check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, st.ng_lw, st.nx_lw, p(st.play), p(st.tlay), p(st.plev),
+                                      p(st.gases["h2o"]), st._g_lw, st._nd_lw, st._nets_lw, len(st.lw_nets),
+                                      p(got[0]), p(got[1])), "gas_optics_lw_nn")
+    check(L.rrtmgpnn_gas_optics_sw_nn(c, nc, nl, st.ng_sw, st.nx_sw, p(st.play), p(st.tlay), p(st.plev),
+                                      p(st.gases["h2o"]), st._g_sw, st._nd_sw, st._nets_sw, p(got[2]), p(got[3]), None),
+          "gas_optics_sw_nn")
+    torch.cuda.synchronize()
+    for k, (a, b) in enumerate(zip(ref, got)):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=str(k))
+    # the g128 single-output model (18-64-64-256, no in-kernel instance): nn_inputs + col_dry in the workspace
+    from rrtmgpnn._lib import int_array
+    hb = _lib.c_vp()
+    check(L.rrtmgpnn_network_load(c, data.path("lw_g128_both").encode(), hb), "network_load")
+    names = data.rbin.unchars(data.load_model("lw_g128_both")["input_names"])
+    g_b = ptr_array([st.gases[n].data_ptr() if (k >= 2 and n in st.gases) else None for k, n in enumerate(names)])
+    nd_b = int_array([2] * len(names))
+    nets_b = ptr_array([hb.value])
+    nx = len(names)
+    x = torch.empty((nc, nl, nx), device=dev)
+    cd = torch.empty((nc, nl), device=dev)
+    out = [torch.full((nc, nl, 128), float("nan"), device=dev) for _ in range(4)]
+    check(L.rrtmgpnn_compute_nn_inputs(c, nc, nl, nx, p(st.play), p(st.tlay), g_b, nd_b, hb, p(x)), "nn_inputs")
+    check(L.rrtmgpnn_get_col_dry(c, nc, nl, p(st.gases["h2o"]), p(st.plev), p(cd)), "col_dry")
+    check(L.rrtmgpnn_predict_nn_lw(c, nc, nl, 128, nx, p(x), p(cd), nets_b, 1, p(out[0]), p(out[1])), "predict")
+    check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, 128, nx, p(st.play), p(st.tlay), p(st.plev), p(st.gases["h2o"]),
+                                      g_b, nd_b, nets_b, 1, p(out[2]), p(out[3])), "gas_optics_lw_nn both")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out[0].cpu().numpy(), out[2].cpu().numpy())
+    np.testing.assert_array_equal(out[1].cpu().numpy(), out[3].cpu().numpy())
+    L.rrtmgpnn_network_destroy(hb)
+
+
 @pytest.mark.parametrize("allsky", [False, True])
 def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky):
     """LW and SW chains on two streams (fork after col_dry, join at the end), eager and as one hipGraph, give the
