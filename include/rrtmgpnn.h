@@ -150,13 +150,15 @@ int rrtmgpnn_lw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int nco
  * + lw_solver_noscat_GaussQuad in one kernel.  Takes the Planck fraction (what predict_nn_lw writes into
  * lay_source) instead of lay/lev/sfc sources, forms every source in-kernel with the same products as
  * rrtmgpnn_compute_planck_source_nn, and never stores them: fluxes are bit-identical to
- * compute_planck_source_nn followed by lw_solver_noscat.  band_lims_gpt HOST (2,nbnd); totplnk DEVICE. */
+ * compute_planck_source_nn followed by lw_solver_noscat.  band_lims_gpt HOST (2,nbnd); totplnk DEVICE.
+ * emis_by_band == 0: sfc_emis is (ngpt, ncol) per g-point; 1: (nbnd, ncol) by band, as rte_lw takes it, expanded
+ * in-kernel (expand, rte/mo_rte_lw.F90:429-447: the same values, no band-to-g-point array in HBM). */
 int rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
                                      const float *Ds, const float *weights, const float *inc_flux, const float *tau,
                                      const float *pfrac, int nbnd, int nPlanckTemp, const float *tlay,
                                      const float *tlev, const float *tsfc, int sfc_lay, const int *band_lims_gpt,
                                      float temp_ref_min, float totplnk_delta, const float *totplnk,
-                                     const float *sfc_emis_gpt, float *flux_up, float *flux_dn);
+                                     int emis_by_band, const float *sfc_emis, float *flux_up, float *flux_dn);
 /* rrtmgpnn_lw_solver_noscat_planck with the atmosphere incremented by a band-resolved absorption optical depth
  * tau_bnd (nbnd, nlay, ncol), e.g. cloud optics: the same fluxes as rrtmgpnn_increment_bybnd (1scl by 1scl)
  * followed by rrtmgpnn_lw_solver_noscat_planck, but the g-point tau array is only read (it is left as it was). */
@@ -165,8 +167,8 @@ int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nl
                                          const float *tau, const float *tau_bnd, const float *pfrac, int nbnd,
                                          int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
                                          int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
-                                         float totplnk_delta, const float *totplnk, const float *sfc_emis_gpt,
-                                         float *flux_up, float *flux_dn);
+                                         float totplnk_delta, const float *totplnk, int emis_by_band,
+                                         const float *sfc_emis, float *flux_up, float *flux_dn);
 /* rte_lw on two-stream optical properties, default branch (rte/mo_rte_lw.F90:372-387): lw_solver_noscat_GaussQuad
  * with do_rescaling -- tau scaled by (1 - ssa + ssa(1-g)/2), a no-scattering pass down, then
  * lw_transport_1rescl up and down again with the adjustment terms (rte/kernels/mo_rte_solver_kernels.F90:209-233,

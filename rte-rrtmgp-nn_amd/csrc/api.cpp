@@ -583,18 +583,20 @@ int rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, 
                                      const float *pfrac, int nbnd, int nPlanckTemp, const float *tlay,
                                      const float *tlev, const float *tsfc, int sfc_lay, const int *band_lims_gpt,
                                      float temp_ref_min, float totplnk_delta, const float *totplnk,
-                                     const float *sfc_emis_gpt, float *flux_up, float *flux_dn)
+                                     int emis_by_band, const float *sfc_emis, float *flux_up, float *flux_dn)
 {
   if (int rc = check_ctx(ctx)) return rc;
-  if (!Ds || !weights || !tau || !pfrac || !tlay || !tlev || !tsfc || !totplnk || !sfc_emis_gpt || !flux_up ||
+  if (!Ds || !weights || !tau || !pfrac || !tlay || !tlev || !tsfc || !totplnk || !sfc_emis || !flux_up ||
       !flux_dn || ngpt < 1 || nlay < 1 || ncol < 0 || nPlanckTemp < 2 || sfc_lay < 1 || sfc_lay > nlay ||
       !(totplnk_delta > 0.0f))
     return fail(RRTMGPNN_ERR_ARGUMENT, "lw_solver_noscat_planck: bad argument");
   BandArgs b;
   if (int rc = band_args(nbnd, band_lims_gpt, ngpt, b)) return rc;
+  if (emis_by_band)
+    if (int rc = bands_cover(b, ngpt)) return rc;
   return launch_lw_noscat_planck(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, pfrac,
                                  nPlanckTemp, tlay, tlev, tsfc, sfc_lay, b, temp_ref_min, totplnk_delta, totplnk,
-                                 sfc_emis_gpt, nullptr, flux_up, flux_dn);
+                                 emis_by_band != 0, sfc_emis, nullptr, flux_up, flux_dn);
 }
 
 int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
@@ -602,11 +604,11 @@ int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nl
                                          const float *tau, const float *tau_bnd, const float *pfrac, int nbnd,
                                          int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
                                          int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
-                                         float totplnk_delta, const float *totplnk, const float *sfc_emis_gpt,
-                                         float *flux_up, float *flux_dn)
+                                         float totplnk_delta, const float *totplnk, int emis_by_band,
+                                         const float *sfc_emis, float *flux_up, float *flux_dn)
 {
   if (int rc = check_ctx(ctx)) return rc;
-  if (!Ds || !weights || !tau || !tau_bnd || !pfrac || !tlay || !tlev || !tsfc || !totplnk || !sfc_emis_gpt ||
+  if (!Ds || !weights || !tau || !tau_bnd || !pfrac || !tlay || !tlev || !tsfc || !totplnk || !sfc_emis ||
       !flux_up || !flux_dn || ngpt < 1 || nlay < 1 || ncol < 0 || nPlanckTemp < 2 || sfc_lay < 1 || sfc_lay > nlay ||
       !(totplnk_delta > 0.0f))
     return fail(RRTMGPNN_ERR_ARGUMENT, "lw_solver_noscat_planck_inc: bad argument");
@@ -615,7 +617,7 @@ int rrtmgpnn_lw_solver_noscat_planck_inc(rrtmgpnn_context *ctx, int ngpt, int nl
   if (int rc = bands_cover(b, ngpt)) return rc;
   return launch_lw_noscat_planck(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, pfrac,
                                  nPlanckTemp, tlay, tlev, tsfc, sfc_lay, b, temp_ref_min, totplnk_delta, totplnk,
-                                 sfc_emis_gpt, tau_bnd, flux_up, flux_dn);
+                                 emis_by_band != 0, sfc_emis, tau_bnd, flux_up, flux_dn);
 }
 
 int rrtmgpnn_lw_solver_1rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,

@@ -135,8 +135,8 @@ int launch_lw_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol,
                             const float *Ds, const float *wts, const float *inc_flux, const float *tau,
                             const float *pfrac, int ntemp, const float *tlay, const float *tlev, const float *tsfc,
                             int sfc_lay, const BandArgs &bands, float temp_ref_min, float totplnk_delta,
-                            const float *totplnk, const float *sfc_emis, const float *tau_bnd, float *flux_up,
-                            float *flux_dn);
+                            const float *totplnk, bool emis_by_band, const float *sfc_emis, const float *tau_bnd,
+                            float *flux_up, float *flux_dn);
 // bands != nullptr: atmosphere incremented by the band-resolved 2str set (tau, ssa, g)_bnd in-kernel
 int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                       const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,

@@ -221,7 +221,10 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     ss = on ? sfc[g + (size_t)ngpt * icol] : 0.0f;
   }
   const float tau_thresh = sqrtf(FLT_EPSILON);
-  const float e = on ? emis[g + (size_t)ngpt * icol] : 0.0f;
+  // emissivity per g-point, or (fused, emis_by_band) the band value rte_lw's expand would copy there
+  const float e = !on ? 0.0f
+                      : (kFused && pl.emis_by_band ? emis[band_of(bands, g) + (size_t)bands.nbnd * icol]
+                                                   : emis[g + (size_t)ngpt * icol]);
   const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   // stage one level's value: slot r of the ring, or (kMulti) the per-g accumulator of plane q
@@ -399,10 +402,10 @@ int launch_lw_noscat_planck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol,
                             const float *Ds, const float *wts, const float *inc_flux, const float *tau,
                             const float *pfrac, int ntemp, const float *tlay, const float *tlev, const float *tsfc,
                             int sfc_lay, const BandArgs &bands, float temp_ref_min, float totplnk_delta,
-                            const float *totplnk, const float *sfc_emis, const float *tau_bnd, float *flux_up,
-                            float *flux_dn)
+                            const float *totplnk, bool emis_by_band, const float *sfc_emis, const float *tau_bnd,
+                            float *flux_up, float *flux_dn)
 {
-  LwPlanck pl{tlay, tlev, tsfc, totplnk, ntemp, sfc_lay, temp_ref_min, totplnk_delta};
+  LwPlanck pl{tlay, tlev, tsfc, totplnk, ntemp, sfc_lay, emis_by_band ? 1 : 0, temp_ref_min, totplnk_delta};
   if (tau_bnd)
     return launch_lw_impl<true, true>(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, wts, inc_flux, tau, pfrac, nullptr,
                                       sfc_emis, nullptr, pl, bands, tau_bnd, flux_up, flux_dn);

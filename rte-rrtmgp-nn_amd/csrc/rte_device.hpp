@@ -61,6 +61,7 @@ __device__ __forceinline__ float interp1d(float val, float offset, float delta, 
 struct LwPlanck {
   const float *tlay, *tlev, *tsfc, *totplnk;
   int ntemp, sfc_lay;
+  int emis_by_band;  // sfc_emis is (nbnd, ncol) and expanded in-kernel (rte_lw's expand)
   float tmin, tdelta;
 };
 

@@ -51,11 +51,11 @@ SIGNATURES = {
                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_lw_solver_noscat_planck": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float), P(c_float),
                                                  c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, P(c_int),
-                                                 c_float, c_float, c_vp, c_vp, c_vp, c_vp]),
+                                                 c_float, c_float, c_vp, c_int, c_vp, c_vp, c_vp]),
     "rrtmgpnn_lw_solver_noscat_planck_inc": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float),
                                                      P(c_float), c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
-                                                     c_vp, c_int, P(c_int), c_float, c_float, c_vp, c_vp, c_vp,
-                                                     c_vp]),
+                                                     c_vp, c_int, P(c_int), c_float, c_float, c_vp, c_int, c_vp,
+                                                     c_vp, c_vp]),
     "rrtmgpnn_sw_solver_2stream_inc": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                c_int, P(c_int), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                c_vp]),

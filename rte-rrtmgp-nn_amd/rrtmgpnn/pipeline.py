@@ -149,10 +149,9 @@ class ClearSkyStep:
             tail = (p(self.tau_lw),) + ((p(self.cld_tau_lw),) if self.allsky else ()) + (
                 p(self.lay_src), self.nb_lw, self.kd_lw["nPlanckTemp"], p(self.tlay), p(self.tlev), p(self.tsfc),
                 self.sfc_lay, self._lims_lw, float(self.kd_lw["temp_ref_min"][0]), float(self.kd_lw["totplnk_delta"]),
-                p(self.totplnk), p(self.emis_gpt), p(self.lw_up), p(self.lw_dn))
+                p(self.totplnk), 1, p(self.sfc_emis), p(self.lw_up), p(self.lw_dn))
+            # the surface emissivity goes in by band (as rte_lw takes it) and is expanded in-kernel
             lw_calls = [
-                ("expand_emis", L.rrtmgpnn_expand_band_to_gpt,
-                 (c, self.nb_lw, self.ng_lw, ncol, self._lims_lw, p(self.sfc_emis), p(self.emis_gpt))),
                 ("lw_solver", L.rrtmgpnn_lw_solver_noscat_planck_inc if self.allsky else L.rrtmgpnn_lw_solver_noscat_planck,
                  (c, self.ng_lw, nlay, ncol, self.top_at_1, nmus, self._Ds, self._W, None) + tail),
             ]

@@ -281,7 +281,7 @@ def test_fused_increment_solvers_match_increment_then_solve(dev, rfmip, top_at_1
     up1, dn1, up2, dn2 = f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1)
     tau0 = tau.clone()
     common = (nb, kl["nPlanckTemp"], tlay.data_ptr(), tlev.data_ptr(), tsfc.data_ptr(), nlay if top_at_1 else 1, lims,
-              float(kl["temp_ref_min"][0]), float(kl["totplnk_delta"]), totplnk.data_ptr(), emis.data_ptr())
+              float(kl["temp_ref_min"][0]), float(kl["totplnk_delta"]), totplnk.data_ptr(), 0, emis.data_ptr())
     Ds, W = float_array(GAUSS_DS[nmus]), float_array(GAUSS_WTS[nmus])
     _lib.check(L.rrtmgpnn_lw_solver_noscat_planck_inc(ctx, ng, nlay, ncol, int(top_at_1), nmus, Ds, W, None,
                                                       tau.data_ptr(), tb.data_ptr(), pfrac.data_ptr(), *common,

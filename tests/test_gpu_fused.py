@@ -60,7 +60,7 @@ def test_fused_lw_solver_matches_oracle(dev, orc, rfmip, nmus, top_at_1):
         ctx.h, ngpt, nlay, ncol, int(top_at_1), nmus, float_array(GAUSS_DS[nmus]), float_array(GAUSS_WTS[nmus]), None,
         args[0].data_ptr(), args[1].data_ptr(), kd["nband"], kd["nPlanckTemp"], args[2].data_ptr(),
         args[3].data_ptr(), args[4].data_ptr(), sfc_lay, int_array(kd["band_lims_gpt"].ravel()),
-        float(kd["temp_ref_min"][0]), float(kd["totplnk_delta"]), args[5].data_ptr(), args[6].data_ptr(),
+        float(kd["temp_ref_min"][0]), float(kd["totplnk_delta"]), args[5].data_ptr(), 0, args[6].data_ptr(),
         up.data_ptr(), dn.data_ptr()), "lw_solver_noscat_planck")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(up.cpu().numpy(), up_o)
