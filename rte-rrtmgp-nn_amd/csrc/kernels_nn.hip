@@ -369,6 +369,16 @@ __device__ __forceinline__ floatx4 mlp_out_tile(const float *__restrict__ img, i
 #define RRTMGPNN_MLP_GO_UNROLL 1
 #endif
 constexpr int kMlpThreads = RRTMGPNN_MLP_THREADS, kGoUnroll = RRTMGPNN_MLP_GO_UNROLL;
+// A 1024-thread instance of the LW pair with in-kernel inputs (4 waves per SIMD instead of 2 under the 108 KB weight
+// image, 128 VGPRs) for batches below RRTMGPNN_MLP_BIG_MAX_TILES tiles: alone it is 13 % faster at C3 (6 750 tiles,
+// no 4th-round tail), but it takes every register of every SIMD while it runs, the SW chain can no longer overlap it,
+// and the C3 step got 18 % slower (0.66 vs 0.56 ms, tools/ab_trees.sh).  Off by default (0).
+#ifndef RRTMGPNN_MLP_BIG_THREADS
+#define RRTMGPNN_MLP_BIG_THREADS 1024
+#endif
+#ifndef RRTMGPNN_MLP_BIG_MAX_TILES
+#define RRTMGPNN_MLP_BIG_MAX_TILES 0
+#endif
 // Compile-time output g-tile count for the shipped pairs (LW 16, SW 14): the output loop unrolls completely and the
 // next tile's inputs are loaded before this tile's stores, so the wait for them (vmcnt counts loads and stores
 // together, in order) no longer drains the stores.  0 compiles the runtime-count loop only.
@@ -388,8 +398,9 @@ constexpr int kMlpThreads = RRTMGPNN_MLP_THREADS, kGoUnroll = RRTMGPNN_MLP_GO_UN
 // nn_inputs_kernel and col_dry_kernel) instead of read from nn_inputs / col_dry arrays.  Lane (j, q) needs inputs
 // k = 4t + q of sample s0 + j: the raw state values are loaded a tile ahead (with the next tile's prefetch) and
 // turned into inputs at the tile's start.
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0, bool XIN = false>
-__global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0, bool XIN = false,
+          int NT = kMlpThreads>
+__global__ __launch_bounds__(NT) void mlp_pair_kernel(MlpArgs a)
 {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   // Stage both weight images in LDS (read by every tile of every wave of this block).
@@ -610,10 +621,11 @@ __global__ __launch_bounds__(kMlpThreads) void mlp_pair_kernel(MlpArgs a)
   }
 }
 
-template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0, bool XIN = false>
+template <int AK, int AH1, int AH2, int BK, int BH1, int BH2, int MODE, int ACTS, int NGTC = 0, bool XIN = false,
+          int NT = kMlpThreads>
 static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
 {
-  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS, NGTC, XIN>;
+  auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS, NGTC, XIN, NT>;
   size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
   // Raise the dynamic-LDS limit once per instantiation (kept out of the per-call path so the launch
@@ -624,13 +636,14 @@ static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
     lds_set = 160 * 1024;
   }
   long long ntiles = (a.nbatch + 15) / 16;
-  const int wpb = kMlpThreads / 64;
+  constexpr int kThreads = NT;
+  const int wpb = kThreads / 64;
   int per_cu = std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1)));
-  per_cu = std::min(per_cu, 2048 / kMlpThreads);
+  per_cu = std::min(per_cu, 2048 / kThreads);
   long long want = (ntiles + wpb - 1) / wpb;
   long long grid = std::min<long long>(want, (long long)ctx->num_cus * per_cu);
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kMlpThreads), lds, ctx->stream, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp_pair_kernel");
   return RRTMGPNN_OK;
 }
@@ -647,6 +660,8 @@ static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
     constexpr bool lw = MODE == MLP_LW_PAIR && AK == 5 && AH1 == 4 && AH2 == 4 && BH1 == 1 && BH2 == 1;
     constexpr bool sw = MODE == MLP_SW_PAIR && AK == 2 && AH1 == 1 && AH2 == 1 && BH1 == 1 && BH2 == 1;
     if constexpr (RRTMGPNN_MLP_NGT_CT && lw) {
+      if (a.ngt == 16 && a.play && (a.nbatch + 15) / 16 < RRTMGPNN_MLP_BIG_MAX_TILES)
+        return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16, true, RRTMGPNN_MLP_BIG_THREADS>(ctx, a);
       if (a.ngt == 16 && a.play) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16, true>(ctx, a);
       if (a.ngt == 16) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16>(ctx, a);
     }

@@ -60,7 +60,7 @@ for v in names:
                 models = ("lw_abs", "lw_pfrac") if "lw" in name else ("sw_abs", "sw_ray")
                 arr = (ctypes.c_void_p * 2)(*[nets[m] for m in models])
                 keep.append(arr)
-                a[7] = arr
+                a[11 if "gas_optics" in fn.__name__ else 7] = arr  # rrtmgpnn_gas_optics_*_nn (fused) or predict_nn_*
             elif name.startswith("nn_inputs"):
                 a[8] = ctypes.c_void_p(nets["lw_abs" if "lw" in name else "sw_abs"])
         for t in (st.lw_up, st.lw_dn, st.sw_up, st.sw_dn, st.sw_dir):
