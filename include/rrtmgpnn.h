@@ -52,7 +52,7 @@ int rrtmgpnn_context_create(int device, void *hip_stream, rrtmgpnn_context **ctx
 int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream);
 /* MI355X tuning, no reference counterpart: which SW two-stream kernel rrtmgpnn_sw_solver_2stream* launch.
- * 0 (default): two g-points per lane (packed fp32, four 224-g-point columns per 7-wave block) when ngpt is even,
+ * 0 (default): two g-points per lane (packed fp32, two columns per block) when ngpt is even,
  * one per lane otherwise; 1 / 2 force one / two g-points per lane (2 needs even ngpt).
  * Both kernels give bit-identical fluxes.  ctx == NULL sets the default of every context not set itself. */
 int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode);

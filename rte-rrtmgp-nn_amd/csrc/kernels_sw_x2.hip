@@ -318,8 +318,11 @@ int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
                          float *flux_dn, float *flux_dir)
 {
+  // Columns per block: 2 (224 g-points: 224 lanes in 4 waves, 32 idle, a 32 KB ring).  Four columns fill 7 waves
+  // exactly and were 5 % faster alone at C4, but in the overlapped step the smaller blocks share the CUs better with
+  // the LW chain: whole step C3 -1.7 %, C4 -3.5 % (tools/ab_env.sh RRTMGPNN_LIB).  0: columns_per_block (fewest idle).
 #ifndef RRTMGPNN_SW_NCB
-#define RRTMGPNN_SW_NCB 0
+#define RRTMGPNN_SW_NCB 2
 #endif
   const int ncb = RRTMGPNN_SW_NCB > 0 && RRTMGPNN_SW_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SW_NCB : columns_per_block(ngpt / 2);
   const int threads = (ncb * (ngpt / 2) + 63) / 64 * 64;
