@@ -144,6 +144,7 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
                       const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, float *flux_up,
                       float *flux_dn, float *flux_dir);
 // kernels_sw_x2.hip (called by launch_sw_2stream for even ngpt; ws sized by it)
+size_t sw_2stream_x2_layer_planes(bool inc);
 int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,

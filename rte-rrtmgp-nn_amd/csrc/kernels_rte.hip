@@ -724,7 +724,8 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
   const bool x2 = kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
-  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + (inc && (kSwIncPark || x2) ? 3 * (size_t)ngpt * nlay * ncol : 0);
+  const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc && kSwIncPark ? 3 : 0);
+  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
   int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;
   if (x2)
