@@ -35,9 +35,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c3", choices=["c3", "c4", "c5"],
-                    help="c3: RFMIP 1800x60 (default, the metric's config); c4: 10000x60 synthetic clear-sky; "
-                         "c5: 125000x137 synthetic per GPU")
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
+                    help="c3: RFMIP 1800x60 LW+SW (default, the metric's config); c2: the same columns, LW only "
+                         "(BASELINE configs[1], metric in LW columns/s); c4: 10000x60 synthetic all-sky; "
+                         "c5: 125000x137 synthetic clear-sky per GPU")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
     ap.add_argument("--unfused", action="store_true",
@@ -124,7 +125,13 @@ def main():
     from rrtmgpnn.pipeline import ClearSkyStep
 
     clouds = None
-    if args.config == "c3":
+    metric = METRIC
+    if args.config == "c2":
+        prob = data.rfmip_problem()
+        workload = "C2: RFMIP clear-sky LW only, 1800 columns x 60 layers x 256 g-points, NN gas optics (g256)"
+        data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
+        metric = "atmospheric columns/sec (LW clear-sky fluxes), 1 MI355X"
+    elif args.config == "c3":
         prob = data.rfmip_problem()
         workload = "C3: RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics (g256 LW + g224 SW)"
         data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
@@ -142,7 +149,8 @@ def main():
     if args.sw_kernel:
         from rrtmgpnn import api
         api.set_sw_kernel_default(args.sw_kernel)
-    step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap)
+    step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap,
+                        sw=args.config != "c2")
     ncol, nlay = step.ncol, step.nlay
 
     use_graph = not args.no_graph
@@ -311,15 +319,15 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if clouds is not None:
             prob = dict(prob, **dict(zip(("lwp", "iwp", "rel", "rei"), clouds)))
-        cpu = cpu_baseline(prob, args.cpu_seconds, args.cpu_kind)
+        cpu = cpu_baseline(prob, args.cpu_seconds, args.cpu_kind, sw=step.sw)
 
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 1), "unit": "columns/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric, "value": round(value, 1), "unit": "columns/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": data_desc,
             "config": {"workload": workload, "ncol_per_gpu": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
-                       "ngpt_sw": step.ng_sw, "parallelism": "column-sharded, 1 process per GPU",
+                       "ngpt_sw": step.ng_sw if step.sw else None, "parallelism": "column-sharded, 1 process per GPU",
                        "launch": ("hipGraph replay" if use_graph else "eager") +
                                  (", LW and SW chains on two streams" if step.overlap else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
@@ -348,7 +356,7 @@ def _subset(prob, n):
     return sub
 
 
-def cpu_baseline(prob, target_s, kind="auto"):
+def cpu_baseline(prob, target_s, kind="auto", sw=True):
     """CPU path on the host cores over a bounded sample of the same workload (rank 0, N=1 only).
 
     kind "reference": the reference's own Fortran compiled from its sources (oracle/_ref: rte_lw, rte_sw and
@@ -392,7 +400,8 @@ def cpu_baseline(prob, target_s, kind="auto"):
                 orc.all_sky_sw(sub, models_sw, kds, co_sw, cl(sub))
             else:
                 orc.clear_sky_lw(sub, models_lw, kd)
-                orc.clear_sky_sw(sub, models_sw, kds)
+                if sw:
+                    orc.clear_sky_sw(sub, models_sw, kds)
         label, desc = "port", "C restatement (oracle), OpenMP over columns"
     else:
         import threading
@@ -415,6 +424,8 @@ def cpu_baseline(prob, target_s, kind="auto"):
             if allsky:  # rrtmgp_allsky.F90: cloud_optics -> clouds%increment(atmos)
                 (tau,) = ref.increment_bybnd(kd, (tau,), ref.cloud_optics(co_lw, *cl(sub), nstr=1, icergh=2))
             ref.rte_lw(kd, tau, lay, lev, sfc, jac, emis, sub["top_at_1"])
+            if not sw:
+                return
             xs = orc.nn_inputs(sub["play"], sub["tlay"], sub["gases"], models_sw[0]).reshape(-1, int(models_sw[0]["dims"][0]))
             ta = orc.tau_post(models_sw[0], ref.mlp(models_sw[0], xs), cd)
             ssa = orc.tau_post(models_sw[1], ref.mlp(models_sw[1], xs), cd, tau_abs_to_tot=ta)
@@ -446,8 +457,9 @@ def cpu_baseline(prob, target_s, kind="auto"):
         n = int(min(n * max(2.0, min(8.0, target_s / max(dt, 1e-3) / 2)), prob["ncol"] * 256))
         n = (n + 35) // 36 * 36
     return {"value": round(n / dt, 1), "unit": "columns/s", "cores": threads, "kind": label,
-            "sample": "%d columns of the same workload (LW+SW gas optics%s + RTE), %.1f s: %s"
-                      % (n, " + cloud optics/increment/delta-scale" if allsky else "", dt, desc)}
+            "sample": "%d columns of the same workload (%s gas optics%s + RTE), %.1f s: %s"
+                      % (n, "LW+SW" if sw else "LW", " + cloud optics/increment/delta-scale" if allsky else "", dt,
+                         desc)}
 
 
 if __name__ == "__main__":

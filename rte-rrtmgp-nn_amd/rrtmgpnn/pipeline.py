@@ -50,7 +50,9 @@ def _t(a, dev):
 
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
-                 sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True):
+                 sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
+                 sw=True):
+        # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         self.dev = torch.device("cuda", device)
         self.allsky = clouds is not None
         self.fused = fused
@@ -91,11 +93,13 @@ class ClearSkyStep:
         self.x_lw, self.x_sw = f(ncol, nlay, self.nx_lw), f(ncol, nlay, self.nx_sw)
         self.tau_lw, self.lay_src = f(ncol, nlay, self.ng_lw), f(ncol, nlay, self.ng_lw)
         self.emis_gpt = f(ncol, self.ng_lw)
-        self.tau_sw, self.ssa_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
+        self.sw = sw
+        if sw:
+            self.tau_sw, self.ssa_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
         if not fused:  # arrays the fused step never materialises
             self.lev_src = f(ncol, nlay + 1, self.ng_lw)
             self.sfc_src, self.sfc_jac = f(ncol, self.ng_lw), f(ncol, self.ng_lw)
-        if not fused:
+        if not fused and sw:
             self.g_sw = f(ncol, nlay, self.ng_sw)
         if self.allsky:
             self.nb_sw = self.kd_sw["nband"]
@@ -105,6 +109,9 @@ class ClearSkyStep:
             self.cloud_lw, self.cloud_sw = (self._cloud_optics(w, cloud_lut, icergh) for w in ("lw", "sw"))
         self.lw_up, self.lw_dn = f(ncol, nlay + 1), f(ncol, nlay + 1)
         self.sw_up, self.sw_dn, self.sw_dir = f(ncol, nlay + 1), f(ncol, nlay + 1), f(ncol, nlay + 1)
+        if not sw:
+            for t in (self.sw_up, self.sw_dn, self.sw_dir):
+                t.zero_()
 
         # ---- prepared ctypes argument lists ----
         def gas_args(names):
@@ -182,6 +189,10 @@ class ClearSkyStep:
                       p(self.cld_tau_lw), None, None)),
                 ]
         self.calls += lw_calls
+        if not sw:
+            self.calls = [c for c in self.calls if c[0] != "cloud_optics_sw"]
+            self._finish(False)
+            return
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
         g_sw = None if fused else p(self.g_sw)
@@ -227,7 +238,10 @@ class ClearSkyStep:
                  (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
-        if fused and os.environ.get("RRTMGPNN_STEP_ORDER", "") != "class":
+        self._finish(overlap)
+
+    def _finish(self, overlap):
+        if self.fused and os.environ.get("RRTMGPNN_STEP_ORDER", "") != "class":
             # the small kernels that do not depend on a network's output go first in their chain, ahead of the big
             # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW
             # solver held while the LW solver, which needs it, could not start
@@ -240,7 +254,7 @@ class ClearSkyStep:
         self.overlap = overlap
         self.ctx2 = None
         if overlap:
-            self.ctx2 = Context(device, self._sw_stream())
+            self.ctx2 = Context(self.dev.index, self._sw_stream())
             self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None

@@ -180,3 +180,30 @@ def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky):
     for k in a:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
         np.testing.assert_array_equal(a[k], c[k], err_msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("allsky", [False, True])
+def test_lw_only_step_equals_lw_half(dev, rfmip, allsky):
+    """Config C2 (bench.py --config c2): the LW half alone, eager and as a hipGraph, gives the LW fluxes of the full
+    LW+SW step bit for bit, and issues no SW launch."""
+    from rrtmgpnn import data
+    from rrtmgpnn.pipeline import ClearSkyStep
+    prob = subset(rfmip, np.arange(0, 1800, 6))
+    clouds = data.allsky_clouds(prob, data.load_cloud_optics("lw")) if allsky else None
+    full = ClearSkyStep(prob, device=0, clouds=clouds)
+    lw = ClearSkyStep(prob, device=0, clouds=clouds, sw=False)
+    assert not lw.overlap and all("sw" not in name for name, _, _ in lw.calls)
+    full.step()
+    lw.step()
+    torch.cuda.synchronize()
+    a, b = full.fluxes(), lw.fluxes()
+    lw.capture()
+    lw.lw_up.fill_(float("nan"))
+    lw.lw_dn.fill_(float("nan"))
+    lw.replay()
+    torch.cuda.synchronize()
+    c = lw.fluxes()
+    for k in ("lw_up", "lw_dn"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        np.testing.assert_array_equal(a[k], c[k], err_msg=k)
