@@ -248,6 +248,16 @@ int rrtmgpnn_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt
  * both sets (ngpt, nlay, ncol); NULL ssa as above. */
 int rrtmgpnn_increment(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, float *tau_io, float *ssa_io, float *g_io,
                        const float *tau_in, const float *ssa_in, const float *g_in);
+/* Heating rate [K/s] per layer, compute_heating_rate (extensions/mo_heating_rates.F90:26-53): grav = 9.80665,
+ * cp_dry = 1004.64 (rrtmgp/mo_rrtmgp_constants.F90:50,53).  The extension predates this fork's layout; here fluxes and
+ * plev are the fork's (nlay+1, ncol), level fastest, and heating_rate is (nlay, ncol). */
+int rrtmgpnn_compute_heating_rate(rrtmgpnn_context *ctx, int ncol, int nlay, const float *flux_up, const float *flux_dn,
+                                  const float *plev, float *heating_rate);
+/* Heating rate [K/day] as the NN evaluation programs report it, calc_heating_rate
+ * (examples/rrtmgp-nn-training/rrtmgp_lw_eval_nn_rfmip.F90:624-653): cp = 1004, -(86400 g / cp) d(F_dn - F_up) / dp.
+ * Same layouts as rrtmgpnn_compute_heating_rate. */
+int rrtmgpnn_calc_heating_rate_k_day(rrtmgpnn_context *ctx, int ncol, int nlay, const float *flux_up,
+                                     const float *flux_dn, const float *plev, float *hr_k_day);
 /* ty_optical_props_2str%delta_scale([for]) (rte/mo_optical_props.F90:576-604; kernels
  * rte/kernels/mo_optical_props_kernels.F90:41-92) on n values in place.  fwd == NULL: f = g**2. */
 int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);

@@ -63,7 +63,16 @@ class Oracle:
         L.orc_increment_bybnd.argtypes = [c_int] * 4 + [_i32p, c_int, _f32p, _f32p, _f32p, c_int, _f32p, _f32p, _f32p]
         L.orc_delta_scale_2str.argtypes = [c_long, _f32p, _f32p, _f32p, ctypes.c_void_p]
         L.orc_set_num_threads.argtypes = [c_int]
+        L.orc_heating_rate.argtypes = [c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p]
         L.orc_num_threads.restype = c_int
+
+    def heating_rate(self, up, dn, plev, k_day=False):
+        """orc_heating_rate: fluxes / plev (ncol, nlay+1) -> (ncol, nlay); K/s (mo_heating_rates) or K/day (eval)."""
+        up, dn, plev = f32(up), f32(dn), f32(plev)
+        ncol, nlev = up.shape
+        out = np.empty((ncol, nlev - 1), np.float32)
+        self.L.orc_heating_rate(ncol, nlev - 1, int(bool(k_day)), up, dn, plev, out)
+        return out
 
     def set_threads(self, n):
         self.L.orc_set_num_threads(int(n))

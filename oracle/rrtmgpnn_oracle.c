@@ -779,6 +779,28 @@ void orc_delta_scale_2str(long n, float *tau, float *ssa, float *g, const float 
   }
 }
 
+/* Heating rates per layer from level fluxes, fluxes/plev (nlay+1, ncol), hr (nlay, ncol).
+ * mode 0, K/s: extensions/mo_heating_rates.F90:48-52 with grav, cp_dry of rrtmgp/mo_rrtmgp_constants.F90:50,53.
+ * mode 1, K/day: examples/rrtmgp-nn-training/rrtmgp_lw_eval_nn_rfmip.F90:639-651 (cp = 1004). */
+void orc_heating_rate(int ncol, int nlay, int mode, const float *up, const float *dn, const float *plev, float *hr)
+{
+  const float grav = 9.80665f, cp_dry = 1004.64f;
+  volatile float day = 24.0f * 3600.0f;
+  volatile float t = day * grav;
+  const float scaling = -(t / 1004.0f);
+  for (long c = 0; c < ncol; c++)
+    for (int l = 0; l < nlay; l++) {
+      const long k = c * (long)(nlay + 1) + l;
+      const float dp = plev[k + 1] - plev[k];
+      if (mode == 0) {
+        hr[c * (long)nlay + l] = (up[k + 1] - up[k] - dn[k + 1] + dn[k]) * grav / (cp_dry * dp);
+      } else {
+        const float net1 = dn[k + 1] - up[k + 1], net0 = dn[k] - up[k];
+        hr[c * (long)nlay + l] = scaling * (net1 - net0) / dp;
+      }
+    }
+}
+
 int orc_num_threads(void)
 {
 #ifdef _OPENMP

@@ -895,6 +895,29 @@ int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, fl
   return launch_delta_scale(ctx, n, tau, ssa, g, fwd);
 }
 
+// ---- heating rates (a-20) ----
+int rrtmgpnn_compute_heating_rate(rrtmgpnn_context *ctx, int ncol, int nlay, const float *flux_up, const float *flux_dn,
+                                  const float *plev, float *heating_rate)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!flux_up || !flux_dn || !plev || !heating_rate || ncol < 0 || nlay < 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "heating_rate: bad argument");
+  // mo_rrtmgp_constants.F90:50,53
+  return launch_heating_rate(ctx, ncol, nlay, 0, 9.80665f, 1004.64f, flux_up, flux_dn, plev, heating_rate);
+}
+
+int rrtmgpnn_calc_heating_rate_k_day(rrtmgpnn_context *ctx, int ncol, int nlay, const float *flux_up,
+                                     const float *flux_dn, const float *plev, float *hr_k_day)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!flux_up || !flux_dn || !plev || !hr_k_day || ncol < 0 || nlay < 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "calc_heating_rate: bad argument");
+  // scaling = -(24.0_wp * 3600.0_wp * grav / SpecificHeatDryAir), each operation rounded to fp32
+  volatile float day = 24.0f * 3600.0f, t = day * 9.80665f;
+  const float scaling = -(t / 1004.0f);
+  return launch_heating_rate(ctx, ncol, nlay, 1, scaling, 0.0f, flux_up, flux_dn, plev, hr_k_day);
+}
+
 // ---- data files: RBIN, classic netCDF, netCDF-4 (datafile.cpp) ----
 struct rrtmgpnn_file {
   DataFile df;

@@ -93,6 +93,8 @@ int launch_cloud_optics(rrtmgpnn_context *ctx, const rrtmgpnn_cloud_optics *co, 
                         const float *ciwp, const float *reliq, const float *reice, float *tau, float *ssa, float *g);
 int launch_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, const BandArgs *bands, float *tau1,
                            float *ssa1, float *g1, const float *tau2, const float *ssa2, const float *g2);
+int launch_heating_rate(rrtmgpnn_context *ctx, int ncol, int nlay, int k_day, float c0, float c1, const float *up,
+                        const float *dn, const float *plev, float *hr);
 int launch_delta_scale(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);
 // kernels_nn.hip
 struct GasArgs {

@@ -9,6 +9,7 @@ module mo_rrtmgpnn_c
   private
   public :: rrtmgpnn_ctx, rrtmgpnn_check, rrtmgpnn_error_message, dev_alloc, dev_free, h2d, d2h, &
             rrtmgpnn_set_context, dev_upload, dev_download, dev_upload_int
+  public :: c_rrtmgpnn_compute_heating_rate
   public :: c_rrtmgpnn_network_load, c_rrtmgpnn_compute_nn_inputs, c_rrtmgpnn_get_col_dry, &
             c_rrtmgpnn_interpolate_tlev, c_rrtmgpnn_predict_nn_lw, c_rrtmgpnn_predict_nn_sw, &
             c_rrtmgpnn_compute_planck_source_nn, c_rrtmgpnn_lw_solver_noscat, c_rrtmgpnn_sw_solver_2stream, &
@@ -145,6 +146,12 @@ module mo_rrtmgpnn_c
       type(c_ptr), value :: ctx, arr_in, arr_out
       integer(c_int), value :: nband, ngpt, ncol
       integer(c_int), dimension(*), intent(in) :: band_lims_gpt
+    end function
+    integer(c_int) function c_rrtmgpnn_compute_heating_rate(ctx, ncol, nlay, flux_up, flux_dn, plev, heating_rate) &
+        bind(C, name="rrtmgpnn_compute_heating_rate")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, flux_up, flux_dn, plev, heating_rate
+      integer(c_int), value :: ncol, nlay
     end function
     ! ---- all-sky: cloud optics, increment, delta scaling ----
     integer(c_int) function c_rrtmgpnn_cloud_optics_create_lut(ctx, nband, band_lims_wvn, nsize_liq, nsize_ice, &

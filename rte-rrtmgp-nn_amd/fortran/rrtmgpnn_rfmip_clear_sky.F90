@@ -6,7 +6,7 @@
 ! usage: rrtmgpnn_rfmip_clear_sky <problem.rbin> <output.rbin> <data_dir> [block_size]
 !   problem.rbin: play/tlay (ncol,nlay), plev/tlev (ncol,nlay+1), tsfc/sfc_emis/sfc_alb/mu0/tsi/usecol
 !   (ncol), gas_names (ngas,32) + vmr_<gas> (ncol,nlay), top_at_1 and n_gauss_angles (1).
-!   output.rbin:  lw_flux_up/dn, sw_flux_up/dn/dir (ncol,nlay+1).
+!   output.rbin:  lw_flux_up/dn, sw_flux_up/dn/dir (ncol,nlay+1), lw_heating_rate (ncol,nlay) [K/s].
 program rrtmgpnn_rfmip_clear_sky
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -18,6 +18,7 @@ program rrtmgpnn_rfmip_clear_sky
   use mo_rte_lw,             only: rte_lw
   use mo_rte_sw,             only: rte_sw
   use mo_rrtmgpnn_rbin
+  use mo_heating_rates, only: compute_heating_rate
   implicit none
 
   character(len=512) :: problem_file, output_file, data_dir, arg
@@ -25,7 +26,7 @@ program rrtmgpnn_rfmip_clear_sky
   real(wp), allocatable :: mu0(:), tsi(:), usecol(:), scal(:), vmr(:,:)
   character(len=32), allocatable :: gas_names(:)
   real(wp), allocatable, target :: lw_up(:,:), lw_dn(:,:), sw_up(:,:), sw_dn(:,:), sw_dir(:,:)
-  real(wp), allocatable :: sfc_emis_spec(:,:), toa_flux(:,:), sfc_alb_spec(:,:), def_tsi(:)
+  real(wp), allocatable :: sfc_emis_spec(:,:), toa_flux(:,:), sfc_alb_spec(:,:), def_tsi(:), lw_hr(:,:)
   type(ty_gas_concs) :: gas_concs
   type(ty_gas_optics_rrtmgp) :: kdist_lw, kdist_sw
   type(rrtmgp_network_type), dimension(2) :: nets_lw, nets_sw
@@ -133,12 +134,17 @@ program rrtmgpnn_rfmip_clear_sky
     deallocate(toa_flux, sfc_alb_spec, def_tsi)
   end do
 
-  u = rbin_write_begin(output_file, 5)
+  ! heating rates of the longwave fluxes (extensions/mo_heating_rates), K/s
+  allocate(lw_hr(nlay, ncol))
+  call stop_on_err(compute_heating_rate(lw_up, lw_dn, plev, lw_hr))
+
+  u = rbin_write_begin(output_file, 6)
   call rbin_write_real(u, "lw_flux_up", lw_up, shape(lw_up))
   call rbin_write_real(u, "lw_flux_dn", lw_dn, shape(lw_dn))
   call rbin_write_real(u, "sw_flux_up", sw_up, shape(sw_up))
   call rbin_write_real(u, "sw_flux_dn", sw_dn, shape(sw_dn))
   call rbin_write_real(u, "sw_flux_dir", sw_dir, shape(sw_dir))
+  call rbin_write_real(u, "lw_heating_rate", lw_hr, shape(lw_hr))
   call rbin_write_end(u)
   write(*, '(a,i0,a,i0,a)') "rrtmgpnn_rfmip_clear_sky: ", ncol, " columns x ", nlay, " layers done"
 

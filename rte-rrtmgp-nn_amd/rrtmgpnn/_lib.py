@@ -65,6 +65,8 @@ SIGNATURES = {
     "rrtmgpnn_sw_solver_2stream": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_expand_band_to_gpt": (c_int, [c_vp, c_int, c_int, c_int, P(c_int), c_vp, c_vp]),
+    "rrtmgpnn_compute_heating_rate": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_calc_heating_rate_k_day": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_cloud_optics_create_lut": (c_int, [c_vp, c_int, P(c_float), c_int, c_int, c_int, c_float, c_float,
                                                  c_float, c_float, P(c_float), P(c_float), P(c_float), P(c_float),
                                                  P(c_float), P(c_float), P(c_vp)]),

@@ -791,3 +791,31 @@ def rte_sw(atmos, top_at_1, mu0, inc_flux, sfc_alb_dir_gpt, sfc_alb_dif_gpt, flu
     if fluxes.flux_net is not None:
         torch.sub(dn, up, out=fluxes.flux_net)
     return ""
+
+
+def _heating_rate(fn, name, flux_up, flux_dn, plev, heating_rate):
+    ncol, nlev = flux_up.shape
+    nlay = nlev - 1
+    if tuple(flux_dn.shape) != (ncol, nlev):
+        return name + ": flux_dn array inconsistently sized."
+    if tuple(plev.shape) != (ncol, nlev):
+        return name + ": plev array inconsistently sized."
+    if tuple(heating_rate.shape) != (ncol, nlay):
+        return name + ": heating_rate array inconsistently sized."
+    ctx = context(flux_up.device.index)
+    check(fn(ctx.h, ncol, nlay, _p(flux_up), _p(flux_dn), _p(plev), _p(heating_rate)), name)
+    return ""
+
+
+def compute_heating_rate(flux_up, flux_dn, plev, heating_rate):
+    """compute_heating_rate (extensions/mo_heating_rates.F90:26-53), K/s, grav / cp_dry from mo_rrtmgp_constants.
+    Arrays in this fork's layout: fluxes and plev (ncol, nlay+1), heating_rate (ncol, nlay) device tensors."""
+    return _heating_rate(_lib.lib().rrtmgpnn_compute_heating_rate, "heating_rate", flux_up, flux_dn, plev,
+                         heating_rate)
+
+
+def calc_heating_rate(flux_up, flux_dn, plev, hr_k_day):
+    """calc_heating_rate (examples/rrtmgp-nn-training/rrtmgp_lw_eval_nn_rfmip.F90:624-653), K/day with cp = 1004,
+    as the NN evaluation programs report it.  Same layouts as compute_heating_rate."""
+    return _heating_rate(_lib.lib().rrtmgpnn_calc_heating_rate_k_day, "calc_heating_rate", flux_up, flux_dn, plev,
+                         hr_k_day)

@@ -101,6 +101,8 @@ def test_fortran_rfmip_driver_matches_oracle(tmp_path, orc, rfmip):
         err = float(np.sqrt(np.mean((g.astype(np.float64) - ref) ** 2)))
         assert err <= 1e-3, "%s: RMS %.3g W/m2" % (k, err)
         np.testing.assert_array_equal(g, ref, err_msg=k + ": not bit-identical")
+    # mo_heating_rates%compute_heating_rate on the driver's LW fluxes (row a-20), K/s
+    np.testing.assert_array_equal(got["lw_heating_rate"], orc.heating_rate(lu, ld, prob["plev"]))
 
 
 @pytest.mark.gpu

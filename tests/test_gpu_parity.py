@@ -310,3 +310,27 @@ def test_api_error_messages(dev):
     assert "too many quadrature points" in api.rte_lw(op, True, src, torch.ones((4, 16), device=dev), fl,
                                                       n_gauss_angles=5)
     assert op.alloc_1scl(0, 5) != ""
+
+
+def test_heating_rates_bitwise(dev, orc, rfmip):
+    """Row a-20: both heating-rate forms (mo_heating_rates K/s, the eval programs' K/day) on the C3 step's LW and SW
+    fluxes, through the C ABI (Python class-layer functions), equal the oracle bit for bit; wrong extents return the
+    reference's error strings."""
+    from rrtmgpnn import api
+    from rrtmgpnn.pipeline import ClearSkyStep
+    step = ClearSkyStep(rfmip, device=0)
+    step.step()
+    torch.cuda.synchronize()
+    plev = torch.from_numpy(np.ascontiguousarray(rfmip["plev"], dtype=np.float32)).to(step.dev)
+    hr = torch.empty((step.ncol, step.nlay), dtype=torch.float32, device=step.dev)
+    for up, dn in ((step.lw_up, step.lw_dn), (step.sw_up, step.sw_dn)):
+        for k_day, fn in ((False, api.compute_heating_rate), (True, api.calc_heating_rate)):
+            hr.fill_(float("nan"))
+            assert fn(up, dn, plev, hr) == ""
+            torch.cuda.synchronize()
+            ref = orc.heating_rate(up.cpu().numpy(), dn.cpu().numpy(), rfmip["plev"], k_day=k_day)
+            np.testing.assert_array_equal(hr.cpu().numpy(), ref)
+    assert api.compute_heating_rate(step.lw_up, step.lw_dn, plev, hr[:, :-1]) == \
+        "heating_rate: heating_rate array inconsistently sized."
+    assert api.compute_heating_rate(step.lw_up, step.lw_dn[:, :-1], plev, hr) == \
+        "heating_rate: flux_dn array inconsistently sized."

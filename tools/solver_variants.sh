@@ -9,7 +9,7 @@ B=${VAR_DIR:-${TMPDIR:-/tmp}/rrtmgpnn_var}
 rm -rf $B; mkdir -p $B
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off"
 # sources without tuning knobs are built once
-COMMON="api.cpp datafile.cpp kernels_clouds.hip kernels_lw_scat.hip"
+COMMON="api.cpp datafile.cpp kernels_clouds.hip kernels_lw_scat.hip kernels_fluxes.hip"
 for f in $COMMON; do /opt/rocm/bin/hipcc $FLAGS -x hip -c $PKG/csrc/$f -o $B/common_${f%.*}.o & done
 names=()
 for spec in "$@"; do
