@@ -43,8 +43,9 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
-    ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2],
-                    help="SW solver: 0 the library's choice, 1 / 2 g-points per lane (rrtmgpnn_context_set_sw_kernel)")
+    ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="SW solver: 0 the library's choice, 1 / 2 g-points per lane, 3 checkpointed passes "
+                         "(rrtmgpnn_context_set_sw_kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],

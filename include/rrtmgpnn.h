@@ -53,11 +53,16 @@ int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream);
 /* MI355X tuning, no reference counterpart: which SW two-stream kernel rrtmgpnn_sw_solver_2stream* launch.
  * 0 (default): two g-points per lane (packed fp32, two columns per block) when ngpt is even,
- * one per lane otherwise; 1 / 2 force one / two g-points per lane (2 needs even ngpt).
- * Both kernels give bit-identical fluxes.  ctx == NULL sets the default of every context not set itself. */
+ * one per lane otherwise; 1 / 2 force one / two g-points per lane (2 needs even ngpt); 3: two g-points per lane
+ * with checkpointed passes (beam / adding state stored every few levels instead of per level, even ngpt).
+ * All kernels give bit-identical fluxes.  ctx == NULL sets the default of every context not set itself. */
 int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode);
 void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_synchronize(rrtmgpnn_context *ctx);
+/* The context's device workspace grows on demand.  A call issued while the context's stream is captured into a
+ * hipGraph pins it (the graph holds its address): later calls that would need more fail with RRTMGPNN_ERR_ARGUMENT
+ * instead of freeing memory the graph writes.  Unpin after destroying the graph (no reference counterpart). */
+int rrtmgpnn_context_unpin_workspace(rrtmgpnn_context *ctx);
 /* Device memory helpers for hosts without their own allocator (Fortran glue). */
 int rrtmgpnn_malloc(rrtmgpnn_context *ctx, long long bytes, void **dptr);
 int rrtmgpnn_free(rrtmgpnn_context *ctx, void *dptr);

@@ -49,6 +49,8 @@ class Oracle:
                                       _f32p, _f32p]
         L.orc_nn_tau_post.argtypes = [c_int, c_long, _f32p, _f32p, _f32p, _f32p, c_vp]
         L.orc_square.argtypes = [c_long, _f32p]
+        L.orc_nn_both_post.argtypes = [c_int, c_long, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
+        L.orc_interpolate_tlev.argtypes = [c_int, c_int, _f32p, _f32p, _f32p, _f32p]
         L.orc_planck_source_nn.argtypes = [c_int, c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, c_int, _i32p,
                                            c_float, c_float, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_lw_solver_noscat_gaussquad.argtypes = [c_int, c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p,
@@ -91,14 +93,33 @@ class Oracle:
                 nds.append(2)
                 continue
             v = np.asarray(gases[n], np.float32)
+            nd = {0: 0, 1: 1}.get(v.ndim, 2)  # before f32(): ascontiguousarray makes a 0-d array 1-d
             v = f32(v)
             keep.append(v)
             ptrs.append(_ptr(v))
-            nds.append({0: 0, 1: 1}.get(v.ndim, 2))
+            nds.append(nd)
         out = np.zeros((ncol, nlay, nx), np.float32)
         self.L.orc_compute_nn_inputs(ncol, nlay, nx, f32(play), f32(tlay), (c_vp * nx)(*ptrs),
                                      np.array(nds, np.int32), f32(model["input_min"]), f32(model["input_max"]), out)
         return out
+
+    def interpolate_tlev(self, play, plev, tlay):
+        """tlev when gas_optics_int gets none (rrtmgp/mo_gas_optics_rrtmgp.F90:317-337): (ncol, nlay+1)."""
+        ncol, nlay = play.shape
+        out = np.zeros((ncol, nlay + 1), np.float32)
+        self.L.orc_interpolate_tlev(ncol, nlay, f32(play), f32(plev), f32(tlay), out)
+        return out
+
+    def both_post(self, model, y, col_dry):
+        """Single "both" model (mo_gas_optics_kernels.F90:744-772): y (..., 2*ngpt) -> tau, pfrac (..., ngpt)."""
+        y = f32(y)
+        ngpt = y.shape[-1] // 2
+        nb = y.size // (2 * ngpt)
+        tau = np.zeros(y.shape[:-1] + (ngpt,), np.float32)
+        pf = np.zeros_like(tau)
+        self.L.orc_nn_both_post(ngpt, nb, y, f32(model["output_mean"]), f32(model["output_std"]),
+                                f32(col_dry).reshape(-1), tau, pf)
+        return tau, pf
 
     def col_dry(self, h2o, plev):
         ncol, nlay = h2o.shape
@@ -206,18 +227,26 @@ class Oracle:
         return tau, ssa, g
 
     # -- class-level pipelines (gas_optics + rte) -------------------------------------------
-    def lw_gas_optics(self, prob, models, kd):
-        """gas_optics_int NN branch (rrtmgp/mo_gas_optics_rrtmgp.F90:239-428). models: [abs, pfrac]."""
+    def lw_gas_optics(self, prob, models, kd, col_dry=None, tlev=True):
+        """gas_optics_int NN branch (rrtmgp/mo_gas_optics_rrtmgp.F90:239-428). models: [abs, pfrac], or [both]
+        (the single-model branch, mo_gas_optics_kernels.F90:744-772).  col_dry: the optional argument (quirk B-3
+        fixed: honoured); tlev=False: interpolated from the layers (:317-337) instead of prob["tlev"]."""
         x = self.nn_inputs(prob["play"], prob["tlay"], prob["gases"], models[0])
-        cd = self.col_dry(prob["gases"]["h2o"], prob["plev"])
+        cd = self.col_dry(prob["gases"]["h2o"], prob["plev"]) if col_dry is None else f32(col_dry)
         ncol, nlay = prob["play"].shape
-        tau = self.tau_post(models[0], self.mlp(models[0], x.reshape(-1, x.shape[-1])), cd).reshape(ncol, nlay, -1)
-        pf = self.mlp(models[1], x.reshape(-1, x.shape[-1]))
-        pf = (pf * pf).astype(np.float32).reshape(ncol, nlay, -1)
+        xf = x.reshape(-1, x.shape[-1])
+        if len(models) == 1:
+            tau, pf = self.both_post(models[0], self.mlp(models[0], xf), cd)
+            tau, pf = tau.reshape(ncol, nlay, -1), pf.reshape(ncol, nlay, -1)
+        else:
+            tau = self.tau_post(models[0], self.mlp(models[0], xf), cd).reshape(ncol, nlay, -1)
+            pf = self.mlp(models[1], xf)
+            pf = (pf * pf).astype(np.float32).reshape(ncol, nlay, -1)
         sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
-        lay, lev, sfc, jac = self.planck_source(kd, prob["tlay"], prob["tlev"], prob["tsfc"], pf, sfc_lay)
+        tl = prob["tlev"] if tlev is True else self.interpolate_tlev(prob["play"], prob["plev"], prob["tlay"])
+        lay, lev, sfc, jac = self.planck_source(kd, prob["tlay"], tl, prob["tsfc"], pf, sfc_lay)
         return {"tau": tau, "lay_source": lay, "lev_source": lev, "sfc_source": sfc, "sfc_source_Jac": jac,
-                "pfrac": pf, "nn_inputs": x, "col_dry": cd}
+                "pfrac": pf, "nn_inputs": x, "col_dry": cd, "tlev": tl}
 
     def sw_gas_optics(self, prob, models):
         """gas_optics_ext NN branch (:433-602), 2str: tau, ssa, g (= 0)."""

@@ -81,6 +81,24 @@ void orc_get_col_dry(int ncol, int nlay, const float *vmr_h2o, const float *plev
     }
 }
 
+/* Level temperatures when gas_optics_int is called without tlev: rrtmgp/mo_gas_optics_rrtmgp.F90:317-337.
+ * Pressure-weighted interpolation inside the column, linear extrapolation in pressure at both ends; Fortran
+ * evaluates a*b/c as (a*b)/c and a*b*c as (a*b)*c, left to right.  play/tlay (nlay,ncol), plev/tlev (nlay+1,ncol). */
+void orc_interpolate_tlev(int ncol, int nlay, const float *play, const float *plev, const float *tlay, float *tlev)
+{
+  for (int icol = 0; icol < ncol; icol++) {
+    const float *pa = play + (size_t)nlay * icol, *ta = tlay + (size_t)nlay * icol;
+    const float *pv = plev + (size_t)(nlay + 1) * icol;
+    float *tv = tlev + (size_t)(nlay + 1) * icol;
+    tv[0] = ta[0] + ((pv[0] - pa[0]) * (ta[1] - ta[0])) / (pa[1] - pa[0]);                           /* :327 */
+    for (int l = 1; l < nlay; l++)                                                                     /* :328-332 */
+      tv[l] = ((pa[l - 1] * ta[l - 1]) * (pv[l] - pa[l]) + (pa[l] * ta[l]) * (pa[l - 1] - pv[l])) /
+              (pv[l] * (pa[l - 1] - pa[l]));
+    tv[nlay] = ta[nlay - 1] + ((pv[nlay] - pa[nlay - 1]) * (ta[nlay - 1] - ta[nlay - 2])) /           /* :333-334 */
+                                  (pa[nlay - 1] - pa[nlay - 2]);
+  }
+}
+
 /* neural/mod_activation.F90:107-184 (bias_and_activation variants) */
 static float activate(int act, float x)
 {
@@ -153,6 +171,24 @@ void orc_nn_tau_post(int ngpt, long nbatch, float *y, const float *mean, const f
 void orc_square(long n, float *y)
 {
   for (long i = 0; i < n; i++) y[i] = y[i] * y[i];
+}
+
+/* The single-model ("both") branch of predict_nn_lw_blas_sp: rrtmgp/kernels/mo_gas_optics_kernels.F90:744-772 on
+ * the output of output_sgemm_lw (neural/mod_network_rrtmgp.F90:319-409: the MLP with the linear last layer, no
+ * scaling).  y (2*ngpt, nbatch): rows 1..ngpt are the scaled absorption output, rows ngpt+1..2*ngpt the square root
+ * of the Planck fraction.  tau = (ystd*y + ymeans)**8 then tau*col_dry (:760-764; ystd/ymeans are the first ngpt
+ * output coefficients, :752-753); pfrac = y(igpt+ngpt)*y(igpt+ngpt) (:766). */
+void orc_nn_both_post(int ngpt, long nbatch, const float *y, const float *mean, const float *std,
+                      const float *coldry, float *tau, float *pfrac)
+{
+  for (long j = 0; j < nbatch; j++)
+    for (int i = 0; i < ngpt; i++) {
+      const float *yj = y + (size_t)2 * ngpt * j;
+      float t = std[i] * yj[i] + mean[i];
+      float t2 = t * t, t4 = t2 * t2, t8 = t4 * t4;
+      tau[(size_t)ngpt * j + i] = t8 * coldry[j];
+      pfrac[(size_t)ngpt * j + i] = yj[i + ngpt] * yj[i + ngpt];
+    }
 }
 
 /* rrtmgp/kernels/mo_gas_optics_kernels.F90:1024-1043 (interpolate1D) */

@@ -5,6 +5,8 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -22,6 +24,19 @@ int fail(int code, const std::string &msg)
 {
   g_last_error = msg;
   return code;
+}
+
+int raise_lds_limit(const void *kernel)
+{
+  static std::mutex mu;
+  static std::set<std::pair<const void *, int>> done;
+  int dev = 0;
+  RRTMGPNN_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count({kernel, dev})) return RRTMGPNN_OK;
+  RRTMGPNN_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  done.insert({kernel, dev});
+  return RRTMGPNN_OK;
 }
 
 // activation names of neural/mod_layer.F90:64-121 (set_activation) -> the codes of network_create
@@ -97,6 +112,16 @@ using namespace rrtmgpnn;
 
 int rrtmgpnn_context::workspace(size_t bytes, void **out)
 {
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) == hipSuccess && cap == hipStreamCaptureStatusActive) {
+    if (bytes > ws_bytes)
+      return fail(RRTMGPNN_ERR_ARGUMENT, "workspace would grow inside a hipGraph capture: issue the call once "
+                                         "eagerly before capturing");
+    ws_pinned = true;  // the captured graph holds this address from now on
+  }
+  if (bytes > ws_bytes && ws_pinned)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "workspace is pinned by a captured hipGraph and too small for this call: use "
+                                       "another context, or rrtmgpnn_context_unpin_workspace after destroying the graph");
   if (bytes > ws_bytes) {
     if (ws) {
       (void)hipStreamSynchronize(stream);
@@ -145,9 +170,16 @@ int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx)
   return RRTMGPNN_OK;
 }
 
+int rrtmgpnn_context_unpin_workspace(rrtmgpnn_context *ctx)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  ctx->ws_pinned = false;
+  return RRTMGPNN_OK;
+}
+
 int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode)
 {
-  if (mode < 0 || mode > 2) return fail(RRTMGPNN_ERR_ARGUMENT, "sw kernel mode must be 0, 1 or 2");
+  if (mode < 0 || mode > 3) return fail(RRTMGPNN_ERR_ARGUMENT, "sw kernel mode must be 0, 1, 2 or 3");
   if (!ctx) {
     rrtmgpnn::g_sw_kernel_default = mode;
     return RRTMGPNN_OK;

@@ -33,11 +33,18 @@ constexpr int kMaxLayers = 7;   // network layers (excluding input)
 constexpr int kMaxInputs = 32;  // NN input features
 constexpr int kMaxBands = 64;
 extern int g_sw_kernel_default;  // rrtmgpnn_context_set_sw_kernel(NULL, mode)
+// Raise a kernel's dynamic-LDS limit to 160 KiB on the current device, once per (kernel, device): a function
+// attribute is per device, so a second GPU of the same process gets its own call.  Thread-safe; after the first
+// call for a (kernel, device) pair it makes no HIP call (hipGraph captures stay attribute-free).
+int raise_lds_limit(const void *kernel);
 
 }  // namespace rrtmgpnn
 
 // Device workspace owned by a context: grown on demand, never shrunk, so steady-state calls
-// (and hipGraph capture of them) perform no allocation.
+// (and hipGraph capture of them) perform no allocation.  A call made while the context's stream is being
+// captured pins the buffer (ws_pinned): the graph holds its address, so a later call that would grow it fails
+// with RRTMGPNN_ERR_ARGUMENT instead of freeing memory the graph still writes (rrtmgpnn_context_unpin_workspace
+// once the graph is destroyed; or give the graph a context of its own).
 struct rrtmgpnn_context {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -46,6 +53,7 @@ struct rrtmgpnn_context {
   int sw_kernel = -1;  // SW two-stream kernel: 0 by ngpt, 1 / 2 g-points per lane, -1 the library default
   void *ws = nullptr;
   size_t ws_bytes = 0;
+  bool ws_pinned = false;
   int workspace(size_t bytes, void **out);
 };
 
@@ -148,6 +156,13 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
 // kernels_sw_x2.hip (called by launch_sw_2stream for even ngpt; ws sized by it)
 size_t sw_2stream_x2_layer_planes(bool inc);
 int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                         const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
+                         const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
+                         const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
+                         float *flux_dn, float *flux_dir);
+// kernels_sw_ck.hip (checkpointed passes; called by launch_sw_2stream for even ngpt in mode 3)
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol);
+int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,

@@ -628,13 +628,9 @@ static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
   auto kern = mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS, NGTC, XIN, NT>;
   size_t lds = sizeof(float) * (size_t)(a.imgA_floats + ((MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR) ? a.imgB_floats : 0));
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: weight images exceed 160 KiB of LDS");
-  // Raise the dynamic-LDS limit once per instantiation (kept out of the per-call path so the launch
-  // sequence is capturable into a hipGraph).
-  static size_t lds_set = 0;
-  if (lds > lds_set) {
-    RRTMGPNN_HIP(hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    lds_set = 160 * 1024;
-  }
+  // the dynamic-LDS limit, raised once per (instantiation, device)
+  if (lds > 64 * 1024)
+    if (int rc = raise_lds_limit((const void *)kern)) return rc;
   long long ntiles = (a.nbatch + 15) / 16;
   constexpr int kThreads = NT;
   const int wpb = kThreads / 64;

@@ -722,12 +722,17 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   // two g-points per lane (kernels_sw_x2.hip, 4 columns per 7-wave block) whenever ngpt is even: alone 7 % faster at
   // C3 and the whole step 1.8 % (C3) / 2 % (C4) faster than one g-point per lane (tools/cmp_sw_kernel.sh)
   const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
-  const bool x2 = kSwX2 && (ngpt % 2) == 0 && mode != 1;
+  const bool ck = (ngpt % 2) == 0 && mode == 3;
+  const bool x2 = !ck && kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc && kSwIncPark ? 3 : 0);
-  const size_t nws = 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
+  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol)
+                        : 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
   int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;
+  if (ck)
+    return launch_sw_2stream_ck(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
+                                alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
   if (x2)
     return launch_sw_2stream_x2(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
                                 alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);

@@ -414,16 +414,10 @@ int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   const BandArgs &b = bands ? *bands : nob;
   const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
   constexpr int PF = RRTMGPNN_SW2_PF, PFN = RRTMGPNN_SW2_PF_NOG, PFI = RRTMGPNN_SW2_PF_INC;
-  // rings past 64 KiB (4 columns of 224 g-points: 64.5 KiB) need the dynamic-LDS limit raised, once for all four
-  // instantiations (so later calls, and hipGraph captures of them, make no attribute call)
-  static bool lds_raised = false;
-  if (lds > 64 * 1024 && !lds_raised) {
-    const void *ks[4] = {(const void *)sw_2stream_x2_kernel<true, true, PF>, (const void *)sw_2stream_x2_kernel<false, true, PFI>,
-                         (const void *)sw_2stream_x2_kernel<true, false, PF>, (const void *)sw_2stream_x2_kernel<false, false, PFN>};
-    for (const void *k : ks) RRTMGPNN_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    lds_raised = true;
-  }
   auto go = [&](auto kern, const float *tb, const float *sb, const float *gb) -> int {
+    // rings past 64 KiB (4 columns of 224 g-points: 64.5 KiB) need the dynamic-LDS limit raised (per device)
+    if (lds > 64 * 1024)
+      if (int rc = raise_lds_limit((const void *)kern)) return rc;
     hipLaunchKernelGGL(kern, grid, block, lds, ctx->stream, ngpt, nlay, ncol, top_at_1, ncb, inc_flux, inc_flux_dif,
                        tau, ssa, g, mu0, alb_dir, alb_dif, b, tb, sb, gb, (float *)ws, flux_up, flux_dn, flux_dir);
     RRTMGPNN_LAUNCH_CHECK("sw_2stream_x2_kernel");

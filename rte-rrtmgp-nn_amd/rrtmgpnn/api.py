@@ -55,6 +55,10 @@ class Context:
     def synchronize(self):
         check(_lib.lib().rrtmgpnn_context_synchronize(self.h), "context_synchronize")
 
+    def unpin_workspace(self):
+        """After destroying every hipGraph captured on this context: let its workspace grow again."""
+        check(_lib.lib().rrtmgpnn_context_unpin_workspace(self.h), "context_unpin_workspace")
+
     def set_sw_kernel(self, mode):
         """0: SW two-stream kernel by ngpt (two g-points per lane when even; default); 1 / 2: one / two (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_sw_kernel(self.h, int(mode)), "context_set_sw_kernel")

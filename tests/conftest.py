@@ -12,9 +12,10 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box with -m gpu)")
 
 
-@pytest.fixture(params=[1, 2], ids=["sw1", "sw2"])
+@pytest.fixture(params=[1, 2, 3], ids=["sw1", "sw2", "sw3"])
 def sw_kernel(request):
-    """Force each SW two-stream kernel (one / two g-points per lane) for the test, then restore the size rule."""
+    """Force each SW two-stream kernel (one / two g-points per lane / checkpointed passes) for the test, then restore
+    the size rule."""
     from rrtmgpnn import api
     api.set_sw_kernel_default(request.param)
     yield request.param

@@ -207,3 +207,35 @@ def test_lw_only_step_equals_lw_half(dev, rfmip, allsky):
     for k in ("lw_up", "lw_dn"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
         np.testing.assert_array_equal(a[k], c[k], err_msg=k)
+
+
+def test_captured_graph_pins_context_workspace(dev, rfmip):
+    """A hipGraph captured on a context holds the address of its workspace: a later, larger call on the same context
+    must fail loudly instead of freeing memory the graph still writes; the graph keeps replaying
+    correctly, and unpinning after the graph is gone lets the workspace grow again."""
+    from rrtmgpnn._lib import RrtmgpnnError
+    from rrtmgpnn.api import Context
+    from rrtmgpnn.pipeline import ClearSkyStep
+    ctx = Context(0)
+    # one stream: the SW solver (the step's workspace user) then runs on ctx
+    small = ClearSkyStep(subset(rfmip, np.arange(0, 64)), device=0, ctx=ctx, overlap=False)
+    small.capture()
+    small.replay()
+    torch.cuda.synchronize()
+    ref = small.fluxes()
+    big = ClearSkyStep(subset(rfmip, np.arange(0, 1800, 2)), device=0, ctx=ctx, overlap=False)
+    with pytest.raises(RrtmgpnnError, match="pinned"):
+        big.step()
+    torch.cuda.synchronize()
+    for t in (small.sw_up, small.sw_dn, small.lw_up):
+        t.fill_(float("nan"))
+    small.replay()
+    torch.cuda.synchronize()
+    got = small.fluxes()
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k])
+    del small.graph
+    ctx.unpin_workspace()
+    big.step()
+    torch.cuda.synchronize()
+    assert np.isfinite(big.fluxes()["sw_dn"]).all()

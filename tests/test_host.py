@@ -96,7 +96,7 @@ def test_c_abi_errors_are_reported_not_crashed():
     assert L.rrtmgpnn_lw_solver_noscat(None, 256, 60, 1, 1, 1, None, None, None, None, None, None, None, None, None,
                                        None) != 0
     assert b"null context" in L.rrtmgpnn_last_error()
-    assert L.rrtmgpnn_context_set_sw_kernel(None, 3) != 0 and b"sw kernel mode" in L.rrtmgpnn_last_error()
+    assert L.rrtmgpnn_context_set_sw_kernel(None, 4) != 0 and b"sw kernel mode" in L.rrtmgpnn_last_error()
     assert L.rrtmgpnn_context_set_sw_kernel(None, 0) == 0
 
 

@@ -16,7 +16,7 @@ import re
 import sys
 
 STAGES = [
-    (re.compile(r"sw_2stream(?:_x2)?_kernel"), "sw_solver"),
+    (re.compile(r"sw_2stream(?:_x2|_ck)?_kernel"), "sw_solver"),
     (re.compile(r"lw_noscat_kernel"), "lw_solver"),
     # mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS>: MODE 1 LW pair, 4 LW "both", 2 SW pair
     (re.compile(r"mlp_pair_kernel<(?:\s*\d+\s*,){6}\s*[14]\s*,"), "predict_nn_lw"),
