@@ -7,10 +7,14 @@ configs[2] "RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics both 
 gas_optics(LW, NN) + rte_lw + gas_optics(SW, NN) + rte_sw over the block, inputs resident in HBM.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each processing its own 1800-column block (weak scaling: columns are independent, no
-collective in the data path); barrier + synchronize around the timed region, max over ranks.
-After timing, the broadband fluxes are all-gathered once over RCCL (the final flux reduction the
-north star names), timed separately ("gather_ms"), outside `value`.
+GPU.  The job is one global problem partitioned by rrtmgpnn.shard.column_range (the gloo-tested
+partition): by default N x the config's block (weak scaling, N x 1800 RFMIP columns at C3, each rank
+a 1800-column block); with --global the config's fixed global size (C5: 1e6 synthetic columns x 137
+layers, strong scaling), each rank streaming its range through the step in chunks of at most
+125 000 columns.  No collective in the data path; barrier + synchronize around the timed region, max
+over ranks.  After timing, the broadband fluxes are all-gathered once with shard.gather_columns over
+RCCL (the final flux reduction the north star names), timed as "gather_ms" and folded into
+"end_to_end" (all columns / (timed steps + gather)), never into `value`.
 
 Prints ONE JSON line on rank 0.
 """
@@ -39,6 +43,9 @@ def parse():
                     help="c3: RFMIP 1800x60 LW+SW (default, the metric's config); c2: the same columns, LW only "
                          "(BASELINE configs[1], metric in LW columns/s); c4: 10000x60 synthetic all-sky; "
                          "c5: 125000x137 synthetic clear-sky per GPU")
+    ap.add_argument("--global", dest="global_cols", nargs="?", type=int, const=-1, default=0,
+                    help="partition one global problem of this many columns over the ranks (strong scaling; "
+                         "without a value the config's global size: C5 1e6 columns); default: N x the config's block")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
     ap.add_argument("--unfused", action="store_true",
@@ -122,43 +129,85 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from rrtmgpnn import data
+    from rrtmgpnn import data, shard
     from rrtmgpnn.pipeline import ClearSkyStep
 
-    clouds = None
+    # ---- the global problem and this rank's part of it (shard.column_range) ----
     metric = METRIC
+    block = {"c2": 1800, "c3": 1800, "c4": 10000, "c5": 125000}[args.config]
+    nlay_cfg = 137 if args.config == "c5" else 60
+    if args.global_cols:
+        global_cols = 1000000 if (args.global_cols < 0 and args.config == "c5") else (
+            args.global_cols if args.global_cols > 0 else block * world)
+        scaling = "strong"
+    else:
+        global_cols = block * world
+        scaling = "weak"
+    lo, hi = shard.column_range(global_cols, rank, world)
+    chunks = [(c, min(c + block, hi)) for c in range(lo, hi, block)] or [(lo, lo)]
+
+    def problem(c0, c1):
+        """Columns [c0, c1) of the global problem (and their clouds at C4)."""
+        if args.config in ("c2", "c3"):
+            return data.rfmip_columns(c0, c1 - c0), None
+        p = data.synthetic_problem(c1 - c0, nlay_cfg, seed=20251015, col0=c0)
+        return p, (data.allsky_clouds(p, data.load_cloud_optics("lw")) if args.config == "c4" else None)
+
     if args.config == "c2":
-        prob = data.rfmip_problem()
         workload = "C2: RFMIP clear-sky LW only, 1800 columns x 60 layers x 256 g-points, NN gas optics (g256)"
         data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
         metric = "atmospheric columns/sec (LW clear-sky fluxes), 1 MI355X"
     elif args.config == "c3":
-        prob = data.rfmip_problem()
         workload = "C3: RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics (g256 LW + g224 SW)"
         data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
     elif args.config == "c4":
-        prob = data.synthetic_problem(10000, 60, seed=20251015 + rank)
-        clouds = data.allsky_clouds(prob, data.load_cloud_optics("lw"))
         workload = ("C4: all-sky LW+SW, 10000 synthetic columns x 60 layers, NN gas optics + cloud_optics (LUT, ice "
                     "roughness 2; LW 1scl increment, SW delta-scaled 2str increment)")
-        data_desc = ("synthetic columns drawn from RFMIP profiles (PCG64 seed 20251015+rank); clouds by the all-sky "
-                     "example's recipe (rrtmgp_allsky.F90:329-350); the reference's cloud-optics coefficients")
+        data_desc = ("synthetic columns drawn from RFMIP profiles (PCG64 streams seeded by (20251015, column block)); "
+                     "clouds by the all-sky example's recipe (rrtmgp_allsky.F90:329-350); the reference's cloud-optics "
+                     "coefficients")
     else:
-        prob = data.synthetic_problem(125000, 137, seed=20251015 + rank)
-        workload = "C5 shard: 125000 synthetic columns x 137 layers per GPU, clear-sky LW+SW"
-        data_desc = "synthetic columns interpolated from RFMIP profiles (PCG64 seed 20251015+rank)"
+        workload = ("C5: 1e6 synthetic columns x 137 layers clear-sky LW+SW, column-sharded" if scaling == "strong"
+                    else "C5 shard: 125000 synthetic columns x 137 layers per GPU, clear-sky LW+SW")
+        data_desc = ("synthetic columns interpolated from RFMIP profiles (PCG64 streams seeded by (20251015, column "
+                     "block))")
     if args.sw_kernel:
         from rrtmgpnn import api
         api.set_sw_kernel_default(args.sw_kernel)
+    prob, clouds = problem(*chunks[0])
     step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap,
                         sw=args.config != "c2")
     ncol, nlay = step.ncol, step.nlay
+    ins, outs = step.io_tensors()
+    # more than one chunk: every chunk's inputs resident in HBM, copied into the step's buffers before its replay and
+    # its fluxes copied out after it (device-to-device, inside the timed region)
+    chunk_ins = [None] * len(chunks)
+    rank_flux = None
+    if len(chunks) > 1:
+        chunk_ins[0] = [t.clone() for t in ins]
+        for k, (c0, c1) in enumerate(chunks[1:], 1):
+            if c1 - c0 != ncol:  # a short last chunk would need a step of its own shape
+                raise SystemExit("bench: rank range %d..%d does not split into %d-column chunks" % (lo, hi, ncol))
+            pk, ck = problem(c0, c1)
+            chunk_ins[k] = step.inputs_for(pk, ck)
+        rank_flux = [torch.empty((hi - lo,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev) for o in outs]
 
     use_graph = not args.no_graph
-    run = step.step
+    run_one = step.step
     if use_graph:
         step.capture()
-        run = step.replay
+        run_one = step.replay
+
+    def run():
+        if len(chunks) == 1:
+            run_one()
+            return
+        for k, (c0, c1) in enumerate(chunks):
+            for d, src in zip(ins, chunk_ins[k]):
+                d.copy_(src, non_blocking=True)
+            run_one()
+            for r, o in zip(rank_flux, outs):
+                r[c0 - lo:c1 - lo].copy_(o, non_blocking=True)
 
     for _ in range(args.warmup):
         run()
@@ -179,11 +228,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
-    total_cols = ncol * world * args.steps
+    total_cols = global_cols * args.steps
     value = total_cols / elapsed
 
-    # ---- host-resident variant: pinned H2D of every input, the step, D2H of the fluxes (never `value`) ----
+    # ---- host-resident variant: pinned H2D of every input, the step, D2H of the fluxes (never `value`; one chunk) ----
     ins, outs = step.io_tensors()
+    run = run_one
     h_ins = [t.cpu().pin_memory() for t in ins]
     h_outs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in outs]
     io_bytes = sum(t.numel() * 4 for t in ins) + sum(t.numel() * 4 for t in outs)
@@ -302,18 +352,26 @@ def main():
         if roof is not None and sq.get(name, {}).get("valu_busy") is not None:
             roof["valu_busy"] = sq[name]["valu_busy"]  # the solvers' binding limit: VALU issue
 
-    # ---- final flux all-gather over RCCL (outside the timed region) ----
+    # ---- final flux all-gather over RCCL (outside the timed region): shard.gather_columns, the partition's
+    # tested exchange, of the rank's (ncol, 5, nlev) flux slab into the global (global_cols, 5, nlev) array ----
     gather_ms = None
+    end_to_end = None
     if world > 1:
-        flat = torch.cat([step.lw_up.reshape(-1), step.lw_dn.reshape(-1), step.sw_up.reshape(-1),
-                          step.sw_dn.reshape(-1), step.sw_dir.reshape(-1)])
-        outs = [torch.empty_like(flat) for _ in range(world)]
+        fl = rank_flux if rank_flux is not None else outs
+        local_slab = torch.stack(list(fl), dim=1)
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
-        dist.all_gather(outs, flat)
+        full = shard.gather_columns(local_slab, global_cols, world)
         torch.cuda.synchronize(dev)
         gather_ms = (time.perf_counter() - g0) * 1e3
+        t = torch.tensor([gather_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gather_ms = float(t.item())
+        assert full.shape[0] == global_cols
+        del full
+        end_to_end = {"value": round(total_cols / (elapsed + gather_ms * 1e-3), 1), "unit": "columns/s",
+                      "note": "all ranks' columns over the timed steps plus one final flux all-gather"}
 
     # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
     cpu = None
@@ -326,9 +384,11 @@ def main():
         out = {
             "metric": metric, "value": round(value, 1), "unit": "columns/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": data_desc,
-            "config": {"workload": workload, "ncol_per_gpu": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
-                       "ngpt_sw": step.ng_sw if step.sw else None, "parallelism": "column-sharded, 1 process per GPU",
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data_desc,
+            "config": {"workload": workload, "global_columns": global_cols, "ncol_per_gpu": hi - lo,
+                       "chunk_columns": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
+                       "ngpt_sw": step.ng_sw if step.sw else None,
+                       "parallelism": "column-sharded (shard.column_range), 1 process per GPU",
                        "launch": ("hipGraph replay" if use_graph else "eager") +
                                  (", LW and SW chains on two streams" if step.overlap else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
@@ -341,6 +401,7 @@ def main():
             "stages_overlapped_ms": None if stages_ov is None else {k: round(v, 4) for k, v in stages_ov.items()},
             "stage_roofline": stage_roofs,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "end_to_end": end_to_end,
             "host_resident": pcie,
         }
         print(json.dumps(out), flush=True)

@@ -198,6 +198,14 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
                                const float *tau, const float *ssa, const float *g, const float *mu0,
                                const float *sfc_alb_dir_gpt, const float *sfc_alb_dif_gpt,
                                float *flux_up, float *flux_dn, float *flux_dir);
+/* rte_sw on absorption-only (1scl) properties (rte/mo_rte_sw.F90:213-222): apply_BC_factor (top level =
+ * inc_flux * mu0, rte/kernels/mo_rte_solver_kernels.F90:1685-1704) and sw_solver_noscat (:496-532), broadband direct
+ * flux (nlay+1, ncol) = sum over g of each column's direct beam (sum_broadband_nocol, sequential).  The reference's
+ * rte_sw swaps the spectral and broadband arguments of sw_solver_noscat (quirk B-10) and the kernel sums column 1 for
+ * every column (B-11): this entry follows the kernels' evident meaning; the spectral beam is the reference's bit for
+ * bit (tests/test_oracle.py).  inc_flux (ngpt, ncol), tau (ngpt, nlay, ncol), mu0 (ncol). */
+int rrtmgpnn_sw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                              const float *tau, const float *mu0, float *flux_dir);
 /* rrtmgpnn_sw_solver_2stream of the atmosphere incremented by band-resolved two-stream properties
  * (tau, ssa, g)_bnd (nbnd, nlay, ncol) -- clouds%increment(atmos) (inc_2stream_by_2stream_bybnd,
  * rte/kernels/mo_optical_props_kernels.F90:430-463) fused into the solver: same fluxes, bit for bit, as

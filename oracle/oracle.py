@@ -60,6 +60,7 @@ class Oracle:
         L.orc_sw_solver_2stream.argtypes = [c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                             _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_expand.argtypes = [c_int, c_int, c_int, _i32p, _f32p, _f32p]
+        L.orc_sw_solver_noscat.argtypes = [c_int] * 4 + [_f32p] * 4 + [c_vp]
         L.orc_cloud_optics.argtypes = ([c_int] * 4 + [c_float] * 4 + [_f32p] * 6 + [c_int] + [_f32p] * 12 +
                                        [c_int, c_int] + [_f32p] * 4 + [c_int] + [_f32p] * 3)
         L.orc_increment_bybnd.argtypes = [c_int] * 4 + [_i32p, c_int, _f32p, _f32p, _f32p, c_int, _f32p, _f32p, _f32p]
@@ -194,6 +195,15 @@ class Oracle:
         self.L.orc_sw_solver_2stream(ngpt, nlay, ncol, int(top_at_1), f32(inc_flux), dif, f32(tau), f32(ssa), f32(g),
                                      f32(mu0), f32(alb_dir_gpt), f32(alb_dif_gpt), up, dn, dr)
         return up, dn, dr
+
+    def sw_solver_noscat(self, tau, mu0, inc_flux, top_at_1=True, gpt=False):
+        """rte_sw on 1scl properties: apply_BC_factor + sw_solver_noscat (rte/mo_rte_sw.F90:213-222) -> flux_dir
+        (and the spectral direct flux (ncol, nlay+1, ngpt) when gpt)."""
+        ncol, nlay, ngpt = tau.shape
+        dr = np.zeros((ncol, nlay + 1), np.float32)
+        g = np.zeros((ncol, nlay + 1, ngpt), np.float32) if gpt else None
+        self.L.orc_sw_solver_noscat(ngpt, nlay, ncol, int(top_at_1), f32(inc_flux), f32(tau), f32(mu0), dr, _ptr(g))
+        return (dr, g) if gpt else dr
 
     def cloud_optics(self, co, clwp, ciwp, reliq, reice, nstr=2, lut=True, icergh=1):
         """ty_cloud_optics%cloud_optics (extensions/cloud_optics/mo_cloud_optics.F90:354-535); by band."""
@@ -358,6 +368,17 @@ class Reference:
         L.ref_increment_bybnd.restype = c_int
         L.ref_delta_scale.argtypes = [c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, c_int, _f32p]
         L.ref_delta_scale.restype = c_int
+        L.ref_sw_noscat.argtypes = [c_int] * 4 + [_f32p] * 5
+        L.ref_sw_noscat.restype = c_int
+
+    def sw_noscat(self, tau, mu0, inc_flux, top_at_1=True):
+        """The reference's apply_BC (-> apply_BC_factor) + sw_solver_noscat kernels: broadband and spectral direct
+        flux (the broadband one is column 1's for every column, quirk B-11)."""
+        ncol, nlay, ngpt = tau.shape
+        dr = np.zeros((ncol, nlay + 1), np.float32)
+        g = np.zeros((ncol, nlay + 1, ngpt), np.float32)
+        self._check(self.L.ref_sw_noscat(ncol, nlay, ngpt, int(top_at_1), f32(inc_flux), f32(tau), f32(mu0), dr, g))
+        return dr, g
 
     def _check(self, rc):
         if rc != 0:

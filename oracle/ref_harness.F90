@@ -6,6 +6,10 @@
 ! output goes to oracle/_ref/ only.  Exposes:
 !   ref_rte_lw   -> rte_lw (rte/mo_rte_lw.F90:60) on ty_optical_props_1scl + ty_source_func_lw
 !   ref_rte_sw   -> rte_sw (rte/mo_rte_sw.F90:48) on ty_optical_props_2str
+!   ref_sw_noscat -> the kernels of rte_sw's 1scl branch (rte/mo_rte_sw.F90:213-222): apply_BC (the generic resolves
+!                    to apply_BC_factor, rte/kernels/mo_rte_solver_kernels.F90:1685-1704) and sw_solver_noscat
+!                    (:496-532), called with the kernels' own argument meaning (rte_sw swaps the spectral and the
+!                    broadband direct-flux arrays at :220-222, quirk B-10, so rte_sw itself is not called)
 !   ref_mlp      -> network_type%output_sgemm_flat (neural/mod_network.F90:273) with MKL sgemm
 !   ref_cloud_optics -> ty_cloud_optics%load (LUT or Pade) + set_ice_roughness + cloud_optics
 !                       (extensions/cloud_optics/mo_cloud_optics.F90) into 1scl or 2str by band
@@ -15,7 +19,8 @@
 ! mo_gas_optics_kernels) are not built: netcdf-fortran is absent and we do not stub it.
 module ref_harness
   use, intrinsic :: iso_c_binding
-  use mo_rte_kind,         only: wp
+  use mo_rte_kind,         only: wp, wl
+  use mo_rte_solver_kernels, only: apply_BC, sw_solver_noscat
   use mo_optical_props,    only: ty_optical_props_1scl, ty_optical_props_2str
   use mo_source_functions, only: ty_source_func_lw
   use mo_fluxes,           only: ty_fluxes_flexible
@@ -168,6 +173,16 @@ contains
     end do
     ref_mlp = 0
   end function ref_mlp
+
+  integer(c_int) function ref_sw_noscat(ncol, nlay, ngpt, top_at_1, inc_flux, tau, mu0, flux_dir, gpt_flux_dir) &
+      bind(C, name="ref_sw_noscat")
+    integer(c_int), value :: ncol, nlay, ngpt, top_at_1
+    real(c_float),  intent(in) :: inc_flux(ngpt, ncol), tau(ngpt, nlay, ncol), mu0(ncol)
+    real(c_float),  intent(out) :: flux_dir(nlay+1, ncol), gpt_flux_dir(ngpt, nlay+1, ncol)
+    call apply_BC(ngpt, nlay, ncol, logical(top_at_1 /= 0, wl), inc_flux, mu0, gpt_flux_dir)
+    call sw_solver_noscat(ngpt, nlay, ncol, logical(top_at_1 /= 0, wl), tau, mu0, gpt_flux_dir, flux_dir)
+    ref_sw_noscat = 0
+  end function ref_sw_noscat
 
   subroutine ref_last_error(buf, n) bind(C, name="ref_last_error")
     integer(c_int), value :: n

@@ -538,6 +538,52 @@ void orc_lw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const flo
 }
 
 /* ---------------------------------------------------------------------------------------------
+ * SW direct beam without scattering (rte_sw on ty_optical_props_1scl, rte/mo_rte_sw.F90:213-222):
+ *   apply_BC(..., inc_flux, mu0, flux_dir) -> the generic resolves to apply_BC_factor
+ *     (rte/kernels/mo_rte_solver_kernels.F90:1685-1704): flux_dir(:, top) = inc_flux * mu0;
+ *   sw_solver_noscat (:496-532): mu0_inv = 1/mu0; flux_dir(:, l+1) = flux_dir(:, l) * exp(-tau(:, l) * mu0_inv)
+ *     walking down from the top; flux_dir_bb = sum(flux_dir, 1) per level (sum_broadband_nocol,
+ *     rte/kernels/mo_fluxes_broadband_kernels.F90:40-47: one sequential sum over g).
+ * The reference's rte_sw passes fluxes%flux_dn_dir and fluxes%gpt_flux_dn_dir in each other's positions (:220-222;
+ * quirk B-10 in DESIGN.md): this follows the kernels' own argument meaning.  sw_solver_noscat also sums the whole
+ * spectral array from its first column for every column (:530 passes flux_dir, not flux_dir(:,:,icol); quirk
+ * B-11): the broadband sum here is each column's own, which equals the reference's for column 1.  inc_flux (ngpt, ncol), tau (ngpt, nlay,
+ * ncol), mu0 (ncol) -> flux_dir (nlay+1, ncol).
+ * ------------------------------------------------------------------------------------------- */
+void orc_sw_solver_noscat(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux, const float *tau,
+                          const float *mu0, float *flux_dir, float *gpt_flux_dir /* (ngpt, nlay+1, ncol) or NULL */)
+{
+#pragma omp parallel
+  {
+    float *f = (float *)malloc(sizeof(float) * ngpt * (nlay + 1));
+#pragma omp for schedule(static)
+    for (int icol = 0; icol < ncol; icol++) {
+      const float mu0_inv = 1.0f / mu0[icol];
+      const int top = top_at_1 ? 0 : nlay;
+      for (int i = 0; i < ngpt; i++) f[i + (size_t)ngpt * top] = inc_flux[i + (size_t)ngpt * icol] * mu0[icol];
+      const float *t = tau + (size_t)ngpt * nlay * icol;
+      if (top_at_1) {
+        for (int l = 1; l <= nlay; l++)
+          for (int i = 0; i < ngpt; i++)
+            f[i + (size_t)ngpt * l] = f[i + (size_t)ngpt * (l - 1)] * expf(-t[i + (size_t)ngpt * (l - 1)] * mu0_inv);
+      } else {
+        for (int l = nlay - 1; l >= 0; l--)
+          for (int i = 0; i < ngpt; i++)
+            f[i + (size_t)ngpt * l] = f[i + (size_t)ngpt * (l + 1)] * expf(-t[i + (size_t)ngpt * l] * mu0_inv);
+      }
+      float *o = flux_dir + (size_t)(nlay + 1) * icol;
+      for (int l = 0; l <= nlay; l++) {
+        float s = 0.0f;
+        for (int i = 0; i < ngpt; i++) s += f[i + (size_t)ngpt * l];
+        o[l] = s;
+      }
+      if (gpt_flux_dir) memcpy(gpt_flux_dir + (size_t)ngpt * (nlay + 1) * icol, f, sizeof(float) * ngpt * (nlay + 1));
+    }
+    free(f);
+  }
+}
+
+/* ---------------------------------------------------------------------------------------------
  * SW two-stream: rte/kernels/mo_rte_solver_kernels.F90:541-692 (sw_solver_2stream),
  * sw_two_stream_source :1366-1480, adding :1526-1637.  k_min = 1e-4 (sp, :76-82).
  * ------------------------------------------------------------------------------------------- */

@@ -691,6 +691,15 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
                            sfc_alb_dif_gpt, nullptr, nullptr, nullptr, nullptr, flux_up, flux_dn, flux_dir);
 }
 
+int rrtmgpnn_sw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                              const float *tau, const float *mu0, float *flux_dir)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!inc_flux || !tau || !mu0 || !flux_dir || ngpt < 1 || nlay < 1 || ncol < 0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "sw_solver_noscat: bad argument");
+  return launch_sw_noscat(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, mu0, flux_dir);
+}
+
 int rrtmgpnn_sw_solver_2stream_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
                                    const float *inc_flux, const float *inc_flux_dif, const float *tau,
                                    const float *ssa, const float *g, int nbnd, const int *band_lims_gpt,

@@ -33,7 +33,7 @@ __device__ __forceinline__ RsLayer rs_layer(float tau, float ssal, float g, floa
   const float scaleTau = (1.0f - ssal + wb);
   r.Cn = 0.4f * wb / scaleTau;
   const float t = tau * D * scaleTau;
-  r.trans = ref_expf_nb(-t, etab);
+  r.trans = solver_exp_neg(-t, etab);
   r.An = (1.0f - r.trans * r.trans);
   const float T = r.trans;
   const float fact = (t > tau_thresh) ? (1.0f - T) / t - T : t * (0.5f - 1.0f / 3.0f * t);
@@ -172,7 +172,7 @@ __device__ __forceinline__ L2Layer l2_layer(float tau, float w0, float g, float 
   const float gamma1 = LW_diff_sec * (1.0f - 0.5f * w0 * (1.0f + g));
   const float gamma2 = LW_diff_sec * 0.5f * w0 * (1.0f - g);
   const float k = sqrtf(fmaxf((gamma1 - gamma2) * (gamma1 + gamma2), k_min));
-  const float emk = ref_expf_nb(-tau * k, etab);
+  const float emk = solver_exp_neg(-tau * k, etab);
   const float em2k = emk * emk;
   const float RT = 1.0f / (k * (1.0f + em2k) + gamma1 * (1.0f - em2k));
   r.Rdif = RT * gamma2 * (1.0f - em2k);

@@ -17,12 +17,9 @@
 namespace rrtmgpnn {
 
 // Ablation switches for tools/ablate_solvers.sh (never set in the product build): they break parity
-// on purpose to attribute solver time.  RRTMGPNN_ABL_NATIVE_EXP: device expf instead of ref_expf;
-// RRTMGPNN_ABL_NO_REDUCE: skip the ordered broadband reduction (barriers kept);
-// RRTMGPNN_ABL_NO_BARRIER: skip staging and flushing entirely.
-#ifdef RRTMGPNN_ABL_NATIVE_EXP
-#define ref_expf_tab(x, t) __expf(x)
-#endif
+// on purpose to attribute solver time.  RRTMGPNN_ABL_NO_REDUCE: skip the ordered broadband reduction (barriers
+// kept); RRTMGPNN_ABL_NO_BARRIER: skip staging and flushing entirely.  (The hardware-exp variant is the opt-in
+// tolerance build RRTMGPNN_FAST_LIBM, rte_device.hpp.)
 
 __device__ __forceinline__ float wave_sum(float v)
 {
@@ -463,7 +460,7 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   SwCoef c;
   const SwDif d = sw_dif(tau, w0, g, etab);
   const float gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
-  float Tnoscat = solver_exp_neg(-tau * mu0_inv, etab);
+  float Tnoscat = solver_exp_beam(-tau * mu0_inv, etab);
   float gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? 0.5f : (2.0f - 3.0f * mu0 * g) * .25f;
   float gamma4 = 1.0f - gamma3;
   float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
@@ -583,7 +580,7 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
           pt[p] = Ttau.ld(vL, row * ln);
           pi[p] = ld_bnd(Bt, ln);
         }
-        if (j < nlay) Fd = solver_exp_neg(-t * mu0_inv, etab) * Fd;
+        if (j < nlay) Fd = solver_exp_beam(-t * mu0_inv, etab) * Fd;
         WA.st(Fd, j < nlay ? vVs : kBufOOB, row * lev_below(l));
       }
     }
@@ -754,6 +751,78 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
     sw_launch<false, false>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
                             mu0, alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
   RRTMGPNN_LAUNCH_CHECK("sw_2stream_kernel");
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// rte_sw on 1scl (absorption-only) properties, rte/mo_rte_sw.F90:213-222: apply_BC_factor
+// (flux_dir(:, top) = inc_flux * mu0, mo_rte_solver_kernels.F90:1685-1704) and sw_solver_noscat (:496-532): the
+// direct beam walked down, flux_dir(l+1) = flux_dir(l) * exp(-tau(l) / mu0), and its broadband sum per level
+// (sum_broadband_nocol: one sequential sum over g).  One block per column, lane = g-point; levels are staged in an
+// LDS ring and each flush sums one level per thread in g order.  The broadband sum is each column's own (the
+// reference sums column 1's spectral fluxes for every column, quirk B-11).
+// ------------------------------------------------------------------------------------------
+constexpr int kNsRing = 8;
+
+__global__ void __launch_bounds__(1024) sw_noscat_kernel(int ngpt, int nlay, int top_at_1,
+                                                         const float *__restrict__ inc_flux,
+                                                         const float *__restrict__ tau, const float *__restrict__ mu0p,
+                                                         float *__restrict__ flux_dir)
+{
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
+  float *ring = smem + kExpTabFloats;  // [kNsRing][ngpt]
+  load_exp_table(etab);
+  __syncthreads();
+  const int icol = blockIdx.x, g = threadIdx.x, nlev = nlay + 1;
+  const bool on = g < ngpt;
+  const int gc = on ? g : ngpt - 1;
+  const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
+  const float *t = tau + (size_t)ngpt * nlay * icol;
+  float *out = flux_dir + (size_t)nlev * icol;
+  const int top = top_at_1 ? 0 : nlay, dl = top_at_1 ? 1 : -1;
+  auto flush = [&](int n, int lev0) {
+    __syncthreads();
+    if ((int)threadIdx.x < n) {
+      const float *r = ring + (size_t)threadIdx.x * ngpt;
+      float s = 0.0f;
+      for (int i = 0; i < ngpt; i++) s = s + r[i];
+      out[lev0 + (int)threadIdx.x * dl] = s;
+    }
+    __syncthreads();
+  };
+  float F = inc_flux[gc + (size_t)ngpt * icol] * mu0;
+  if (on) ring[g] = F;
+  flush(1, top);
+  for (int j0 = 0; j0 < nlay; j0 += kNsRing) {
+    const int n = min(kNsRing, nlay - j0);
+    float tv[kNsRing];
+#pragma unroll
+    for (int r = 0; r < kNsRing; r++) {
+      const int j = min(j0 + r, nlay - 1);
+      tv[r] = t[gc + (size_t)ngpt * (top_at_1 ? j : nlay - 1 - j)];
+    }
+#pragma unroll
+    for (int r = 0; r < kNsRing; r++) {
+      if (r < n) {
+        F = F * solver_exp_beam(-tv[r] * mu0_inv, etab);
+        if (on) ring[(size_t)r * ngpt + g] = F;
+      }
+    }
+    flush(n, top + dl * (j0 + 1));
+  }
+}
+
+int launch_sw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                     const float *tau, const float *mu0, float *flux_dir)
+{
+  if (ncol == 0) return RRTMGPNN_OK;
+  if (ngpt > 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw_solver_noscat: more than 1024 g-points");
+  const int threads = (ngpt + 63) / 64 * 64;
+  const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kNsRing * ngpt);
+  hipLaunchKernelGGL(sw_noscat_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, top_at_1, inc_flux,
+                     tau, mu0, flux_dir);
+  RRTMGPNN_LAUNCH_CHECK("sw_noscat_kernel");
   return RRTMGPNN_OK;
 }
 

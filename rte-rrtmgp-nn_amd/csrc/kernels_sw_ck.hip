@@ -97,14 +97,20 @@ __device__ __forceinline__ void ck_inc(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, f2 
 
 // K: layers per chunk (checkpoint spacing); RING: levels staged for the ordered broadband sums (a multiple of K)
 #ifndef RRTMGPNN_SWCK_K
-#define RRTMGPNN_SWCK_K 4
+#define RRTMGPNN_SWCK_K 3
 #endif
 #ifndef RRTMGPNN_SWCK_RING
-#define RRTMGPNN_SWCK_RING 4
+#define RRTMGPNN_SWCK_RING 6
 #endif
 #ifndef RRTMGPNN_SWCK_WAVES
 #define RRTMGPNN_SWCK_WAVES 4
 #endif
+// KEEPD = 1: the walk up keeps each layer's adding denominator for the walk down (K more register pairs); 0: the walk
+// down forms it again (one more reciprocal per element, fewer registers)
+#ifndef RRTMGPNN_SWCK_KEEPD
+#define RRTMGPNN_SWCK_KEEPD 1
+#endif
+constexpr bool kCkKeepD = RRTMGPNN_SWCK_KEEPD != 0;
 constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
 static_assert(kCkRing % kCkK == 0, "the flux ring must hold whole chunks");
 
@@ -204,7 +210,7 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SWCK_WAVES)
       const int n = min(K, nlay - ck * K);
       f2 Tn[K];
 #pragma unroll
-      for (int p = 0; p < K; p++) Tn[p] = exp2v(-(kInc ? cur.t[p] + cur.qt[p] : cur.t[p]) * mu0_inv, etab);
+      for (int p = 0; p < K; p++) Tn[p] = exp2v_beam(-(kInc ? cur.t[p] + cur.qt[p] : cur.t[p]) * mu0_inv, etab);
 #pragma unroll
       for (int p = 0; p < K; p++)
         if (p < n) Fd = Tn[p] * Fd;
@@ -228,7 +234,7 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SWCK_WAVES)
 #pragma unroll
       for (int p = 0; p < K; p++) {
         props(cur, p, t[p], w[p], g0[p]);
-        Tn[p] = exp2v(-t[p] * mu0_inv, etab);  // pass 1's transmittance, same bits
+        Tn[p] = exp2v_beam(-t[p] * mu0_inv, etab);  // pass 1's transmittance, same bits
         Fin[p] = Fb;                           // the beam at the layer's top
         Fb = Tn[p] * Fb;
       }
@@ -280,7 +286,7 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SWCK_WAVES)
       for (int p = 0; p < K; p++) {
         f2 t, w, g0;
         props(cur, p, t, w, g0);
-        const f2 Tn = exp2v(-t * mu0_inv, etab);
+        const f2 Tn = exp2v_beam(-t * mu0_inv, etab);
         const Coef2 cf = ck_two_stream<kG0>(t, w, g0, mu0, Tn, Fd3, etab);
         Rd[p] = cf.Rdif;
         Td[p] = cf.Tdif;
@@ -298,10 +304,10 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SWCK_WAVES)
         for (int p = K - 1; p >= 0; p--) {
           A[p] = a;
           S[p] = s;
-          D[p] = splat(0.0f);
+          if (kCkKeepD) D[p] = splat(0.0f);
           if (p < n) {
             const f2 denom = rcp2(1.0f - Rd[p] * a);
-            D[p] = denom;
+            if (kCkKeepD) D[p] = denom;
             if (p > 0) {
               const f2 an = Rd[p] + Td[p] * Td[p] * a * denom;
               const f2 sn = Su[p] + Td[p] * denom * (s + a * Sd[p]);
@@ -316,7 +322,8 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SWCK_WAVES)
 #pragma unroll
       for (int p = 0; p < K; p++) {
         if (p < n) {
-          Fdn = (Td[p] * Fdn + Rd[p] * S[p] + Sd[p]) * D[p];
+          const f2 denom = kCkKeepD ? D[p] : rcp2(1.0f - Rd[p] * A[p]);
+          Fdn = (Td[p] * Fdn + Rd[p] * S[p] + Sd[p]) * denom;
           const f2 up = Fdn * A[p] + S[p];
           put(up, Fdn, Fdir[p], rbase + p);
         }

@@ -45,7 +45,7 @@ __device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0
   SwCoef2 c;
   const SwDif2 d = sw_dif2(tau, w0, g, etab);
   const f2 gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
-  const f2 Tnoscat = kTn ? Tn_in : exp2v(-tau * mu0_inv, etab);  // kTn: pass 1's value of the same expression
+  const f2 Tnoscat = kTn ? Tn_in : exp2v_beam(-tau * mu0_inv, etab);  // kTn: pass 1's value of the same expression
   const f2 gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? splat(0.5f) : (2.0f - 3.0f * mu0 * g) * .25f;  // g == 0: exactly 0.5
   const f2 gamma4 = 1.0f - gamma3;
   const f2 alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
@@ -237,12 +237,12 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
           pi[p] = ld_bnd(Bt, ln);
         }
         if constexpr (kBl) {
-          const f2 Tn = exp2v(-t * mu0_inv, etab);
+          const f2 Tn = exp2v_beam(-t * mu0_inv, etab);
           if constexpr (kSw2StoreTns) WTn.st(Tn, j < nlay ? vLs : kBufOOB, row * l);
           const f2 Fn = Tn * Fd;
           Fd = j < nlay ? Fn : Fd;  // uniform select
         } else if (j < nlay) {
-          const f2 Tn = exp2v(-t * mu0_inv, etab);
+          const f2 Tn = exp2v_beam(-t * mu0_inv, etab);
           if constexpr (kSw2StoreTns) WTn.st(Tn, vLs, row * l);
           Fd = Tn * Fd;
         }

@@ -36,9 +36,38 @@ __device__ __forceinline__ float solver_div(float a, float b)
   return a / b;
 #endif
 }
+// RRTMGPNN_FAST_LIBM (opt-in tolerance build, librrtmgpnn_fastlibm.so; never the default): the solvers' exps of
+// non-positive arguments use the hardware exponential (v_exp_f32, a few ulp) instead of glibc's algorithm
+// evaluated in double.  Fluxes then differ from the reference's in the last bits; tests/test_gpu_tolerance.py holds
+// them to the north star's 1e-3 W/m2 RMS.
+#ifndef RRTMGPNN_FAST_LIBM
+#define RRTMGPNN_FAST_LIBM 0
+#endif
+// The direct-beam transmittance exp(-tau/mu0) multiplies down every layer of a column, so its rounding errors compound:
+// it keeps glibc's algorithm in the tolerance build too (with the hardware exp there, C3 SW down-flux errors reached
+// 1.0e-3 W/m2 RMS, the north star's bar itself).
+__device__ __forceinline__ float solver_exp_beam(float x, const uint64_t *tab)
+{
+#if RRTMGPNN_FASTOPS || RRTMGPNN_FAST_LIBM
+  return ref_expf_neg(x, tab);
+#else
+  return ref_expf_nb(x, tab);
+#endif
+}
 __device__ __forceinline__ float solver_exp_neg(float x, const uint64_t *tab)
 {
-#if RRTMGPNN_FASTOPS
+#if RRTMGPNN_FAST_LIBM
+  // 2^(x log2 e) on the hardware exp2 (v_exp_f32, ~1 ulp), with the product x*log2(e) carried in two parts (hi by
+  // the rounded product, lo by fma residual + x*(log2(e) - hi constant)) so its rounding does not scale with |x|;
+  // the lo part enters as the first-order factor (1 + lo*ln2).
+  (void)tab;
+  const float L = 1.44269502162933349609375f, L_lo = 1.925963033500011079E-8f, LN2 = 0.693147180559945f;
+  const float t = x * L;
+  float e = fmaf(x, L, -t);
+  e = fmaf(x, L_lo, e);
+  const float r = __builtin_amdgcn_exp2f(t);
+  return (x < -0x1.9fe368p6f) ? 0.0f : fmaf(r, e * LN2, r);
+#elif RRTMGPNN_FASTOPS
   return ref_expf_neg(x, tab);
 #else
   return ref_expf_nb(x, tab);

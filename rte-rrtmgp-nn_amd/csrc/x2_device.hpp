@@ -20,6 +20,11 @@ __device__ __forceinline__ f2 exp2v(f2 x, const uint64_t *etab)
 {
   return (f2){solver_exp_neg(x.x, etab), solver_exp_neg(x.y, etab)};
 }
+// the direct-beam transmittance exp(-tau/mu0) (solver_exp_beam)
+__device__ __forceinline__ f2 exp2v_beam(f2 x, const uint64_t *etab)
+{
+  return (f2){solver_exp_beam(x.x, etab), solver_exp_beam(x.y, etab)};
+}
 
 // sqrt_rn_normal (libm_ref.hpp) with the correction fmas paired
 __device__ __forceinline__ f2 sqrt2(f2 x)

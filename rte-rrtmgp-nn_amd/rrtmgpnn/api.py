@@ -767,11 +767,12 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
 
 
 def rte_sw(atmos, top_at_1, mu0, inc_flux, sfc_alb_dir_gpt, sfc_alb_dif_gpt, fluxes, inc_flux_dif=None):
-    """rte/mo_rte_sw.F90:48-266 (fork: albedos per g-point (ncol, ngpt))."""
+    """rte/mo_rte_sw.F90:48-266 (fork: albedos per g-point (ncol, ngpt)).  1scl: the direct beam (sw_solver_noscat);
+    2str: sw_solver_2stream."""
     if not fluxes.are_desired():
         return "rte_sw: no space allocated for fluxes"
-    if not isinstance(atmos, OpticalProps2str):
-        return "rte_sw: the no-scattering (1scl) shortwave solver is not implemented (2str only)"
+    if not isinstance(atmos, (OpticalProps1scl, OpticalProps2str)):
+        return "sw_solver(...ty_optical_props_nstr...) not yet implemented"
     ncol, nlay, ngpt = atmos.tau.shape
     if tuple(mu0.shape) != (ncol,):
         return "rte_sw: mu0 inconsistently sized"
@@ -785,6 +786,14 @@ def rte_sw(atmos, top_at_1, mu0, inc_flux, sfc_alb_dir_gpt, sfc_alb_dif_gpt, flu
         return "rte_sw: inc_flux_dif inconsistently sized"
     ctx = context(atmos.tau.device.index)
     dev = atmos.tau.device
+    if isinstance(atmos, OpticalProps1scl):
+        # direct beam only (:213-222): apply_BC_factor + sw_solver_noscat; as in the reference only the direct flux
+        # is written (flux_up / flux_dn / flux_net are left as they are)
+        if fluxes.flux_dn_dir is None:
+            return "rte_sw: the no-scattering solution needs flux_dn_dir"
+        check(_lib.lib().rrtmgpnn_sw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
+                                                   _p(atmos.tau), _p(mu0), _p(fluxes.flux_dn_dir)), "sw_solver_noscat")
+        return ""
     up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=dev)
     dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=dev)
     dr = fluxes.flux_dn_dir if fluxes.flux_dn_dir is not None else torch.empty((ncol, nlay + 1), device=dev)

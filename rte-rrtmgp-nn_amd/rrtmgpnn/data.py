@@ -62,12 +62,13 @@ def load_cloud_optics(which):
 
 def allsky_clouds(problem, co):
     """The all-sky example's cloud recipe (examples/all-sky/rrtmgp_allsky.F90:323-349): clouds where
-    100 hPa < p < 900 hPa in columns with mod(icol, 3) /= 0 (1-based icol); liquid water path 10 g/m2
-    where T > 263 K, ice 10 g/m2 where T < 273 K; effective radii at the middle of the tables' ranges.
+    100 hPa < p < 900 hPa in columns with mod(icol, 3) /= 0 (1-based icol of the whole problem: a shard starting at
+    global column problem["col0"] keeps its columns' clouds); liquid water path 10 g/m2 where T > 263 K, ice
+    10 g/m2 where T < 273 K; effective radii at the middle of the tables' ranges.
     Returns clwp, ciwp, rel, rei as (ncol, nlay) float32."""
     play, tlay = np.asarray(problem["play"], np.float32), np.asarray(problem["tlay"], np.float32)
     ncol = play.shape[0]
-    col = (np.arange(ncol) + 1) % 3 != 0
+    col = (int(problem.get("col0", 0)) + np.arange(ncol) + 1) % 3 != 0
     mask = (play > np.float32(100 * 100)) & (play < np.float32(900 * 100)) & col[:, None]
     rel_val = np.float32(0.5) * (np.float32(co["radliq_lwr"][0]) + np.float32(co["radliq_upr"][0]))
     rei_val = np.float32(0.5) * (np.float32(co["radice_lwr"][0]) + np.float32(co["radice_upr"][0]))
@@ -146,63 +147,93 @@ def rfmip_problem(lw_press_clamp=True, fields=None):
     }
 
 
-def synthetic_problem(ncol, nlay=60, seed=20251015, t_sigma=2.0, h2o_sigma=0.2):
-    """Synthetic clear-sky columns built from RFMIP profiles (BASELINE configs C4/C5).
+SYN_BLOCK = 1024  # columns per random stream of synthetic_problem
 
-    Each column takes an RFMIP (site, expt) drawn by PCG64(seed); for nlay != 60 the profile is
-    interpolated linearly in ln(p) onto nlay layers between the surface and press_ref_min.
-    T += N(0, t_sigma K) clipped to the NN training range [160, 320.5] K; h2o *= lognormal(0, h2o_sigma)
-    clipped to the NN range [xmin^4, xmax^4].
-    """
-    base = rfmip_problem()
-    rng = np.random.Generator(np.random.PCG64(seed))
-    pick = rng.integers(0, base["ncol"], size=ncol)
-    kd = load_kdist("lw")
-    pmin = np.float32(kd["press_ref_min"][0])
+
+def _interp_base(base, nlay, pmin):
+    """RFMIP profiles (every base column) interpolated linearly in ln(p) onto nlay layers between the column's surface
+    pressure and press_ref_min (top at index 0).  Depends on the base column only, so it is computed once per base
+    column and indexed by each synthetic column's draw."""
     nl0 = base["nlay"]
     if nlay == nl0:
-        play = base["play"][pick].copy()
-        plev = base["plev"][pick].copy()
-        tlay = base["tlay"][pick].copy()
-        tlev = base["tlev"][pick].copy()
-        gases = {k: v[pick].copy() for k, v in base["gases"].items()}
-    else:
-        # new level grid: log-spaced from surface pressure to press_ref_min (top at index 0)
-        psfc = base["plev"][pick, nl0].astype(np.float64)
-        frac = np.linspace(0.0, 1.0, nlay + 1)[None, :]
-        lev = np.exp(np.log(psfc)[:, None] * frac + np.log(np.float64(pmin) * 1.0001) * (1.0 - frac))
-        lay = np.sqrt(lev[:, :-1] * lev[:, 1:])
-        src_lay = np.log(base["play"][pick].astype(np.float64))
-        src_lev = np.log(base["plev"][pick].astype(np.float64))
-        src_lev[:, 0] = np.log(np.float64(pmin))
+        return {k: base[k] for k in ("play", "plev", "tlay", "tlev")}, dict(base["gases"])
+    psfc = base["plev"][:, nl0].astype(np.float64)
+    frac = np.linspace(0.0, 1.0, nlay + 1)[None, :]
+    lev = np.exp(np.log(psfc)[:, None] * frac + np.log(np.float64(pmin) * 1.0001) * (1.0 - frac))
+    lay = np.sqrt(lev[:, :-1] * lev[:, 1:])
+    src_lay = np.log(base["play"].astype(np.float64))
+    src_lev = np.log(base["plev"].astype(np.float64))
+    src_lev[:, 0] = np.log(np.float64(pmin))
+    lnl, lnv = np.log(lay), np.log(lev)
 
-        def interp(src_lnp, vals, dst_lnp):
-            out = np.empty(dst_lnp.shape)
-            for i in range(dst_lnp.shape[0]):
-                out[i] = np.interp(dst_lnp[i], src_lnp[i], vals[i])
-            return out
+    def interp(src_lnp, vals, dst_lnp):
+        out = np.empty(dst_lnp.shape)
+        for i in range(dst_lnp.shape[0]):
+            out[i] = np.interp(dst_lnp[i], src_lnp[i], vals[i])
+        return out
 
-        lnl, lnv = np.log(lay), np.log(lev)
-        tlay = interp(src_lay, base["tlay"][pick], lnl)
-        tlev = interp(src_lev, base["tlev"][pick], lnv)
-        gases = {k: interp(src_lay, v[pick], lnl) for k, v in base["gases"].items()}
-        play, plev = lay, lev
-        plev[:, 0] = pmin + F32_EPS
-    tlay = np.clip(tlay + rng.normal(0.0, t_sigma, size=tlay.shape), 160.0, 320.5)
-    tlev = np.clip(tlev + rng.normal(0.0, t_sigma, size=tlev.shape), 160.0, 320.5)
+    prof = {"play": lay, "plev": lev, "tlay": interp(src_lay, base["tlay"], lnl),
+            "tlev": interp(src_lev, base["tlev"], lnv)}
+    prof["plev"][:, 0] = pmin + F32_EPS
+    gases = {k: interp(src_lay, v, lnl) for k, v in base["gases"].items()}
+    return prof, gases
+
+
+def synthetic_problem(ncol, nlay=60, seed=20251015, t_sigma=2.0, h2o_sigma=0.2, col0=0):
+    """Columns [col0, col0 + ncol) of the synthetic clear-sky problem of BASELINE configs C4/C5.
+
+    Column i takes an RFMIP (site, expt) and its perturbations from the random stream of its block of SYN_BLOCK
+    columns (PCG64 seeded by (seed, i // SYN_BLOCK)), so any column range of one global problem -- the rank's shard of
+    the 1e6-column C5 problem, or a strided test sample -- is generated alone and is identical to the same columns of
+    the whole.  For nlay != 60 the profile is interpolated linearly in ln(p) onto nlay layers between the surface and
+    press_ref_min.  T += N(0, t_sigma K) clipped to the NN training range [160, 320.5] K; h2o *= lognormal(0,
+    h2o_sigma) clipped to the NN range [xmin^4, xmax^4]; tsfc += N(0, t_sigma K).
+    """
+    base = rfmip_problem()
+    kd = load_kdist("lw")
+    pmin = np.float32(kd["press_ref_min"][0])
+    prof, bgas = _interp_base(base, nlay, pmin)
+    b0, b1 = col0 // SYN_BLOCK, (col0 + ncol + SYN_BLOCK - 1) // SYN_BLOCK
+    pick, tn_lay, tn_lev, hf, tn_sfc = [], [], [], [], []
+    for b in range(b0, b1):
+        rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence([seed, b])))
+        pick.append(rng.integers(0, base["ncol"], size=SYN_BLOCK))
+        tn_lay.append(rng.normal(0.0, t_sigma, size=(SYN_BLOCK, nlay)))
+        tn_lev.append(rng.normal(0.0, t_sigma, size=(SYN_BLOCK, nlay + 1)))
+        hf.append(rng.lognormal(0.0, h2o_sigma, size=(SYN_BLOCK, nlay)))
+        tn_sfc.append(rng.normal(0.0, t_sigma, size=SYN_BLOCK))
+    sl = slice(col0 - b0 * SYN_BLOCK, col0 - b0 * SYN_BLOCK + ncol)
+    pick = np.concatenate(pick)[sl]
+    cat = lambda xs: np.concatenate(xs)[sl]  # noqa: E731
+    tlay = np.clip(prof["tlay"][pick] + cat(tn_lay), 160.0, 320.5)
+    tlev = np.clip(prof["tlev"][pick] + cat(tn_lev), 160.0, 320.5)
+    gases = {k: v[pick] for k, v in bgas.items()}
     h2o_lo, h2o_hi = 0.0101 ** 4, 0.5077 ** 4
-    gases["h2o"] = np.clip(gases["h2o"] * rng.lognormal(0.0, h2o_sigma, size=gases["h2o"].shape), h2o_lo, h2o_hi)
-    out = {
-        "ncol": ncol, "nlay": nlay, "top_at_1": True,
-        "play": np.ascontiguousarray(play, np.float32), "plev": np.ascontiguousarray(plev, np.float32),
+    gases["h2o"] = np.clip(gases["h2o"] * cat(hf), h2o_lo, h2o_hi)
+    return {
+        "ncol": ncol, "nlay": nlay, "top_at_1": True, "col0": col0,
+        "play": np.ascontiguousarray(prof["play"][pick], np.float32),
+        "plev": np.ascontiguousarray(prof["plev"][pick], np.float32),
         "tlay": np.ascontiguousarray(tlay, np.float32), "tlev": np.ascontiguousarray(tlev, np.float32),
-        "tsfc": np.clip(base["tsfc"][pick] + rng.normal(0.0, t_sigma, size=ncol), 160.0, 340.0).astype(np.float32),
+        "tsfc": np.clip(base["tsfc"][pick] + cat(tn_sfc), 160.0, 340.0).astype(np.float32),
         "gases": {k: np.ascontiguousarray(v, np.float32) for k, v in gases.items()},
         "sfc_emis": base["sfc_emis"][pick].copy(), "sfc_alb": base["sfc_alb"][pick].copy(),
         "sza": base["sza"][pick].copy(), "mu0": base["mu0"][pick].copy(), "usecol": base["usecol"][pick].copy(),
         "tsi": base["tsi"][pick].copy(),
     }
-    return out
+
+
+def rfmip_columns(col0, ncol):
+    """Columns [col0, col0 + ncol) of the RFMIP set tiled without end (global column i is RFMIP column i % 1800):
+    one rank's block when N ranks process N x 1800 columns (bench.py, weak scaling)."""
+    base = rfmip_problem()
+    idx = (col0 + np.arange(ncol)) % base["ncol"]
+    sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == base["ncol"] else v)
+           for k, v in base.items()}
+    sub["gases"] = {k: v[idx] for k, v in base["gases"].items()}
+    sub["ncol"] = ncol
+    sub["col0"] = col0
+    return sub
 
 
 def toa_flux(problem, kd_sw, tsi_default=1361.0):

@@ -77,13 +77,11 @@ class ClearSkyStep:
         self.nb_lw = self.kd_lw["nband"]
 
         # ---- inputs (HBM resident) ----
-        self.play, self.plev = _t(prob["play"], dev), _t(prob["plev"], dev)
-        self.tlay, self.tlev, self.tsfc = _t(prob["tlay"], dev), _t(prob["tlev"], dev), _t(prob["tsfc"], dev)
-        self.gases = {k: _t(v, dev) for k, v in prob["gases"].items()}
-        self.sfc_emis = _t(np.repeat(prob["sfc_emis"][:, None], self.nb_lw, axis=1), dev)  # (ncol, nband)
-        self.mu0 = _t(prob["mu0"], dev)
-        self.toa = _t(data.toa_flux(prob, self.kd_sw), dev)
-        self.alb = _t(np.repeat(prob["sfc_alb"][:, None], self.ng_sw, axis=1), dev)
+        self._gas_names = list(prob["gases"])
+        ins = self._inputs(prob, clouds)
+        self.play, self.plev, self.tlay, self.tlev, self.tsfc = ins[:5]
+        self.gases = dict(zip(self._gas_names, ins[5:5 + len(self._gas_names)]))
+        self.sfc_emis, self.mu0, self.toa, self.alb = ins[5 + len(self._gas_names):9 + len(self._gas_names)]
         self.totplnk = _t(self.kd_lw["totplnk"], dev)
         self.sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
 
@@ -103,7 +101,7 @@ class ClearSkyStep:
             self.g_sw = f(ncol, nlay, self.ng_sw)
         if self.allsky:
             self.nb_sw = self.kd_sw["nband"]
-            self.lwp, self.iwp, self.rel, self.rei = (_t(a, dev) for a in clouds)
+            self.lwp, self.iwp, self.rel, self.rei = ins[-4:]
             self.cld_tau_lw = f(ncol, nlay, self.nb_lw)
             self.cld_tau_sw, self.cld_ssa_sw, self.cld_g_sw = (f(ncol, nlay, self.nb_sw) for _ in range(3))
             self.cloud_lw, self.cloud_sw = (self._cloud_optics(w, cloud_lut, icergh) for w in ("lw", "sw"))
@@ -331,6 +329,26 @@ class ClearSkyStep:
 
     def replay(self):
         self.graph.replay()
+
+    def _inputs(self, prob, clouds=None):
+        """Device input tensors of a host problem, in io_tensors() order: the state, the gases, the surface emissivity
+        by band, mu0, the renormalised incident flux per g-point and the albedo per g-point (+ the cloud fields)."""
+        dev = self.dev
+        ins = [_t(prob[k], dev) for k in ("play", "plev", "tlay", "tlev", "tsfc")]
+        ins += [_t(prob["gases"][k], dev) for k in self._gas_names]
+        ins += [_t(np.repeat(prob["sfc_emis"][:, None], self.nb_lw, axis=1), dev),  # (ncol, nband)
+                _t(prob["mu0"], dev), _t(data.toa_flux(prob, self.kd_sw), dev),
+                _t(np.repeat(prob["sfc_alb"][:, None], self.ng_sw, axis=1), dev)]
+        if clouds is not None:
+            ins += [_t(a, dev) for a in clouds]
+        return ins
+
+    def inputs_for(self, prob, clouds=None):
+        """io_tensors()-ordered device inputs of another block of the same shape (bench.py's chunked shard: copied
+        into this step's inputs before each replay)."""
+        if prob["ncol"] != self.ncol or prob["nlay"] != self.nlay or list(prob["gases"]) != self._gas_names:
+            raise ValueError("inputs_for: block shape differs from the step's")
+        return self._inputs(prob, clouds if self.allsky else None)
 
     def io_tensors(self):
         """(inputs, outputs): the device tensors a host-resident caller would upload / download per step."""

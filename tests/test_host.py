@@ -131,3 +131,24 @@ def test_column_sharding_gloo_world2():
         p.join(timeout=60)
     assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 1001
     assert res[0][3] and res[1][3]
+
+
+def test_synthetic_problem_column_ranges_are_slices_of_the_whole():
+    """bench.py builds each rank's shard (and each chunk of it) as a column range of one global synthetic problem:
+    a range generated alone must equal the same columns of the whole, at 60 and 137 layers."""
+    from rrtmgpnn import data
+    for nlay in (60, 137):
+        whole = data.synthetic_problem(2500, nlay, seed=7)
+        part = data.synthetic_problem(900, nlay, seed=7, col0=1100)
+        for k in ("play", "plev", "tlay", "tlev", "tsfc", "mu0", "sfc_alb", "tsi"):
+            np.testing.assert_array_equal(part[k], whole[k][1100:2000], err_msg=k)
+        for g in whole["gases"]:
+            np.testing.assert_array_equal(part["gases"][g], whole["gases"][g][1100:2000], err_msg=g)
+    co = data.load_cloud_optics("lw")
+    whole = data.synthetic_problem(300, 60, seed=7)
+    part = data.synthetic_problem(100, 60, seed=7, col0=101)
+    for a, b in zip(data.allsky_clouds(part, co), data.allsky_clouds(whole, co)):
+        np.testing.assert_array_equal(a, b[101:201])
+    r = data.rfmip_columns(3500, 200)
+    full = data.rfmip_problem()
+    np.testing.assert_array_equal(r["tlay"], full["tlay"][(3500 + np.arange(200)) % 1800])

@@ -125,3 +125,25 @@ def test_oracle_bitwise_vs_reference_full_rfmip(orc, rfmip, models):
     np.testing.assert_array_equal(ups, u2)
     np.testing.assert_array_equal(dns, d2)
     np.testing.assert_array_equal(drs, r2)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="reference oracle not built (needs /root/reference)")
+@pytest.mark.parametrize("top_at_1", [True, False])
+def test_sw_noscat_bitwise_vs_reference_kernels(orc, rfmip, models, top_at_1):
+    """rte_sw's 1scl branch (rte/mo_rte_sw.F90:213-222): the restatement == the reference's apply_BC_factor +
+    sw_solver_noscat kernels, bit for bit, on the NN absorption optical depths of RFMIP columns."""
+    import oracle as O
+    from rrtmgpnn import data
+    ref = O.Reference()
+    prob = subset(rfmip, np.arange(0, 1800, 7))
+    go = orc.sw_gas_optics(prob, [models["sw_abs"], models["sw_ray"]])
+    tau = go["tau"] if top_at_1 else np.ascontiguousarray(go["tau"][:, ::-1])
+    toa = data.toa_flux(prob, data.load_kdist("sw"))
+    got, got_g = orc.sw_solver_noscat(tau, prob["mu0"], toa, top_at_1, gpt=True)
+    want, want_g = ref.sw_noscat(tau, prob["mu0"], toa, top_at_1)
+    np.testing.assert_array_equal(got_g, want_g)               # the spectral beam, every column
+    np.testing.assert_array_equal(got[0], want[0])             # broadband: the reference's own sum for column 1
+    np.testing.assert_array_equal(got, data.seqsum(want_g, axis=-1))  # every column: sum(flux_dir, 1) of its own
+    assert np.all(want == want[:1])  # quirk B-11: the reference sums column 1 for every column
+    top = 0 if top_at_1 else -1
+    assert np.all(got[:, top] > 0) and np.all(np.diff(got, axis=1) * (1 if top_at_1 else -1) <= 0)
