@@ -52,9 +52,9 @@ int rrtmgpnn_context_create(int device, void *hip_stream, rrtmgpnn_context **ctx
 int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream);
 /* MI355X tuning, no reference counterpart: which SW two-stream kernel rrtmgpnn_sw_solver_2stream* launch.
- * 0 (default): two g-points per lane (packed fp32, two columns per block) when ngpt is even,
- * one per lane otherwise; 1 / 2 force one / two g-points per lane (2 needs even ngpt); 3: two g-points per lane
- * with checkpointed passes (beam / adding state stored every few levels instead of per level, even ngpt).
+ * 0 (default): mode 3 when ngpt is even, one g-point per lane otherwise.  1: one g-point per lane.  2: two g-points
+ * per lane (packed fp32, two columns per block) with per-level workspace planes.  3: two g-points per lane with
+ * checkpointed passes (beam / adding state stored every 3 levels instead of per level).  2 and 3 need even ngpt.
  * All kernels give bit-identical fluxes.  ctx == NULL sets the default of every context not set itself. */
 int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode);
 void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx);

@@ -716,10 +716,11 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
   const bool inc = bands != nullptr;
-  // two g-points per lane (kernels_sw_x2.hip, 4 columns per 7-wave block) whenever ngpt is even: alone 7 % faster at
-  // C3 and the whole step 1.8 % (C3) / 2 % (C4) faster than one g-point per lane (tools/cmp_sw_kernel.sh)
+  // Even ngpt: two g-points per lane.  By default the checkpointed kernel (kernels_sw_ck.hip: 0.67 instead of 1.07 GB
+  // per launch at C3, whole step C3 -3 %, C4 -1 % against kernels_sw_x2.hip, tools/gpu_ab.sh); mode 2 forces the
+  // workspace-plane kernel, mode 1 one g-point per lane (also the odd-ngpt kernel).
   const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
-  const bool ck = (ngpt % 2) == 0 && mode == 3;
+  const bool ck = (ngpt % 2) == 0 && (mode == 3 || mode == 0);
   const bool x2 = !ck && kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc && kSwIncPark ? 3 : 0);

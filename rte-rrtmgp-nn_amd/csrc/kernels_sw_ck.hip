@@ -102,8 +102,11 @@ __device__ __forceinline__ void ck_inc(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, f2 
 #ifndef RRTMGPNN_SWCK_RING
 #define RRTMGPNN_SWCK_RING 6
 #endif
+// K = 3 layers per chunk under a 3-waves-per-SIMD register budget (132 VGPRs, no spill; at 4 waves K = 3 spilled and
+// K = 2 fit): C3 step -3 %, C4 -1 % against K = 2 or the two-per-lane workspace kernel; K = 4 (148 VGPRs) was best
+// alone at C3 but 13 % slower at C4, K = 6 spilled (tools/gpu_ab.sh, round 2)
 #ifndef RRTMGPNN_SWCK_WAVES
-#define RRTMGPNN_SWCK_WAVES 4
+#define RRTMGPNN_SWCK_WAVES 3
 #endif
 // KEEPD = 1: the walk up keeps each layer's adding denominator for the walk down (K more register pairs); 0: the walk
 // down forms it again (one more reciprocal per element, fewer registers)
