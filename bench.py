@@ -39,8 +39,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c4", "c5"],
-                    help="c3: RFMIP 1800x60 LW+SW (default, the metric's config); c2: the same columns, LW only "
+    ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"],
+                    help="c3: RFMIP 1800x60 LW+SW (default, the metric's config); c1: the first 100 RFMIP columns, LW "
+                         "only (BASELINE configs[0], the reference's CPU case); c2: the 1800 columns, LW only "
                          "(BASELINE configs[1], metric in LW columns/s); c4: 10000x60 synthetic all-sky; "
                          "c5: 125000x137 synthetic clear-sky per GPU")
     ap.add_argument("--global", dest="global_cols", nargs="?", type=int, const=-1, default=0,
@@ -134,7 +135,7 @@ def main():
 
     # ---- the global problem and this rank's part of it (shard.column_range) ----
     metric = METRIC
-    block = {"c2": 1800, "c3": 1800, "c4": 10000, "c5": 125000}[args.config]
+    block = {"c1": 100, "c2": 1800, "c3": 1800, "c4": 10000, "c5": 125000}[args.config]
     nlay_cfg = 137 if args.config == "c5" else 60
     if args.global_cols:
         global_cols = 1000000 if (args.global_cols < 0 and args.config == "c5") else (
@@ -148,12 +149,16 @@ def main():
 
     def problem(c0, c1):
         """Columns [c0, c1) of the global problem (and their clouds at C4)."""
-        if args.config in ("c2", "c3"):
+        if args.config in ("c1", "c2", "c3"):
             return data.rfmip_columns(c0, c1 - c0), None
         p = data.synthetic_problem(c1 - c0, nlay_cfg, seed=20251015, col0=c0)
         return p, (data.allsky_clouds(p, data.load_cloud_optics("lw")) if args.config == "c4" else None)
 
-    if args.config == "c2":
+    if args.config == "c1":
+        workload = "C1: RFMIP clear-sky LW only, 100 columns x 60 layers x 256 g-points, NN gas optics (g256)"
+        data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
+        metric = "atmospheric columns/sec (LW clear-sky fluxes), 1 MI355X"
+    elif args.config == "c2":
         workload = "C2: RFMIP clear-sky LW only, 1800 columns x 60 layers x 256 g-points, NN gas optics (g256)"
         data_desc = "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables"
         metric = "atmospheric columns/sec (LW clear-sky fluxes), 1 MI355X"
@@ -176,7 +181,7 @@ def main():
         api.set_sw_kernel_default(args.sw_kernel)
     prob, clouds = problem(*chunks[0])
     step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap,
-                        sw=args.config != "c2")
+                        sw=args.config not in ("c1", "c2"))
     ncol, nlay = step.ncol, step.nlay
     ins, outs = step.io_tensors()
     # more than one chunk: every chunk's inputs resident in HBM, copied into the step's buffers before its replay and
@@ -376,9 +381,7 @@ def main():
     # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if clouds is not None:
-            prob = dict(prob, **dict(zip(("lwp", "iwp", "rel", "rei"), clouds)))
-        cpu = cpu_baseline(prob, args.cpu_seconds, args.cpu_kind, sw=step.sw)
+        cpu = cpu_baseline(prob, clouds, args.cpu_seconds, args.cpu_kind, sw=step.sw)
 
     if rank == 0:
         out = {
@@ -409,119 +412,107 @@ def main():
         dist.destroy_process_group()
 
 
-def _subset(prob, n):
-    idx = np.arange(n) % prob["ncol"]
+def _subset(prob, idx):
     sub = {k: (v[idx] if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == prob["ncol"] else v)
            for k, v in prob.items()}
-    sub["gases"] = {k: v[idx] for k, v in prob["gases"].items()}
-    sub["ncol"] = n
+    sub["gases"] = {k: (v[idx] if np.ndim(v) == 2 else v) for k, v in prob["gases"].items()}
+    sub["ncol"] = len(idx)
     return sub
 
 
-def cpu_baseline(prob, target_s, kind="auto", sw=True):
+def _cpu_block(ncol):
+    """Columns per block: the reference RFMIP example's 36 (examples/rfmip-clear-sky/Makefile:7) when it divides the
+    sample, else the largest divisor <= 36 (the driver needs whole blocks, rrtmgp_rfmip_lw.F90:213)."""
+    return max(d for d in range(1, min(36, ncol) + 1) if ncol % d == 0)
+
+
+def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
     """CPU path on the host cores over a bounded sample of the same workload (rank 0, N=1 only).
 
-    kind "reference": the reference's own Fortran compiled from its sources (oracle/_ref: rte_lw, rte_sw and
-    network_type%output_sgemm_flat on MKL sgemm), driven like rrtmgp_rfmip_{lw,sw}.F90 -- OpenMP-style
-    parallelism over blocks of 36 columns (examples/rfmip-clear-sky/Makefile:7), one block per host thread.
-    The reference's NN glue (compute_nn_inputs, get_col_dry, output scaling, compute_Planck_source_nn) is
-    not buildable without netcdf-fortran and is timed from the C restatement (its cost is < 5 %).
-    kind "port": the C restatement alone (bit-identical to the reference on the solvers and MLP), OpenMP."""
+    kind "reference" (default when oracle/_ref is built): oracle/_ref/rrtmgp_cpu_bench (oracle/cpu_bench.F90), the
+    reference's own rte_lw / rte_sw / network_type%output_sgemm_flat (MKL sgemm, sequential) / ty_cloud_optics,
+    compiled from its sources and driven as examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:364-446 drives them: an
+    OpenMP loop over blocks of 36 columns, per-thread objects allocated once.  The NN glue (compute_nn_inputs,
+    get_col_dry, output scaling, compute_Planck_source_nn) is the C restatement's (its reference modules need
+    netcdf-fortran).  Blocks cycle through up to 3 600 columns of the workload; `reps` timed runs, the median
+    reported (tests/test_cpu_bench.py checks the program's fluxes against the oracle bit for bit).
+    kind "port": the C restatement alone, OpenMP over columns (when oracle/_ref is absent)."""
+    import statistics
+    import subprocess
+    import tempfile
+    from rrtmgpnn import data
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    exe = os.path.join(ROOT, "oracle", "_ref", "rrtmgp_cpu_bench")
+    what = "%s gas optics%s + RTE" % ("LW+SW" if sw else "LW",
+                                      " + cloud optics/increment/delta-scale" if clouds is not None else "")
+    if kind in ("auto", "reference") and os.path.exists(exe):
+        ncol = prob["ncol"]
+        nsamp = ncol if ncol <= 3600 else 3600
+        sub = prob if nsamp == ncol else _subset(prob, np.arange(nsamp))
+        cl = None if clouds is None else tuple(np.asarray(c)[:nsamp] for c in clouds)
+        block = _cpu_block(nsamp)
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_STACKSIZE="256M", MKL_THREADING_LAYER="SEQUENTIAL")
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "problem.rbin")
+            data.write_problem(sub, path, clouds=cl)
+
+            def run(ncols, nreps):
+                r = subprocess.run([exe, path, data.DATA_DIR, str(threads), str(block), str(ncols), str(int(sw)),
+                                    str(nreps)], capture_output=True, text=True, env=env, timeout=600)
+                if r.returncode != 0:
+                    raise RuntimeError("rrtmgp_cpu_bench failed: " + (r.stdout + r.stderr)[-400:])
+                return json.loads(r.stdout.strip().splitlines()[-1])
+
+            try:
+                cal = run(nsamp, 1)
+                per_rep = target_s / reps
+                n = max(nsamp, int(round(nsamp * per_rep / max(cal["seconds"][0], 1e-3) / block)) * block)
+                res = run(n, reps)
+            except (RuntimeError, ValueError, subprocess.TimeoutExpired) as e:
+                return {"value": None, "unit": "columns/s", "cores": threads, "kind": "reference",
+                        "sample": "failed: %s" % e}
+        secs = res["seconds"]
+        med = statistics.median(secs)
+        return {"value": round(res["columns"] / med, 1), "unit": "columns/s", "cores": threads, "kind": "reference",
+                "nproc": res["nproc"], "runs_s": [round(t, 4) for t in secs],
+                "spread": round((max(secs) - min(secs)) / med, 4),
+                "sample": ("%d columns per run (blocks of %d cycling through %d columns of the workload), %s, median "
+                           "of %d runs: the reference's Fortran rte_lw/rte_sw + network_type sgemm MLP (MKL, "
+                           "sequential)%s compiled from its sources, OpenMP over blocks on %d threads "
+                           "(oracle/cpu_bench.F90, as rrtmgp_rfmip_lw.F90:364-446); NN glue from the C restatement"
+                           % (res["columns"], block, nsamp, what, len(secs),
+                              " + ty_cloud_optics" if clouds is not None else "", threads))}
+    # the C restatement alone (bit-identical to the reference on the solvers and MLP), OpenMP over columns
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         import oracle as O
         orc = O.Oracle()
     except Exception as e:  # oracle library not built
         return {"value": None, "unit": "columns/s", "cores": 0, "kind": "port", "sample": "unavailable: %s" % e}
-    ref = None
-    if kind in ("auto", "reference"):
-        try:
-            ref = O.Reference()
-        except Exception as e:
-            if kind == "reference":
-                return {"value": None, "unit": "columns/s", "cores": 0, "kind": "reference",
-                        "sample": "unavailable: %s" % e}
-    from rrtmgpnn import data
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    orc.set_threads(threads)
     models_lw = [data.load_model("lw_abs"), data.load_model("lw_pfrac")]
     models_sw = [data.load_model("sw_abs"), data.load_model("sw_ray")]
     kd, kds = data.load_kdist("lw"), data.load_kdist("sw")
-    allsky = "lwp" in prob
-    co_lw, co_sw = (data.load_cloud_optics(w) for w in ("lw", "sw")) if allsky else (None, None)
-
-    def cl(sub):
-        return tuple(sub[k] for k in ("lwp", "iwp", "rel", "rei"))
-
-    if ref is None:
-        orc.set_threads(threads)
-
-        def run(n):
-            sub = _subset(prob, n)
-            if allsky:
-                orc.all_sky_lw(sub, models_lw, kd, co_lw, cl(sub))
-                orc.all_sky_sw(sub, models_sw, kds, co_sw, cl(sub))
-            else:
-                orc.clear_sky_lw(sub, models_lw, kd)
-                if sw:
-                    orc.clear_sky_sw(sub, models_sw, kds)
-        label, desc = "port", "C restatement (oracle), OpenMP over columns"
-    else:
-        import threading
-        from concurrent.futures import ThreadPoolExecutor
-        orc.set_threads(1)
-        threading.stack_size(256 << 20)  # the reference's automatic arrays live on the thread stack
-        block = 36
-
-        def one_block(sub):
-            ncol = sub["ncol"]
-            x = orc.nn_inputs(sub["play"], sub["tlay"], sub["gases"], models_lw[0]).reshape(-1, int(models_lw[0]["dims"][0]))
-            cd = orc.col_dry(sub["gases"]["h2o"], sub["plev"])
-            nlay = sub["play"].shape[1]
-            tau = orc.tau_post(models_lw[0], ref.mlp(models_lw[0], x), cd).reshape(ncol, nlay, -1)
-            pf = ref.mlp(models_lw[1], x)
-            pf = (pf * pf).astype(np.float32).reshape(ncol, nlay, -1)
-            sfc_lay = 1 if sub["play"][0, 0] > sub["play"][0, nlay - 1] else nlay
-            lay, lev, sfc, jac = orc.planck_source(kd, sub["tlay"], sub["tlev"], sub["tsfc"], pf, sfc_lay)
-            emis = np.repeat(np.asarray(sub["sfc_emis"], np.float32)[:, None], kd["nband"], axis=1)
-            if allsky:  # rrtmgp_allsky.F90: cloud_optics -> clouds%increment(atmos)
-                (tau,) = ref.increment_bybnd(kd, (tau,), ref.cloud_optics(co_lw, *cl(sub), nstr=1, icergh=2))
-            ref.rte_lw(kd, tau, lay, lev, sfc, jac, emis, sub["top_at_1"])
-            if not sw:
-                return
-            xs = orc.nn_inputs(sub["play"], sub["tlay"], sub["gases"], models_sw[0]).reshape(-1, int(models_sw[0]["dims"][0]))
-            ta = orc.tau_post(models_sw[0], ref.mlp(models_sw[0], xs), cd)
-            ssa = orc.tau_post(models_sw[1], ref.mlp(models_sw[1], xs), cd, tau_abs_to_tot=ta)
-            ng = ta.shape[-1]
-            toa = data.toa_flux(sub, kds)
-            alb = np.repeat(np.asarray(sub["sfc_alb"], np.float32)[:, None], ng, axis=1)
-            ta, ssa, g = ta.reshape(ncol, nlay, ng), ssa.reshape(ncol, nlay, ng), np.zeros((ncol, nlay, ng), np.float32)
-            if allsky:  # cloud_optics -> clouds%delta_scale() -> clouds%increment(atmos)
-                c = ref.cloud_optics(co_sw, *cl(sub), nstr=2, icergh=2)
-                ta, ssa, g = ref.increment_bybnd(kds, (ta, ssa, g), ref.delta_scale(kds, *c))
-            ref.rte_sw(kds, ta, ssa, g, sub["mu0"], toa, alb, alb, sub["top_at_1"])
-
-        pool = ThreadPoolExecutor(max_workers=threads)
-
-        def run(n):
-            subs = [_subset(prob, block) for _ in range((n + block - 1) // block)]
-            list(pool.map(one_block, subs))
-        label, desc = "reference", ("reference Fortran rte_lw/rte_sw + network_type sgemm MLP (MKL, sequential) "
-                                    "compiled from its sources, blocks of 36 columns over %d host threads; NN glue "
-                                    "from the C restatement" % threads)
-
-    n = 72
-    while True:
+    co_lw, co_sw = (data.load_cloud_optics(w) for w in ("lw", "sw")) if clouds is not None else (None, None)
+    n = min(prob["ncol"], 3600)
+    sub = _subset(prob, np.arange(n))
+    cl = None if clouds is None else tuple(np.asarray(c)[:n] for c in clouds)
+    secs = []
+    for _ in range(reps):
         t0 = time.perf_counter()
-        run(n)
-        dt = time.perf_counter() - t0
-        if dt * 4 > target_s or n >= prob["ncol"] * 256:
-            break
-        n = int(min(n * max(2.0, min(8.0, target_s / max(dt, 1e-3) / 2)), prob["ncol"] * 256))
-        n = (n + 35) // 36 * 36
-    return {"value": round(n / dt, 1), "unit": "columns/s", "cores": threads, "kind": label,
-            "sample": "%d columns of the same workload (%s gas optics%s + RTE), %.1f s: %s"
-                      % (n, "LW+SW" if sw else "LW", " + cloud optics/increment/delta-scale" if allsky else "", dt,
-                         desc)}
+        if cl is not None:
+            orc.all_sky_lw(sub, models_lw, kd, co_lw, cl)
+            orc.all_sky_sw(sub, models_sw, kds, co_sw, cl)
+        else:
+            orc.clear_sky_lw(sub, models_lw, kd)
+            if sw:
+                orc.clear_sky_sw(sub, models_sw, kds)
+        secs.append(time.perf_counter() - t0)
+    med = float(np.median(secs))
+    return {"value": round(n / med, 1), "unit": "columns/s", "cores": threads, "kind": "port",
+            "runs_s": [round(t, 4) for t in secs],
+            "sample": "%d columns of the workload (%s), median of %d runs: C restatement (oracle), OpenMP over columns"
+                      % (n, what, reps)}
 
 
 if __name__ == "__main__":

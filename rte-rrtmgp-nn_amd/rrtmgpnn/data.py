@@ -246,3 +246,23 @@ def toa_flux(problem, kd_sw, tsi_default=1361.0):
     def_tsi = seqsum(toa, axis=1)
     # toa_flux * total_solar_irradiance / def_tsi, evaluated left to right as the driver does (:423)
     return ((toa * np.asarray(problem["tsi"], np.float32)[:, None]) / def_tsi[:, None]).astype(np.float32)
+
+
+def write_problem(prob, path, n_gauss_angles=1, clouds=None):
+    """Write a problem dict in the Fortran host programs' RBIN input format (rrtmgpnn_rfmip_clear_sky.F90's header;
+    also read by oracle/cpu_bench.F90): state arrays, top_at_1, n_gauss_angles, gas_names + vmr_<gas> (every gas
+    broadcast to (ncol, nlay)) and, for all-sky, clouds = (clwp, ciwp, rel, rei) as (ncol, nlay) arrays."""
+    names = sorted(prob["gases"])
+    arrays = {k: np.asarray(prob[k], np.float32) for k in ("play", "plev", "tlay", "tlev", "tsfc", "sfc_emis",
+                                                             "sfc_alb", "mu0", "tsi")}
+    arrays["usecol"] = np.asarray(prob["usecol"], np.float32)
+    arrays["top_at_1"] = np.array([1.0 if prob["top_at_1"] else 0.0], np.float32)
+    arrays["n_gauss_angles"] = np.array([n_gauss_angles], np.float32)
+    arrays["gas_names"] = rbin.chars(names, 32)
+    for g in names:
+        arrays["vmr_" + g] = np.broadcast_to(np.asarray(prob["gases"][g], np.float32), prob["play"].shape).copy()
+    if clouds is not None:
+        for k, a in zip(("clwp", "ciwp", "rel", "rei"), clouds):
+            arrays[k] = np.asarray(a, np.float32)
+    rbin.write(path, arrays)
+    return names

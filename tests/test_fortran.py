@@ -31,19 +31,8 @@ def _make():
 
 
 def write_problem(prob, path, n_gauss_angles=1):
-    from rrtmgpnn import rbin
-    names = sorted(prob["gases"])
-    arrays = {k: np.asarray(prob[k], np.float32) for k in ("play", "plev", "tlay", "tlev", "tsfc", "sfc_emis",
-                                                             "sfc_alb", "mu0", "tsi")}
-    arrays["usecol"] = np.asarray(prob["usecol"], np.float32)
-    arrays["top_at_1"] = np.array([1.0 if prob["top_at_1"] else 0.0], np.float32)
-    arrays["n_gauss_angles"] = np.array([n_gauss_angles], np.float32)
-    arrays["gas_names"] = rbin.chars(names, 32)
-    for g in names:
-        arrays["vmr_" + g] = np.broadcast_to(np.asarray(prob["gases"][g], np.float32),
-                                             prob["play"].shape).copy()
-    rbin.write(path, arrays)
-    return names
+    from rrtmgpnn import data
+    return data.write_problem(prob, path, n_gauss_angles)
 
 
 @needs_fc
