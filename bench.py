@@ -464,9 +464,10 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
                 return json.loads(r.stdout.strip().splitlines()[-1])
 
             try:
-                cal = run(nsamp, 1)
-                per_rep = target_s / reps
-                n = max(nsamp, int(round(nsamp * per_rep / max(cal["seconds"][0], 1e-3) / block)) * block)
+                n0 = max(nsamp, 8 * threads * block)  # every thread busy for the calibration run too
+                cal = run(n0, 1)  # after the program's own untimed warm-up pass
+                per_rep = target_s / (reps + 1)
+                n = max(nsamp, int(round(n0 * per_rep / max(cal["seconds"][0], 1e-4) / block)) * block)
                 res = run(n, reps)
             except (RuntimeError, ValueError, subprocess.TimeoutExpired) as e:
                 return {"value": None, "unit": "columns/s", "cores": threads, "kind": "reference",
