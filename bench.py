@@ -54,6 +54,11 @@ def parse():
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
                     help="SW solver: 0 the library's choice, 1 / 2 g-points per lane, 3 checkpointed passes "
                          "(rrtmgpnn_context_set_sw_kernel)")
+    ap.add_argument("--fortran", action="store_true",
+                    help="time the Fortran drop-in instead: rrtmgpnn_rfmip_clear_sky's block loop on the C3 columns "
+                         "(host arrays in and out, as a reference driver calls it)")
+    ap.add_argument("--fortran-block", type=int, default=1800, help="--fortran: columns per block")
+    ap.add_argument("--fortran-threads", type=int, default=1, help="--fortran: OpenMP threads over blocks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
@@ -113,8 +118,46 @@ def stage_work(name, step):
     return "byte", 0, None, None
 
 
+def fortran_bench(args):
+    """--fortran: the Fortran drop-in measured through its own host program.  rrtmgpnn_rfmip_clear_sky
+    (rte-rrtmgp-nn_amd/fortran, shaped like examples/rfmip-clear-sky/rrtmgp_rfmip_{lw,sw}.F90) runs its block loop
+    --steps + 1 times over the 1800 C3 columns -- per block gas_optics -> rte_lw and gas_optics -> rte_sw through the
+    reference's interfaces, state arrays copied in and fluxes copied out every call, optical properties and sources
+    device-resident in between -- and reports the mean of the last --steps loops (system_clock)."""
+    import re
+    import subprocess
+    import tempfile
+    from rrtmgpnn import data
+    exe = os.path.join(ROOT, "rte-rrtmgp-nn_amd", "fortran", "build", "rrtmgpnn_rfmip_clear_sky")
+    prob = data.rfmip_columns(0, 1800)
+    env = dict(os.environ, OMP_NUM_THREADS=str(args.fortran_threads))
+    with tempfile.TemporaryDirectory() as td:
+        pin, pout = os.path.join(td, "p.rbin"), os.path.join(td, "f.rbin")
+        data.write_problem(prob, pin)
+        r = subprocess.run([exe, pin, pout, data.DATA_DIR, str(args.fortran_block), str(args.steps + 1)],
+                           capture_output=True, text=True, env=env, timeout=600)
+    m = re.search(r"timing:\s*([0-9.]+) ms per block loop", r.stdout)
+    if r.returncode != 0 or not m:
+        raise SystemExit("bench --fortran: host program failed: " + (r.stdout + r.stderr)[-600:])
+    ms = float(m.group(1))
+    nblocks = (1800 + args.fortran_block - 1) // args.fortran_block
+    print(json.dumps({
+        "metric": METRIC, "value": round(1800 / (ms * 1e-3), 1), "unit": "columns/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": 1, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "real RFMIP inputs (reference's RFMIP file) + the reference's trained NN weights; surrogate k-dist tables",
+        "config": {"workload": "C3 through the Fortran drop-in: rrtmgpnn_rfmip_clear_sky's block loop (gas_optics + "
+                               "rte_lw, gas_optics + rte_sw per block; host arrays in, fluxes out)",
+                   "global_columns": 1800, "nlay": 60, "block_size": args.fortran_block, "blocks": nblocks,
+                   "threads": args.fortran_threads, "parallelism": "OpenMP over blocks, a device context per thread"},
+        "column_layers_per_s": round(1800 * 60 / (ms * 1e-3), 1)}), flush=True)
+
+
 def main():
     args = parse()
+    if args.fortran:
+        fortran_bench(args)
+        return
     import torch
     import torch.distributed as dist
 

@@ -68,6 +68,42 @@ int rrtmgpnn_malloc(rrtmgpnn_context *ctx, long long bytes, void **dptr);
 int rrtmgpnn_free(rrtmgpnn_context *ctx, void *dptr);
 int rrtmgpnn_memcpy_h2d(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes);
 int rrtmgpnn_memcpy_d2h(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes);
+/* A context whose work runs on a stream it creates and owns (non-blocking), so host threads with a context each
+ * (OpenMP over blocks, rrtmgp_rfmip_lw.F90:364-367) run concurrently on the device.  No reference counterpart. */
+int rrtmgpnn_context_create_owned(int device, rrtmgpnn_context **ctx);
+
+/* ---- Device data environment of a context: the OpenACC data regions of the reference's GPU build ----
+ * The reference keeps optical properties, sources and gas concentrations on the device between calls with
+ * `!$acc enter data create/copyin` (ty_gas_concs%set_vmr, rrtmgp/mo_gas_concentrations.F90:166; the optical-property
+ * and source constructors, examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:325-327; gas_optics,
+ * rrtmgp/mo_gas_optics_rrtmgp.F90:281-426) and `!$acc update host` / `exit data delete`.  Here a context maps a
+ * host array (its address and size) to a device copy from the context's pool, with a state: host newer, both
+ * current, device newer.  All transfers are ordered on the context's stream; a context serves one host thread.
+ * rrtmgpnn_present: the device copy of host[0, bytes); mode RRTMGPNN_PRESENT_READ uploads it first when the host
+ *   copy is newer (created on first use, `copyin`); RRTMGPNN_PRESENT_WRITE marks the device copy newer (the caller's
+ *   kernel writes it; `create`); both bits: upload if needed, then device newer.  A different size for the same
+ *   address replaces the entry (host newer).
+ * rrtmgpnn_present_update_host: copy a device-newer array back (`!$acc update host`) and wait for it.
+ * rrtmgpnn_present_update_device: the host copy changed: it is uploaded at its next READ (`!$acc update device`).
+ * rrtmgpnn_present_delete: drop the entry (its buffer returns to the pool; `!$acc exit data delete`); no-op if absent.
+ * rrtmgpnn_stage_h2d / rrtmgpnn_scratch / rrtmgpnn_release: stream-ordered per-call buffers from the same pool
+ *   (a call's inputs copied in, its intermediates); released buffers are reused by later work on the stream.
+ * rrtmgpnn_copy_d2h / rrtmgpnn_copy_h2d / rrtmgpnn_copy_d2d: enqueue a copy on the context's stream (the device side complete after
+ *   rrtmgpnn_context_synchronize; the host buffer of an H2D copy may be reused on return).
+ * rrtmgpnn_memset_async: bytes of a device buffer set to `value`, on the context's stream. */
+#define RRTMGPNN_PRESENT_READ  1
+#define RRTMGPNN_PRESENT_WRITE 2
+int rrtmgpnn_present(rrtmgpnn_context *ctx, const void *host, long long bytes, int mode, void **dptr);
+int rrtmgpnn_present_update_host(rrtmgpnn_context *ctx, void *host);
+int rrtmgpnn_present_update_device(rrtmgpnn_context *ctx, const void *host);
+int rrtmgpnn_present_delete(rrtmgpnn_context *ctx, const void *host);
+int rrtmgpnn_stage_h2d(rrtmgpnn_context *ctx, const void *host, long long bytes, void **dptr);
+int rrtmgpnn_scratch(rrtmgpnn_context *ctx, long long bytes, void **dptr);
+int rrtmgpnn_release(rrtmgpnn_context *ctx, void *dptr);
+int rrtmgpnn_copy_d2h(rrtmgpnn_context *ctx, void *host, const void *dptr, long long bytes);
+int rrtmgpnn_copy_h2d(rrtmgpnn_context *ctx, void *dptr, const void *host, long long bytes);
+int rrtmgpnn_copy_d2d(rrtmgpnn_context *ctx, void *dst, const void *src, long long bytes);
+int rrtmgpnn_memset_async(rrtmgpnn_context *ctx, void *dptr, int value, long long bytes);
 
 /* ---- neural networks: replaces rrtmgp_network_type (neural/mod_network_rrtmgp.F90:34-122) ---- */
 /* Load an RBIN model file (converted from the reference's netCDF model files). */

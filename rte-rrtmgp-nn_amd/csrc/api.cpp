@@ -163,7 +163,7 @@ int rrtmgpnn_context_destroy(rrtmgpnn_context *ctx)
 {
   if (!ctx) return RRTMGPNN_OK;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  ctx->pool_clear();
   if (ctx->ws) (void)hipFree(ctx->ws);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -206,8 +206,7 @@ void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx) { return ctx ? (void *)ctx-
 int rrtmgpnn_context_synchronize(rrtmgpnn_context *ctx)
 {
   if (int rc = check_ctx(ctx)) return rc;
-  RRTMGPNN_HIP(hipStreamSynchronize(ctx->stream));
-  return RRTMGPNN_OK;
+  return ctx->sync();  // also completes queued rrtmgpnn_copy_d2h copies
 }
 
 int rrtmgpnn_malloc(rrtmgpnn_context *ctx, long long bytes, void **dptr)

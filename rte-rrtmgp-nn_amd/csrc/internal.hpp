@@ -4,7 +4,9 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/rrtmgpnn.h"
@@ -55,6 +57,32 @@ struct rrtmgpnn_context {
   size_t ws_bytes = 0;
   bool ws_pinned = false;
   int workspace(size_t bytes, void **out);
+  // device data environment (present.cpp): a caching pool of device buffers and the host -> device map
+  struct Present {
+    void *dev = nullptr;
+    size_t bytes = 0;
+    int state = 0;  // 0 host newer, 1 both current, 2 device newer
+  };
+  std::multimap<size_t, void *> pool_free;      // capacity -> buffer
+  std::unordered_map<void *, size_t> pool_live;  // buffer -> capacity
+  std::unordered_map<const void *, Present> present;
+  int pool_get(size_t bytes, void **out);
+  void pool_put(void *p);
+  void pool_clear();
+  // pinned staging ring for host <-> device copies of pageable host arrays: the host side is one memcpy into the
+  // ring, the DMA runs asynchronously on the stream; the ring is reused after sync(), which also completes the
+  // device-to-host copies queued in pending_d2h
+  void *pin = nullptr;
+  size_t pin_cap = 0, pin_head = 0;
+  struct PendingD2H {
+    void *dst;
+    const void *src;
+    size_t bytes;
+  };
+  std::vector<PendingD2H> pending_d2h;
+  int h2d(void *dst, const void *host, size_t bytes);
+  int d2h(void *host, const void *dev, size_t bytes);
+  int sync();
 };
 
 // A network: host copy of the model + device images.

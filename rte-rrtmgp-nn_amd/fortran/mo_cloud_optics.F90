@@ -191,9 +191,9 @@ contains
     real(wp), dimension(:,:),     intent(in)    :: clwp, ciwp, reliq, reice
     class(ty_optical_props_arry), intent(inout) :: optical_props
     character(len=128) :: error_msg
-    integer :: ncol, nlay, nbnd, n
+    integer :: ncol, nlay, nbnd
+    integer(c_long_long) :: n, nl
     type(c_ptr) :: d_lwp, d_iwp, d_rel, d_rei, d_tau, d_ssa, d_g
-    character(len=128) :: e
 
     error_msg = ''
     if (.not. c_associated(this%h)) then
@@ -221,33 +221,25 @@ contains
       if (error_msg /= "") return
     end if
 
-    n = nbnd * nlay * ncol
-    d_lwp = dev_upload(clwp, nlay * ncol)
-    d_iwp = dev_upload(ciwp, nlay * ncol)
-    d_rel = dev_upload(reliq, nlay * ncol)
-    d_rei = dev_upload(reice, nlay * ncol)
-    d_tau = dev_alloc(n)
+    n = int(nbnd, c_long_long) * nlay * ncol
+    nl = int(nlay, c_long_long) * ncol
+    d_lwp = dev_stage(clwp, nl)
+    d_iwp = dev_stage(ciwp, nl)
+    d_rel = dev_stage(reliq, nl)
+    d_rei = dev_stage(reice, nl)
+    d_tau = dev_present(optical_props%tau, n, PRESENT_WRITE)
     d_ssa = c_null_ptr
     d_g   = c_null_ptr
     select type (optical_props)
     class is (ty_optical_props_2str)
-      d_ssa = dev_alloc(n)
-      d_g   = dev_alloc(n)
+      d_ssa = dev_present(optical_props%ssa, n, PRESENT_WRITE)
+      d_g   = dev_present(optical_props%g, n, PRESENT_WRITE)
+      optical_props%g_zero = .false.
     end select
+    ! the cloud optical properties stay on the device for increment / delta_scale / the solvers
     error_msg = rrtmgpnn_check(c_rrtmgpnn_cloud_optics_compute(rrtmgpnn_ctx(), this%h, ncol, nlay, d_lwp, d_iwp, &
                                d_rel, d_rei, d_tau, d_ssa, d_g), "cloud optics")
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "cloud optics")
-    if (error_msg == '') error_msg = e
-    if (error_msg == '') then
-      call dev_download(optical_props%tau, d_tau, n)
-      select type (optical_props)
-      class is (ty_optical_props_2str)
-        call dev_download(optical_props%ssa, d_ssa, n)
-        call dev_download(optical_props%g, d_g, n)
-      end select
-    end if
-    call dev_free(d_lwp); call dev_free(d_iwp); call dev_free(d_rel); call dev_free(d_rei)
-    call dev_free(d_tau); call dev_free(d_ssa); call dev_free(d_g)
+    call dev_release(d_lwp); call dev_release(d_iwp); call dev_release(d_rel); call dev_release(d_rei)
   end function cloud_optics
 
   ! set_ice_roughness (:541-554)

@@ -1,13 +1,19 @@
 ! mo_gas_concentrations -- drop-in for rrtmgp/mo_gas_concentrations.F90 (ty_gas_concs): per-gas volume
 ! mixing ratios stored as conc(1,1) (scalar), conc(nlay,1) (1-D) or conc(nlay,ncol) (2-D), as :50-59.
+! Each concentration array has a device copy in the calling thread's context, uploaded when gas optics first
+! reads it after set_vmr (the reference copies it in set_vmr, `!$acc enter data copyin`, :166).
 module mo_gas_concentrations
+  use, intrinsic :: iso_c_binding, only: c_ptr, c_long_long
   use mo_rte_kind, only: wp
+  use mo_rrtmgpnn_c, only: dev_present, dev_delete, PRESENT_READ
   implicit none
   private
   integer, parameter, public :: GAS_NOT_IN_LIST = 0
 
   type, public :: conc_field
     real(wp), dimension(:,:), allocatable :: conc
+  contains
+    final :: final_conc  ! drops the device copy with the array
   end type conc_field
 
   type, public :: ty_gas_concs
@@ -21,6 +27,7 @@ module mo_gas_concentrations
     procedure, public :: get_gas_names
     procedure, public :: find_gas
     procedure, public :: get_conc_dims_and_igas
+    procedure, public :: device_conc
   end type ty_gas_concs
 
 contains
@@ -40,7 +47,12 @@ contains
       end do
     end do
     if (allocated(this%gas_name)) deallocate(this%gas_name)
-    if (allocated(this%concs)) deallocate(this%concs)
+    if (allocated(this%concs)) then
+      do i = 1, size(this%concs)
+        call drop_conc(this%concs(i))
+      end do
+      deallocate(this%concs)
+    end if
     allocate(this%gas_name(size(gas_names)), this%concs(size(gas_names)))
     do i = 1, size(gas_names)
       this%gas_name(i) = lower(gas_names(i))
@@ -63,7 +75,7 @@ contains
     if (igas == GAS_NOT_IN_LIST) then
       error_msg = 'ty_gas_concs%set_vmr(): trying to set ' // trim(gas) // ' but name not present'; return
     end if
-    if (allocated(this%concs(igas)%conc)) deallocate(this%concs(igas)%conc)
+    call drop_conc(this%concs(igas))
     allocate(this%concs(igas)%conc(1,1))
     this%concs(igas)%conc(1,1) = w
   end function set_vmr_scalar
@@ -86,7 +98,7 @@ contains
       error_msg = 'ty_gas_concs%set_vmr(): trying to set ' // trim(gas) // ' but name not present'; return
     end if
     this%nlay = size(w)
-    if (allocated(this%concs(igas)%conc)) deallocate(this%concs(igas)%conc)
+    call drop_conc(this%concs(igas))
     allocate(this%concs(igas)%conc(this%nlay, 1))
     this%concs(igas)%conc(:,1) = w
   end function set_vmr_1d
@@ -110,7 +122,7 @@ contains
     end if
     this%nlay = size(w, 1)
     this%ncol = size(w, 2)
-    if (allocated(this%concs(igas)%conc)) deallocate(this%concs(igas)%conc)
+    call drop_conc(this%concs(igas))
     allocate(this%concs(igas)%conc(this%nlay, this%ncol))
     this%concs(igas)%conc = w
   end function set_vmr_2d
@@ -155,6 +167,27 @@ contains
       ndims = 1
     end if
   end function get_conc_dims_and_igas
+
+  ! The device copy of gas igas's concentration array (uploaded when set_vmr changed it since the last read).
+  function device_conc(this, igas) result(d)
+    class(ty_gas_concs), intent(in) :: this
+    integer, intent(in) :: igas
+    type(c_ptr) :: d
+    d = dev_present(this%concs(igas)%conc, size(this%concs(igas)%conc, kind=c_long_long), PRESENT_READ)
+  end function device_conc
+
+  subroutine drop_conc(f)
+    type(conc_field), intent(inout) :: f
+    if (allocated(f%conc)) then
+      call dev_delete(f%conc)
+      deallocate(f%conc)
+    end if
+  end subroutine drop_conc
+
+  subroutine final_conc(f)
+    type(conc_field), intent(inout) :: f
+    if (allocated(f%conc)) call dev_delete(f%conc)
+  end subroutine final_conc
 
   pure function lower(s) result(r)
     character(len=*), intent(in) :: s

@@ -1,9 +1,12 @@
 ! mo_gas_optics_rrtmgp -- drop-in for rrtmgp/mo_gas_optics_rrtmgp.F90, neural-network branch.
 ! ty_gas_optics_rrtmgp keeps the reference's generic `gas_optics` (gas_optics_int :239-428 for the
 ! longwave / internal source, gas_optics_ext :433-602 for the shortwave / external source) with the
-! same arguments, error strings and optional `neural_nets`.  Inputs are staged to the device once per
-! call, the whole chain (col_dry, tlev, compute_nn_inputs, fused MLP, Planck source) runs in the HIP
-! kernels of librrtmgpnn.so, and the outputs come back into the caller's host arrays.
+! same arguments, error strings and optional `neural_nets`.  The state arrays are copied to the device per call
+! (gas_optics' `!$acc enter data copyin`, :281), gas concentrations once per set_vmr; compute_nn_inputs,
+! get_col_dry and the networks run as one fused kernel (rrtmgpnn_gas_optics_{lw,sw}_nn) writing the optical
+! properties' device copies, which stay there for rte_lw / rte_sw (mo_optical_props).  The longwave Planck sources
+! are left to be formed inside the solver (ty_source_func_lw%planck_deferred).  Nothing waits for the device here:
+! errors of the enqueued kernels surface at the next synchronising call.
 ! The lookup-table branch (compute_gas_optics) needs the k-distribution netCDF files that are absent
 ! from the reference; calling gas_optics without neural_nets returns an error string.
 module mo_gas_optics_rrtmgp
@@ -28,7 +31,6 @@ module mo_gas_optics_rrtmgp
     real(wp), dimension(:,:), allocatable :: totplnk        ! (nPlanckTemp, nband)
     real(wp), dimension(:),   allocatable :: solar_source   ! (ngpt)
     character(len=32), dimension(:), allocatable :: gas_names
-    type(c_ptr) :: d_totplnk = c_null_ptr
   contains
     procedure, public :: load_rbin
     procedure, public :: source_is_internal
@@ -70,14 +72,15 @@ contains
     this%temp_ref_min = tmp(1)
     call rbin_real1(filename, "temp_ref_max", tmp, error_msg); if (error_msg /= '') return
     this%temp_ref_max = tmp(1)
-    if (allocated(this%totplnk)) deallocate(this%totplnk)
+    if (allocated(this%totplnk)) then
+      call dev_delete(this%totplnk)
+      deallocate(this%totplnk)
+    end if
     if (allocated(this%solar_source)) deallocate(this%solar_source)
-    call dev_free(this%d_totplnk)
     call rbin_real2(filename, "totplnk", this%totplnk, e)
     if (e == '') then
       ! totplnk_delta = (temp_ref_max - temp_ref_min) / (nPlanckTemp - 1)   (:1218)
       this%totplnk_delta = (this%temp_ref_max - this%temp_ref_min) / real(size(this%totplnk, 1) - 1, wp)
-      this%d_totplnk = dev_upload(this%totplnk, size(this%totplnk))
     else
       call rbin_real1(filename, "solar_source", this%solar_source, e)
       if (e /= '') then
@@ -155,25 +158,25 @@ contains
   end function set_tsi
 
   ! ---------------------------------------------------------------------------------------------------
-  ! Device staging shared by both entry points: col_dry (given or from h2o, :347-363) and the network
-  ! input tensor (compute_nn_inputs, :618-798).  On success d_coldry and d_x are device arrays the caller
-  ! frees.
-  function stage_inputs(nlay, ncol, play, plev, tlay, gas_desc, col_dry, net, d_play, d_plev, d_tlay, &
-                        d_coldry, d_x) result(error_msg)
+  ! Network inputs on the device, shared by both entry points: the gas concentrations of inputs 3.. (their device
+  ! copies, cached per set_vmr), h2o as a (nlay, ncol) array for get_col_dry (:347-363).  On success d_h2o must be
+  ! released by the caller when h2o_tmp is set.
+  function gas_inputs(nlay, ncol, gas_desc, net, gas_ptr, gas_nd, d_h2o, h2o_tmp) result(error_msg)
     integer, intent(in) :: nlay, ncol
-    real(wp), dimension(:,:), intent(in) :: play, plev, tlay
     type(ty_gas_concs), intent(in) :: gas_desc
-    real(wp), dimension(:,:), optional, intent(in) :: col_dry
     type(rrtmgp_network_type), intent(in) :: net
-    type(c_ptr), intent(out) :: d_play, d_plev, d_tlay, d_coldry, d_x
+    type(c_ptr), intent(out) :: gas_ptr(MAX_INPUTS), d_h2o
+    integer(c_int), intent(out) :: gas_nd(MAX_INPUTS)
+    logical, intent(out) :: h2o_tmp
     character(len=128) :: error_msg
-    type(c_ptr) :: d_h2o, gas_ptr(MAX_INPUTS)
-    integer(c_int) :: gas_nd(MAX_INPUTS)
     integer :: ninputs, k, igas, nd
     real(wp), allocatable :: h2o(:,:)
     character(len=128) :: e
     error_msg = ''
-    d_play = c_null_ptr; d_plev = c_null_ptr; d_tlay = c_null_ptr; d_coldry = c_null_ptr; d_x = c_null_ptr
+    gas_ptr = c_null_ptr
+    gas_nd = 2
+    d_h2o = c_null_ptr
+    h2o_tmp = .false.
     ninputs = size(net%layers(1)%w_transposed, 2)
     if (ninputs > MAX_INPUTS .or. ninputs < 3) then
       error_msg = "compute_nn_inputs: unsupported number of network inputs"; return
@@ -186,44 +189,27 @@ contains
         error_msg = "compute_nn_inputs: gas " // trim(net%input_names(k)) // " not found"; return
       end if
     end do
-    d_play = dev_upload(play, nlay * ncol)
-    d_plev = dev_upload(plev, (nlay + 1) * ncol)
-    d_tlay = dev_upload(tlay, nlay * ncol)
-    if (present(col_dry)) then
-      d_coldry = dev_upload(col_dry, nlay * ncol)
+    e = gas_desc%get_conc_dims_and_igas('h2o', nd, igas)
+    if (e /= '') then
+      error_msg = "gas_optics(): h2o concentration is required"; return
+    end if
+    if (nd == 2) then
+      d_h2o = gas_desc%device_conc(igas)
     else
-      d_coldry = dev_alloc(nlay * ncol)
-      e = gas_desc%get_conc_dims_and_igas('h2o', nd, igas)
-      if (e /= '') then
-        error_msg = "gas_optics(): h2o concentration is required"; return
-      end if
       allocate(h2o(nlay, ncol))
       h2o = spread_conc(gas_desc%concs(igas)%conc, nd, nlay, ncol)
-      d_h2o = dev_upload(h2o, nlay * ncol)
-      error_msg = rrtmgpnn_check(c_rrtmgpnn_get_col_dry(rrtmgpnn_ctx(), ncol, nlay, d_h2o, d_plev, d_coldry), &
-                                 "get_col_dry")
-      call dev_free(d_h2o)
-      if (error_msg /= '') return
+      d_h2o = dev_stage(h2o, int(nlay, c_long_long) * ncol)
+      h2o_tmp = .true.
     end if
-    gas_ptr = c_null_ptr
-    gas_nd = 2
     do k = 3, ninputs
       igas = gas_desc%find_gas(net%input_names(k))
-      if (igas == GAS_NOT_IN_LIST) cycle
+      if (igas == GAS_NOT_IN_LIST) cycle  ! missing gases are zero (quirk B-2)
       if (.not. allocated(gas_desc%concs(igas)%conc)) cycle
       e = gas_desc%get_conc_dims_and_igas(net%input_names(k), nd, igas)
       gas_nd(k) = nd
-      gas_ptr(k) = dev_upload(gas_desc%concs(igas)%conc, size(gas_desc%concs(igas)%conc))
+      gas_ptr(k) = gas_desc%device_conc(igas)
     end do
-    d_x = dev_alloc(ninputs * nlay * ncol)
-    error_msg = rrtmgpnn_check(c_rrtmgpnn_compute_nn_inputs(rrtmgpnn_ctx(), ncol, nlay, ninputs, d_play, d_tlay, &
-                               gas_ptr, gas_nd, net%handle, d_x), "compute_nn_inputs")
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "compute_nn_inputs")
-    if (error_msg == '') error_msg = e
-    do k = 3, ninputs
-      call dev_free(gas_ptr(k))
-    end do
-  end function stage_inputs
+  end function gas_inputs
 
   function spread_conc(conc, nd, nlay, ncol) result(full)
     real(wp), dimension(:,:), intent(in) :: conc
@@ -242,6 +228,24 @@ contains
     end select
   end function spread_conc
 
+  ! compute_nn_inputs + get_col_dry (or the caller's col_dry) as separate kernels into scratch buffers: the path
+  ! of a user col_dry= (the fused kernels form the column amounts from h2o themselves)
+  function staged_nn_inputs(nlay, ncol, net, d_play, d_tlay, gas_ptr, gas_nd, col_dry, d_x, d_cd) result(error_msg)
+    integer, intent(in) :: nlay, ncol
+    type(rrtmgp_network_type), intent(in) :: net
+    type(c_ptr), intent(in) :: d_play, d_tlay, gas_ptr(MAX_INPUTS)
+    integer(c_int), intent(in) :: gas_nd(MAX_INPUTS)
+    real(wp), dimension(:,:), intent(in) :: col_dry
+    type(c_ptr), intent(out) :: d_x, d_cd
+    character(len=128) :: error_msg
+    integer :: ninputs
+    ninputs = size(net%layers(1)%w_transposed, 2)
+    d_cd = dev_stage(col_dry, int(nlay, c_long_long) * ncol)
+    d_x = dev_scratch(int(ninputs, c_long_long) * nlay * ncol)
+    error_msg = rrtmgpnn_check(c_rrtmgpnn_compute_nn_inputs(rrtmgpnn_ctx(), ncol, nlay, ninputs, d_play, d_tlay, &
+                               gas_ptr, gas_nd, net%handle, d_x), "compute_nn_inputs")
+  end function staged_nn_inputs
+
   ! ---------------------------------------------------------------------------------------------------
   ! gas_optics_int (:239-428): LW optical depth and Planck sources.
   function gas_optics_int(this, play, plev, tlay, tsfc, gas_desc, optical_props, sources, col_dry, tlev, &
@@ -256,11 +260,12 @@ contains
     real(wp), dimension(:,:), intent(in), optional :: tlev
     type(rrtmgp_network_type), dimension(:), intent(in), optional :: neural_nets
     character(len=128) :: error_msg
-    integer :: ncol, nlay, ngpt, nband, ninputs, n, sfc_lay
-    type(c_ptr) :: d_play, d_plev, d_tlay, d_coldry, d_x, d_tsfc, d_tlev, d_tau, d_lay, d_lev, d_sfc, d_jac
-    type(c_ptr) :: nets(2)
-    integer(c_int), allocatable :: lims(:,:)
-    character(len=128) :: e
+    integer :: ncol, nlay, ngpt, nband, ninputs, n
+    integer(c_long_long) :: nl, nv, ng
+    type(c_ptr) :: d_play, d_plev, d_tlay, d_tlev, d_tsfc, d_tau, d_pf, d_h2o, d_x, d_cd
+    type(c_ptr) :: nets(2), gas_ptr(MAX_INPUTS)
+    integer(c_int) :: gas_nd(MAX_INPUTS)
+    logical :: h2o_tmp
 
     ncol  = size(play, dim=2)
     nlay  = size(play, dim=1)
@@ -294,53 +299,78 @@ contains
       return
     end if
     ninputs = size(neural_nets(1)%layers(1)%w_transposed, 2)
+    error_msg = gas_inputs(nlay, ncol, gas_desc, neural_nets(1), gas_ptr, gas_nd, d_h2o, h2o_tmp)
+    if (error_msg /= '') return
+    nl = int(nlay, c_long_long) * ncol
+    nv = int(nlay + 1, c_long_long) * ncol
+    ng = int(ngpt, c_long_long) * nlay * ncol
 
-    error_msg = stage_inputs(nlay, ncol, play, plev, tlay, gas_desc, col_dry, neural_nets(1), &
-                             d_play, d_plev, d_tlay, d_coldry, d_x)
-    if (error_msg == '') then
-      if (present(tlev)) then
-        d_tlev = dev_upload(tlev, (nlay + 1) * ncol)
-      else
-        d_tlev = dev_alloc((nlay + 1) * ncol)
-        error_msg = rrtmgpnn_check(c_rrtmgpnn_interpolate_tlev(rrtmgpnn_ctx(), ncol, nlay, d_play, d_plev, d_tlay, &
-                                                               d_tlev), "interpolate_tlev")
-      end if
-      d_tsfc = dev_upload(tsfc, ncol)
-      d_tau = dev_alloc(ngpt * nlay * ncol)
-      d_lay = dev_alloc(ngpt * nlay * ncol)
-      d_lev = dev_alloc(ngpt * (nlay + 1) * ncol)
-      d_sfc = dev_alloc(ngpt * ncol)
-      d_jac = dev_alloc(ngpt * ncol)
-      nets = c_null_ptr
-      nets(1) = neural_nets(1)%handle
-      if (n == 2) nets(2) = neural_nets(2)%handle
-      if (error_msg == '') &
-        error_msg = rrtmgpnn_check(c_rrtmgpnn_predict_nn_lw(rrtmgpnn_ctx(), ncol, nlay, ngpt, ninputs, d_x, d_coldry, &
-                                                            nets, n, d_tau, d_lay), "predict_nn_lw")
-      ! Planck source from the predicted Planck fraction (:398-404); surface at index 1 if pressure decreases
-      sfc_lay = merge(1, nlay, play(1, 1) > play(nlay, 1))
-      lims = this%get_band_lims_gpoint()
-      if (error_msg == '') &
-        error_msg = rrtmgpnn_check(c_rrtmgpnn_compute_planck_source_nn(rrtmgpnn_ctx(), ncol, nlay, nband, ngpt, &
-                      this%get_nPlanckTemp(), d_tlay, d_tlev, d_tsfc, sfc_lay, lims, this%temp_ref_min, &
-                      this%totplnk_delta, this%d_totplnk, d_sfc, d_jac, d_lay, d_lev), "compute_planck_source_nn")
-      e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "gas_optics")
-      if (error_msg == '') error_msg = e
-      if (error_msg == '') then
-        call dev_download(optical_props%tau, d_tau, ngpt * nlay * ncol)
-        call dev_download(sources%lay_source, d_lay, ngpt * nlay * ncol)
-        call dev_download(sources%lev_source, d_lev, ngpt * (nlay + 1) * ncol)
-        call dev_download(sources%sfc_source, d_sfc, ngpt * ncol)
-        call dev_download(sources%sfc_source_Jac, d_jac, ngpt * ncol)
-      end if
-      call dev_free(d_tlev); call dev_free(d_tsfc); call dev_free(d_tau); call dev_free(d_lay)
-      call dev_free(d_lev); call dev_free(d_sfc); call dev_free(d_jac)
+    ! the temperatures the deferred Planck sources need live on in the source object's device copies
+    call keep_shape2(sources%pk_tlay, nlay, ncol)
+    call keep_shape2(sources%pk_tlev, nlay + 1, ncol)
+    if (allocated(sources%pk_tsfc)) then
+      if (size(sources%pk_tsfc) /= ncol) deallocate(sources%pk_tsfc)
     end if
-    call dev_free(d_play); call dev_free(d_plev); call dev_free(d_tlay); call dev_free(d_coldry); call dev_free(d_x)
+    if (.not. allocated(sources%pk_tsfc)) allocate(sources%pk_tsfc(ncol))
+    d_tlay = dev_present(sources%pk_tlay, nl, PRESENT_WRITE)
+    call dev_copy_in(d_tlay, tlay, nl)
+    d_tsfc = dev_present(sources%pk_tsfc, int(ncol, c_long_long), PRESENT_WRITE)
+    call dev_copy_in(d_tsfc, tsfc, int(ncol, c_long_long))
+    d_play = dev_stage(play, nl)
+    d_plev = dev_stage(plev, nv)
+    d_tlev = dev_present(sources%pk_tlev, nv, PRESENT_WRITE)
+    if (present(tlev)) then
+      call dev_copy_in(d_tlev, tlev, nv)
+    else  ! level temperatures interpolated from the layers (:317-337)
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_interpolate_tlev(rrtmgpnn_ctx(), ncol, nlay, d_play, d_plev, d_tlay, &
+                                                             d_tlev), "interpolate_tlev")
+    end if
+    d_tau = dev_present(optical_props%tau, ng, PRESENT_WRITE)
+    d_pf = dev_present(sources%lay_source, ng, PRESENT_WRITE)  ! the Planck fraction until the sources are formed
+    nets = c_null_ptr
+    nets(1) = neural_nets(1)%handle
+    if (n == 2) nets(2) = neural_nets(2)%handle
+    if (error_msg == '') then
+      if (present(col_dry)) then  ! B-3 fixed: the caller's column amounts are used (:342-346)
+        error_msg = staged_nn_inputs(nlay, ncol, neural_nets(1), d_play, d_tlay, gas_ptr, gas_nd, col_dry, d_x, d_cd)
+        if (error_msg == '') &
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_predict_nn_lw(rrtmgpnn_ctx(), ncol, nlay, ngpt, ninputs, d_x, d_cd, &
+                                                              nets, n, d_tau, d_pf), "predict_nn_lw")
+        call dev_release(d_x)
+        call dev_release(d_cd)
+      else  ! compute_nn_inputs + get_col_dry + predict_nn_lw_blas in one kernel (:342-391)
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_gas_optics_lw_nn(rrtmgpnn_ctx(), ncol, nlay, ngpt, ninputs, d_play, &
+                                   d_tlay, d_plev, d_h2o, gas_ptr, gas_nd, nets, n, d_tau, d_pf), "gas_optics_lw_nn")
+      end if
+    end if
+    call dev_release(d_play)
+    call dev_release(d_plev)
+    if (h2o_tmp) call dev_release(d_h2o)
+    if (error_msg /= '') return
+    ! Planck source from the predicted Planck fraction (:398-404), deferred to the solver; surface at index 1 if
+    ! pressure decreases with index
+    sources%planck_deferred = .true.
+    sources%pk_sfc_lay = merge(1, nlay, play(1, 1) > play(nlay, 1))
+    sources%pk_ntemp = this%get_nPlanckTemp()
+    sources%pk_tmin = this%temp_ref_min
+    sources%pk_tdelta = this%totplnk_delta
+    sources%pk_totplnk = dev_present(this%totplnk, size(this%totplnk, kind=c_long_long), PRESENT_READ)
   end function gas_optics_int
 
+  subroutine keep_shape2(a, n1, n2)
+    real(wp), allocatable, intent(inout) :: a(:,:)
+    integer, intent(in) :: n1, n2
+    if (allocated(a)) then
+      if (size(a, 1) /= n1 .or. size(a, 2) /= n2) then
+        call dev_delete(a)
+        deallocate(a)
+      end if
+    end if
+    if (.not. allocated(a)) allocate(a(n1, n2))
+  end subroutine keep_shape2
+
   ! ---------------------------------------------------------------------------------------------------
-  ! gas_optics_ext (:433-602): SW optical depth (+ Rayleigh single-scattering albedo for 2str) and the
+  ! gas_optics_ext (:433-602): SW optical depth (+ Rayleigh single-scattering albedo for 2str, g = 0) and the
   ! top-of-atmosphere source.
   function gas_optics_ext(this, play, plev, tlay, gas_desc, optical_props, toa_src, col_dry, neural_nets) &
       result(error_msg)
@@ -353,9 +383,11 @@ contains
     type(rrtmgp_network_type), dimension(2), intent(in), optional :: neural_nets
     character(len=128) :: error_msg
     integer :: ncol, nlay, ngpt, ninputs, icol
-    type(c_ptr) :: d_play, d_plev, d_tlay, d_coldry, d_x, d_tau, d_ssa, d_g
-    type(c_ptr) :: nets(2)
-    character(len=128) :: e
+    integer(c_long_long) :: nl, nv, ng
+    type(c_ptr) :: d_play, d_plev, d_tlay, d_tau, d_ssa, d_h2o, d_x, d_cd
+    type(c_ptr) :: nets(2), gas_ptr(MAX_INPUTS)
+    integer(c_int) :: gas_nd(MAX_INPUTS)
+    logical :: h2o_tmp
 
     ncol = size(play, dim=2)
     nlay = size(play, dim=1)
@@ -371,43 +403,51 @@ contains
       error_msg = "gas_optics(): optical properties inconsistently sized"
     if (.not. this%source_is_external()) error_msg = "gas_optics(): this k-distribution has no external source"
     if (error_msg /= '') return
+    if (any(shape(toa_src) /= [ngpt, ncol])) then
+      error_msg = "gas_optics(): array toa_src has wrong size"; return
+    end if
     if (.not. present(neural_nets)) then
       error_msg = "gas_optics(): the lookup-table branch is not available (k-distribution files missing); " // &
                   "pass neural_nets"
       return
     end if
     ninputs = size(neural_nets(1)%layers(1)%w_transposed, 2)
-    error_msg = stage_inputs(nlay, ncol, play, plev, tlay, gas_desc, col_dry, neural_nets(1), &
-                             d_play, d_plev, d_tlay, d_coldry, d_x)
-    if (error_msg == '') then
-      nets(1) = neural_nets(1)%handle
-      nets(2) = neural_nets(2)%handle
-      d_tau = dev_alloc(ngpt * nlay * ncol)
-      d_ssa = c_null_ptr; d_g = c_null_ptr
-      select type (optical_props)
-      type is (ty_optical_props_2str)
-        d_ssa = dev_alloc(ngpt * nlay * ncol)
-        d_g = dev_alloc(ngpt * nlay * ncol)
-      end select
-      error_msg = rrtmgpnn_check(c_rrtmgpnn_predict_nn_sw(rrtmgpnn_ctx(), ncol, nlay, ngpt, ninputs, d_x, d_coldry, &
-                                                          nets, d_tau, d_ssa, d_g), "predict_nn_sw")
-      e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "gas_optics")
-      if (error_msg == '') error_msg = e
-      if (error_msg == '') then
-        call dev_download(optical_props%tau, d_tau, ngpt * nlay * ncol)
-        select type (optical_props)
-        type is (ty_optical_props_2str)
-          call dev_download(optical_props%ssa, d_ssa, ngpt * nlay * ncol)
-          call dev_download(optical_props%g, d_g, ngpt * nlay * ncol)
-        end select
-      end if
-      call dev_free(d_tau); call dev_free(d_ssa); call dev_free(d_g)
-    end if
-    call dev_free(d_play); call dev_free(d_plev); call dev_free(d_tlay); call dev_free(d_coldry); call dev_free(d_x)
+    error_msg = gas_inputs(nlay, ncol, gas_desc, neural_nets(1), gas_ptr, gas_nd, d_h2o, h2o_tmp)
     if (error_msg /= '') return
-    if (any(shape(toa_src) /= [ngpt, ncol])) then
-      error_msg = "gas_optics(): array toa_src has wrong size"; return
+    nl = int(nlay, c_long_long) * ncol
+    nv = int(nlay + 1, c_long_long) * ncol
+    ng = int(ngpt, c_long_long) * nlay * ncol
+    d_play = dev_stage(play, nl)
+    d_plev = dev_stage(plev, nv)
+    d_tlay = dev_stage(tlay, nl)
+    nets(1) = neural_nets(1)%handle
+    nets(2) = neural_nets(2)%handle
+    d_tau = dev_present(optical_props%tau, ng, PRESENT_WRITE)
+    d_ssa = c_null_ptr
+    select type (optical_props)
+    type is (ty_optical_props_2str)
+      d_ssa = dev_present(optical_props%ssa, ng, PRESENT_WRITE)
+    end select
+    if (present(col_dry)) then
+      error_msg = staged_nn_inputs(nlay, ncol, neural_nets(1), d_play, d_tlay, gas_ptr, gas_nd, col_dry, d_x, d_cd)
+      if (error_msg == '') &
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_predict_nn_sw(rrtmgpnn_ctx(), ncol, nlay, ngpt, ninputs, d_x, d_cd, &
+                                                            nets, d_tau, d_ssa, c_null_ptr), "predict_nn_sw")
+      call dev_release(d_x)
+      call dev_release(d_cd)
+    else
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_gas_optics_sw_nn(rrtmgpnn_ctx(), ncol, nlay, ngpt, ninputs, d_play, d_tlay, &
+                                 d_plev, d_h2o, gas_ptr, gas_nd, nets, d_tau, d_ssa, c_null_ptr), "gas_optics_sw_nn")
     end if
+    call dev_release(d_play)
+    call dev_release(d_plev)
+    call dev_release(d_tlay)
+    if (h2o_tmp) call dev_release(d_h2o)
+    if (error_msg /= '') return
+    select type (optical_props)
+    type is (ty_optical_props_2str)
+      optical_props%g_zero = .true.  ! g = 0 (:560-567), left implicit on the device
+    end select
     do icol = 1, ncol
       toa_src(:, icol) = this%solar_source(:)
     end do

@@ -16,8 +16,8 @@ contains
     real(wp), dimension(:,:), intent(out) :: heating_rate             ! (nlay, ncol) [K/s]
     character(len=128) :: error_msg
     integer :: ncol, nlay
+    integer(c_long_long) :: nv
     type(c_ptr) :: d_up, d_dn, d_p, d_hr
-    character(len=128) :: e
 
     error_msg = ""
     nlay = size(flux_up, 1) - 1
@@ -31,15 +31,15 @@ contains
     if (any(shape(heating_rate) /= [nlay, ncol])) then
       error_msg = "heating_rate: heating_rate array inconsistently sized."; return
     end if
-    d_up = dev_upload(flux_up, (nlay + 1) * ncol)
-    d_dn = dev_upload(flux_dn, (nlay + 1) * ncol)
-    d_p  = dev_upload(plev, (nlay + 1) * ncol)
-    d_hr = dev_alloc(nlay * ncol)
+    nv = int(nlay + 1, c_long_long) * ncol
+    d_up = dev_stage(flux_up, nv)
+    d_dn = dev_stage(flux_dn, nv)
+    d_p  = dev_stage(plev, nv)
+    d_hr = dev_scratch(int(nlay, c_long_long) * ncol)
     error_msg = rrtmgpnn_check(c_rrtmgpnn_compute_heating_rate(rrtmgpnn_ctx(), ncol, nlay, d_up, d_dn, d_p, d_hr), &
                                "heating_rate")
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "heating_rate")
-    if (error_msg == '') error_msg = e
-    if (error_msg == '') call dev_download(heating_rate, d_hr, nlay * ncol)
-    call dev_free(d_up); call dev_free(d_dn); call dev_free(d_p); call dev_free(d_hr)
+    if (error_msg == '') call dev_copy_out(heating_rate, d_hr, int(nlay, c_long_long) * ncol)
+    call rrtmgpnn_sync(error_msg, "heating_rate")
+    call dev_release(d_up); call dev_release(d_dn); call dev_release(d_p); call dev_release(d_hr)
   end function compute_heating_rate
 end module mo_heating_rates

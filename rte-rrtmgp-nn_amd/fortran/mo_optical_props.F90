@@ -1,6 +1,14 @@
 ! mo_optical_props -- drop-in for rte/mo_optical_props.F90: spectral discretisation and the
 ! (ngpt, nlay, ncol) optical-property arrays, g-point fastest (the fork's layout, :99,179-180).
 ! increment (:882-1023) and delta_scale (:565-604) run in the HIP kernels behind the C ABI.
+!
+! Device residency, as in the reference's OpenACC build (the arrays are created on the device by the constructors,
+! examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:325-327): every array has a device copy in the calling thread's
+! context (mo_rrtmgpnn_c: dev_present).  Arrays the library produces (gas_optics, cloud_optics, increment,
+! delta_scale) stay on the device until a consumer reads them there (rte_lw, rte_sw, increment); the host copy is
+! refreshed only by update_host() (`!$acc update host`).  Arrays the caller fills on the host are uploaded when a
+! kernel first reads them; after host writes to an array the library had produced, call update_device()
+! (`!$acc update device`).
 module mo_optical_props
   use, intrinsic :: iso_c_binding
   use mo_rte_kind, only: wp
@@ -34,6 +42,9 @@ module mo_optical_props
     procedure, public :: get_ncol
     procedure, public :: get_nlay
     procedure, public :: increment
+    procedure, public :: update_host
+    procedure, public :: update_device
+    final :: final_arry
   end type ty_optical_props_arry
 
   type, extends(ty_optical_props_arry), public :: ty_optical_props_1scl
@@ -48,6 +59,9 @@ module mo_optical_props
 
   type, extends(ty_optical_props_arry), public :: ty_optical_props_2str
     real(wp), dimension(:,:,:), allocatable :: ssa, g
+    ! g is identically zero and its device copy was never written (gas_optics' NN shortwave, which sets g = 0,
+    ! mo_gas_optics_rrtmgp.F90:560-567): rte_sw passes no g array; other device consumers fill it first
+    logical :: g_zero = .false.
   contains
     procedure, private :: alloc_only_2str
     procedure, private :: init_and_alloc_2str
@@ -56,7 +70,9 @@ module mo_optical_props
     procedure, public  :: finalize => finalize_2str
     procedure, public  :: delta_scale => delta_scale_2str
     procedure, public  :: validate => validate_2stream
+    final :: final_2str
   end type ty_optical_props_2str
+  public :: dev_g, dev_g_read
 
 contains
 
@@ -193,7 +209,7 @@ contains
     if (.not. this%is_initialized()) then
       err_message = "optical_props%alloc: spectral discretization hasn't been provided"; return
     end if
-    if (allocated(this%tau)) deallocate(this%tau)
+    call drop_arrays(this)
     allocate(this%tau(this%get_ngpt(), nlay, ncol))
   end function alloc_only_1scl
 
@@ -223,7 +239,7 @@ contains
 
   subroutine finalize_1scl(this)
     class(ty_optical_props_1scl), intent(inout) :: this
-    if (allocated(this%tau)) deallocate(this%tau)
+    call drop_arrays(this)
     if (allocated(this%band2gpt)) deallocate(this%band2gpt)
     if (allocated(this%band_lims_wvn)) deallocate(this%band_lims_wvn)
   end subroutine finalize_1scl
@@ -239,9 +255,7 @@ contains
     if (.not. this%is_initialized()) then
       err_message = "optical_props%alloc: spectral discretization hasn't been provided"; return
     end if
-    if (allocated(this%tau)) deallocate(this%tau)
-    if (allocated(this%ssa)) deallocate(this%ssa)
-    if (allocated(this%g)) deallocate(this%g)
+    call drop_arrays(this)
     allocate(this%tau(this%get_ngpt(), nlay, ncol), this%ssa(this%get_ngpt(), nlay, ncol), &
              this%g(this%get_ngpt(), nlay, ncol))
   end function alloc_only_2str
@@ -272,23 +286,21 @@ contains
 
   subroutine finalize_2str(this)
     class(ty_optical_props_2str), intent(inout) :: this
-    if (allocated(this%tau)) deallocate(this%tau)
-    if (allocated(this%ssa)) deallocate(this%ssa)
-    if (allocated(this%g)) deallocate(this%g)
+    call drop_arrays(this)
     if (allocated(this%band2gpt)) deallocate(this%band2gpt)
     if (allocated(this%band_lims_wvn)) deallocate(this%band_lims_wvn)
   end subroutine finalize_2str
 
   ! op_in%increment(op_io) (rte/mo_optical_props.F90:882-1023): add op_in to op_io, at the same g-point
-  ! resolution or, when op_in is defined by band, by band into op_io's g-points.
+  ! resolution or, when op_in is defined by band, by band into op_io's g-points.  On the device copies.
   function increment(op_in, op_io) result(err_message)
     class(ty_optical_props_arry), intent(in)    :: op_in
     class(ty_optical_props_arry), intent(inout) :: op_io
     character(len=128) :: err_message
-    integer :: ncol, nlay, ngpt, n_io, n_in
-    logical :: same
+    integer :: ncol, nlay, ngpt
+    integer(c_long_long) :: n_io, n_in
+    logical :: same, g2_tmp
     type(c_ptr) :: t1, s1, g1, t2, s2, g2
-    character(len=128) :: e
 
     err_message = ""
     if (.not. op_in%bands_are_equal(op_io)) then
@@ -305,20 +317,27 @@ contains
       err_message = "ty_optical_props%increment: optical properties objects have incompatible g-point structures"
       return
     end if
-    n_io = size(op_io%tau)
-    n_in = size(op_in%tau)
+    n_io = size(op_io%tau, kind=c_long_long)
+    n_in = size(op_in%tau, kind=c_long_long)
     s1 = c_null_ptr; g1 = c_null_ptr; s2 = c_null_ptr; g2 = c_null_ptr
-    t1 = dev_upload(op_io%tau, n_io)
-    select type (op_io)
-    class is (ty_optical_props_2str)
-      s1 = dev_upload(op_io%ssa, n_io)
-      g1 = dev_upload(op_io%g, n_io)
-    end select
-    t2 = dev_upload(op_in%tau, n_in)
+    g2_tmp = .false.
+    t2 = dev_present(op_in%tau, n_in, PRESENT_READ)
     select type (op_in)
     class is (ty_optical_props_2str)
-      s2 = dev_upload(op_in%ssa, n_in)
-      g2 = dev_upload(op_in%g, n_in)
+      s2 = dev_present(op_in%ssa, n_in, PRESENT_READ)
+      if (op_in%g_zero) then  ! op_in is intent(in): a zero-filled scratch copy stands in for its g
+        g2 = dev_scratch(n_in)
+        call dev_zero(g2, n_in)
+        g2_tmp = .true.
+      else
+        g2 = dev_present(op_in%g, n_in, PRESENT_READ)
+      end if
+    end select
+    t1 = dev_present(op_io%tau, n_io, ior(PRESENT_READ, PRESENT_WRITE))
+    select type (op_io)
+    class is (ty_optical_props_2str)
+      s1 = dev_present(op_io%ssa, n_io, ior(PRESENT_READ, PRESENT_WRITE))
+      g1 = dev_g(op_io)
     end select
     if (same) then
       err_message = rrtmgpnn_check(c_rrtmgpnn_increment(rrtmgpnn_ctx(), ncol, nlay, ngpt, t1, s1, g1, t2, s2, g2), &
@@ -327,33 +346,145 @@ contains
       err_message = rrtmgpnn_check(c_rrtmgpnn_increment_bybnd(rrtmgpnn_ctx(), ncol, nlay, ngpt, op_io%get_nband(), &
                                    op_io%band2gpt, t1, s1, g1, t2, s2, g2), "ty_optical_props%increment")
     end if
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "ty_optical_props%increment")
-    if (err_message == '') err_message = e
-    if (err_message == '') then
-      call dev_download(op_io%tau, t1, n_io)
-      select type (op_io)
-      class is (ty_optical_props_2str)
-        call dev_download(op_io%ssa, s1, n_io)
-        call dev_download(op_io%g, g1, n_io)
-      end select
-    end if
-    call dev_free(t1); call dev_free(s1); call dev_free(g1)
-    call dev_free(t2); call dev_free(s2); call dev_free(g2)
+    if (g2_tmp) call dev_release(g2)
   end function increment
 
-  ! validate_2stream (:635-671)
+  ! The device copy of a two-stream g for a kernel that reads and writes it: an identically zero g (g_zero) is
+  ! filled on the device first.
+  function dev_g(op) result(d)
+    class(ty_optical_props_2str), intent(inout) :: op
+    type(c_ptr) :: d
+    integer(c_long_long) :: n
+    n = size(op%g, kind=c_long_long)
+    if (op%g_zero) then
+      d = dev_present(op%g, n, PRESENT_WRITE)
+      call dev_zero(d, n)
+      op%g_zero = .false.
+    else
+      d = dev_present(op%g, n, ior(PRESENT_READ, PRESENT_WRITE))
+    end if
+  end function dev_g
+
+  ! The device copy of a two-stream g for a kernel that only reads it; for an identically zero g (g_zero) a
+  ! zero-filled scratch buffer the caller releases (tmp), leaving op untouched.
+  function dev_g_read(op, tmp) result(d)
+    class(ty_optical_props_2str), intent(in) :: op
+    logical, intent(out) :: tmp
+    type(c_ptr) :: d
+    integer(c_long_long) :: n
+    n = size(op%g, kind=c_long_long)
+    tmp = op%g_zero
+    if (tmp) then
+      d = dev_scratch(n)
+      call dev_zero(d, n)
+    else
+      d = dev_present(op%g, n, PRESENT_READ)
+    end if
+  end function dev_g_read
+
+  ! `!$acc update host`: refresh the host arrays from their device copies
+  subroutine update_host(this)
+    class(ty_optical_props_arry), intent(inout) :: this
+    if (allocated(this%tau)) call dev_update_host(this%tau)
+    select type (this)
+    class is (ty_optical_props_2str)
+      if (allocated(this%ssa)) call dev_update_host(this%ssa)
+      if (this%g_zero) then
+        this%g = 0._wp
+        this%g_zero = .false.
+        call dev_delete(this%g)
+      else if (allocated(this%g)) then
+        call dev_update_host(this%g)
+      end if
+    end select
+  end subroutine update_host
+
+  ! `!$acc update device`: the host arrays were written; kernels read them from the host copies next
+  subroutine update_device(this)
+    class(ty_optical_props_arry), intent(inout) :: this
+    if (allocated(this%tau)) call dev_update_device(this%tau)
+    select type (this)
+    class is (ty_optical_props_2str)
+      if (allocated(this%ssa)) call dev_update_device(this%ssa)
+      if (allocated(this%g)) call dev_update_device(this%g)
+      this%g_zero = .false.
+    end select
+  end subroutine update_device
+
+  ! drop the device copies of the arrays and deallocate them
+  subroutine drop_arrays(this)
+    class(ty_optical_props_arry), intent(inout) :: this
+    if (allocated(this%tau)) then
+      call dev_delete(this%tau)
+      deallocate(this%tau)
+    end if
+    select type (this)
+    class is (ty_optical_props_2str)
+      if (allocated(this%ssa)) then
+        call dev_delete(this%ssa)
+        deallocate(this%ssa)
+      end if
+      if (allocated(this%g)) then
+        call dev_delete(this%g)
+        deallocate(this%g)
+      end if
+      this%g_zero = .false.
+    end select
+  end subroutine drop_arrays
+
+  ! finalizers: an object going out of scope (or a private copy of one) drops its device copies, so a later
+  ! array at the same address never finds them
+  subroutine final_arry(this)
+    type(ty_optical_props_arry), intent(inout) :: this
+    if (allocated(this%tau)) call dev_delete(this%tau)
+  end subroutine final_arry
+
+  subroutine final_2str(this)
+    type(ty_optical_props_2str), intent(inout) :: this
+    if (allocated(this%ssa)) call dev_delete(this%ssa)
+    if (allocated(this%g)) call dev_delete(this%g)
+  end subroutine final_2str
+
+  ! validate_2stream (:635-671), on the current values (a device-newer array is checked from a copy of its device
+  ! data; the host arrays are left as they are)
   function validate_2stream(this) result(err_message)
     class(ty_optical_props_2str), intent(in) :: this
     character(len=128) :: err_message
+    real(wp), allocatable :: tau(:,:,:), ssa(:,:,:), g(:,:,:)
     err_message = ''
     if (.not. all([allocated(this%tau), allocated(this%ssa), allocated(this%g)])) then
       err_message = "validate: arrays not allocated/initialized"; return
     end if
-    if (any(shape(this%ssa) /= shape(this%tau)) .or. any(shape(this%g) /= shape(this%tau))) &
-      err_message = "validate: arrays not sized consistently"
-    if (any(this%tau < 0._wp)) err_message = "validate: tau values out of range"
-    if (any(this%ssa < 0._wp .or. this%ssa > 1.0001_wp)) err_message = "validate: ssa values out of range"
-    if (any(this%g < -1._wp .or. this%g > 1._wp)) err_message = "validate: g values out of range"
+    if (any(shape(this%ssa) /= shape(this%tau)) .or. any(shape(this%g) /= shape(this%tau))) then
+      err_message = "validate: arrays not sized consistently"; return
+    end if
+    call current(this%tau, tau)
+    call current(this%ssa, ssa)
+    if (this%g_zero) then
+      allocate(g(size(this%g, 1), size(this%g, 2), size(this%g, 3)))
+      g = 0._wp
+    else
+      call current(this%g, g)
+    end if
+    if (any(tau < 0._wp)) err_message = "validate: tau values out of range"
+    if (any(ssa < 0._wp .or. ssa > 1.0001_wp)) err_message = "validate: ssa values out of range"
+    if (any(g < -1._wp .or. g > 1._wp)) err_message = "validate: g values out of range"
+  contains
+    subroutine current(a, c)
+      real(wp), intent(in) :: a(:,:,:)
+      real(wp), allocatable, intent(out) :: c(:,:,:)
+      character(len=128) :: e
+      integer(c_long_long) :: n
+      allocate(c(size(a, 1), size(a, 2), size(a, 3)))
+      if (.not. rrtmgpnn_has_context()) then
+        c = a
+        return
+      end if
+      n = size(a, kind=c_long_long)
+      call dev_copy_out(c, dev_present(a, n, PRESENT_READ), n)
+      e = ''
+      call rrtmgpnn_sync(e, "validate")
+    end subroutine current
   end function validate_2stream
 
   ! delta_scale_1scl (:565-574): absorption optical depth needs no scaling
@@ -364,16 +495,15 @@ contains
     err_message = ''
   end function delta_scale_1scl
 
-  ! delta_scale_2str (:576-604): forward-scattering fraction `for`, g**2 if absent
+  ! delta_scale_2str (:576-604): forward-scattering fraction `for`, g**2 if absent; on the device copies
   function delta_scale_2str(this, for) result(err_message)
     class(ty_optical_props_2str), intent(inout) :: this
     real(wp), dimension(:,:,:), optional, intent(in) :: for
     character(len=128) :: err_message
-    integer :: n
+    integer(c_long_long) :: n
     type(c_ptr) :: dt, ds, dg, df
-    character(len=128) :: e
     err_message = ''
-    n = size(this%tau)
+    n = size(this%tau, kind=c_long_long)
     df = c_null_ptr
     if (present(for)) then
       if (any(shape(for) /= shape(this%tau))) then
@@ -382,20 +512,12 @@ contains
       if (any(for < 0._wp .or. for > 1._wp)) then
         err_message = "delta_scale: values of 'for' out of bounds [0,1]"; return
       end if
-      df = dev_upload(for, n)
+      df = dev_stage(for, n)
     end if
-    dt = dev_upload(this%tau, n)
-    ds = dev_upload(this%ssa, n)
-    dg = dev_upload(this%g, n)
-    err_message = rrtmgpnn_check(c_rrtmgpnn_delta_scale_2str(rrtmgpnn_ctx(), int(n, c_long_long), dt, ds, dg, df), &
-                                 "delta_scale")
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "delta_scale")
-    if (err_message == '') err_message = e
-    if (err_message == '') then
-      call dev_download(this%tau, dt, n)
-      call dev_download(this%ssa, ds, n)
-      call dev_download(this%g, dg, n)
-    end if
-    call dev_free(dt); call dev_free(ds); call dev_free(dg); call dev_free(df)
+    dt = dev_present(this%tau, n, ior(PRESENT_READ, PRESENT_WRITE))
+    ds = dev_present(this%ssa, n, ior(PRESENT_READ, PRESENT_WRITE))
+    dg = dev_g(this)
+    err_message = rrtmgpnn_check(c_rrtmgpnn_delta_scale_2str(rrtmgpnn_ctx(), n, dt, ds, dg, df), "delta_scale")
+    call dev_release(df)
   end function delta_scale_2str
 end module mo_optical_props

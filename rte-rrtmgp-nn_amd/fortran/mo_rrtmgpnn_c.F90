@@ -7,8 +7,13 @@ module mo_rrtmgpnn_c
   use, intrinsic :: iso_c_binding
   implicit none
   private
-  public :: rrtmgpnn_ctx, rrtmgpnn_check, rrtmgpnn_error_message, dev_alloc, dev_free, h2d, d2h, &
-            rrtmgpnn_set_context, dev_upload, dev_download, dev_upload_int
+  public :: rrtmgpnn_ctx, rrtmgpnn_check, rrtmgpnn_error_message, rrtmgpnn_set_context, rrtmgpnn_sync, &
+            rrtmgpnn_has_context
+  ! the context's device data environment (include/rrtmgpnn.h, "Device data environment")
+  public :: PRESENT_READ, PRESENT_WRITE, dev_present, dev_update_host, dev_update_device, dev_delete, dev_stage, &
+            dev_scratch, dev_release, dev_copy_out, dev_copy_in, dev_copy_dd, dev_zero
+  public :: c_rrtmgpnn_gas_optics_lw_nn, c_rrtmgpnn_gas_optics_sw_nn, c_rrtmgpnn_lw_solver_noscat_planck, &
+            c_rrtmgpnn_sw_solver_noscat
   public :: c_rrtmgpnn_compute_heating_rate
   public :: c_rrtmgpnn_network_load, c_rrtmgpnn_compute_nn_inputs, c_rrtmgpnn_get_col_dry, &
             c_rrtmgpnn_interpolate_tlev, c_rrtmgpnn_predict_nn_lw, c_rrtmgpnn_predict_nn_sw, &
@@ -22,6 +27,7 @@ module mo_rrtmgpnn_c
 
   type(c_ptr), save :: ctx_ = c_null_ptr
   !$omp threadprivate(ctx_)
+  integer(c_int), parameter :: PRESENT_READ = 1, PRESENT_WRITE = 2
 
   interface
     integer(c_int) function c_rrtmgpnn_context_create(device, stream, ctx) bind(C, name="rrtmgpnn_context_create")
@@ -30,32 +36,105 @@ module mo_rrtmgpnn_c
       type(c_ptr), value :: stream
       type(c_ptr), intent(out) :: ctx
     end function
+    integer(c_int) function c_rrtmgpnn_context_create_owned(device, ctx) bind(C, name="rrtmgpnn_context_create_owned")
+      import :: c_int, c_ptr
+      integer(c_int), value :: device
+      type(c_ptr), intent(out) :: ctx
+    end function
+    integer(c_int) function c_rrtmgpnn_present(ctx, host, bytes, mode, dptr) bind(C, name="rrtmgpnn_present")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, host
+      integer(c_long_long), value :: bytes
+      integer(c_int), value :: mode
+      type(c_ptr), intent(out) :: dptr
+    end function
+    integer(c_int) function c_rrtmgpnn_present_update_host(ctx, host) bind(C, name="rrtmgpnn_present_update_host")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, host
+    end function
+    integer(c_int) function c_rrtmgpnn_present_update_device(ctx, host) bind(C, name="rrtmgpnn_present_update_device")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, host
+    end function
+    integer(c_int) function c_rrtmgpnn_present_delete(ctx, host) bind(C, name="rrtmgpnn_present_delete")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, host
+    end function
+    integer(c_int) function c_rrtmgpnn_stage_h2d(ctx, host, bytes, dptr) bind(C, name="rrtmgpnn_stage_h2d")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, host
+      integer(c_long_long), value :: bytes
+      type(c_ptr), intent(out) :: dptr
+    end function
+    integer(c_int) function c_rrtmgpnn_scratch(ctx, bytes, dptr) bind(C, name="rrtmgpnn_scratch")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx
+      integer(c_long_long), value :: bytes
+      type(c_ptr), intent(out) :: dptr
+    end function
+    integer(c_int) function c_rrtmgpnn_release(ctx, dptr) bind(C, name="rrtmgpnn_release")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, dptr
+    end function
+    integer(c_int) function c_rrtmgpnn_copy_d2h(ctx, host, dptr, bytes) bind(C, name="rrtmgpnn_copy_d2h")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, host, dptr
+      integer(c_long_long), value :: bytes
+    end function
+    integer(c_int) function c_rrtmgpnn_copy_h2d(ctx, dptr, host, bytes) bind(C, name="rrtmgpnn_copy_h2d")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, dptr, host
+      integer(c_long_long), value :: bytes
+    end function
+    integer(c_int) function c_rrtmgpnn_copy_d2d(ctx, dst, src, bytes) bind(C, name="rrtmgpnn_copy_d2d")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, dst, src
+      integer(c_long_long), value :: bytes
+    end function
+    integer(c_int) function c_rrtmgpnn_memset_async(ctx, dptr, val, bytes) bind(C, name="rrtmgpnn_memset_async")
+      import :: c_int, c_ptr, c_long_long
+      type(c_ptr), value :: ctx, dptr
+      integer(c_int), value :: val
+      integer(c_long_long), value :: bytes
+    end function
+    integer(c_int) function c_rrtmgpnn_gas_optics_lw_nn(ctx, ncol, nlay, ngpt, ninputs, play, tlay, plev, vmr_h2o, &
+        gas_conc, gas_ndims, nets, nnets, tau, pfrac) bind(C, name="rrtmgpnn_gas_optics_lw_nn")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, play, tlay, plev, vmr_h2o, tau, pfrac
+      integer(c_int), value :: ncol, nlay, ngpt, ninputs, nnets
+      type(c_ptr), dimension(*), intent(in) :: gas_conc, nets
+      integer(c_int), dimension(*), intent(in) :: gas_ndims
+    end function
+    integer(c_int) function c_rrtmgpnn_gas_optics_sw_nn(ctx, ncol, nlay, ngpt, ninputs, play, tlay, plev, vmr_h2o, &
+        gas_conc, gas_ndims, nets, tau, ssa, g) bind(C, name="rrtmgpnn_gas_optics_sw_nn")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, play, tlay, plev, vmr_h2o, tau, ssa, g
+      integer(c_int), value :: ncol, nlay, ngpt, ninputs
+      type(c_ptr), dimension(*), intent(in) :: gas_conc, nets
+      integer(c_int), dimension(*), intent(in) :: gas_ndims
+    end function
+    integer(c_int) function c_rrtmgpnn_lw_solver_noscat_planck(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, &
+        inc_flux, tau, pfrac, nbnd, nPlanckTemp, tlay, tlev, tsfc, sfc_lay, band_lims_gpt, temp_ref_min, &
+        totplnk_delta, totplnk, emis_by_band, sfc_emis, flux_up, flux_dn) bind(C, name="rrtmgpnn_lw_solver_noscat_planck")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx, inc_flux, tau, pfrac, tlay, tlev, tsfc, totplnk, sfc_emis, flux_up, flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus, nbnd, nPlanckTemp, sfc_lay, emis_by_band
+      real(c_float), dimension(*), intent(in) :: Ds, weights
+      integer(c_int), dimension(*), intent(in) :: band_lims_gpt
+      real(c_float), value :: temp_ref_min, totplnk_delta
+    end function
+    integer(c_int) function c_rrtmgpnn_sw_solver_noscat(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, mu0, flux_dir) &
+        bind(C, name="rrtmgpnn_sw_solver_noscat")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, inc_flux, tau, mu0, flux_dir
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1
+    end function
     integer(c_int) function c_rrtmgpnn_context_synchronize(ctx) bind(C, name="rrtmgpnn_context_synchronize")
       import :: c_int, c_ptr
       type(c_ptr), value :: ctx
     end function
     type(c_ptr) function c_rrtmgpnn_last_error() bind(C, name="rrtmgpnn_last_error")
       import :: c_ptr
-    end function
-    integer(c_int) function c_rrtmgpnn_malloc(ctx, bytes, dptr) bind(C, name="rrtmgpnn_malloc")
-      import :: c_int, c_ptr, c_long_long
-      type(c_ptr), value :: ctx
-      integer(c_long_long), value :: bytes
-      type(c_ptr), intent(out) :: dptr
-    end function
-    integer(c_int) function c_rrtmgpnn_free(ctx, dptr) bind(C, name="rrtmgpnn_free")
-      import :: c_int, c_ptr
-      type(c_ptr), value :: ctx, dptr
-    end function
-    integer(c_int) function c_rrtmgpnn_memcpy_h2d(ctx, dst, src, bytes) bind(C, name="rrtmgpnn_memcpy_h2d")
-      import :: c_int, c_ptr, c_long_long
-      type(c_ptr), value :: ctx, dst, src
-      integer(c_long_long), value :: bytes
-    end function
-    integer(c_int) function c_rrtmgpnn_memcpy_d2h(ctx, dst, src, bytes) bind(C, name="rrtmgpnn_memcpy_d2h")
-      import :: c_int, c_ptr, c_long_long
-      type(c_ptr), value :: ctx, dst, src
-      integer(c_long_long), value :: bytes
     end function
     integer(c_int) function c_rrtmgpnn_network_load(ctx, path, net) bind(C, name="rrtmgpnn_network_load")
       import :: c_int, c_ptr, c_char
@@ -233,12 +312,13 @@ module mo_rrtmgpnn_c
 
 contains
 
-  ! The calling thread's context (created on device 0, legacy default stream, on first use).
+  ! The calling thread's context (created on device 0 with a stream of its own, on first use): host threads with a
+  ! context each -- OpenMP over blocks, rrtmgp_rfmip_lw.F90:364-367 -- run concurrently on the device.
   function rrtmgpnn_ctx() result(ctx)
     type(c_ptr) :: ctx
     integer(c_int) :: rc
     if (.not. c_associated(ctx_)) then
-      rc = c_rrtmgpnn_context_create(0_c_int, c_null_ptr, ctx_)
+      rc = c_rrtmgpnn_context_create_owned(0_c_int, ctx_)
       if (rc /= 0) then
         write(*, '(a)') "rrtmgpnn: " // trim(rrtmgpnn_error_message())
         error stop 1
@@ -246,6 +326,11 @@ contains
     end if
     ctx = ctx_
   end function rrtmgpnn_ctx
+
+  ! Whether this thread has a context yet (host-only uses of the classes never create one).
+  logical function rrtmgpnn_has_context()
+    rrtmgpnn_has_context = c_associated(ctx_)
+  end function rrtmgpnn_has_context
 
   ! Use an existing context (e.g. one per OpenMP thread / GPU) for this thread's calls.
   subroutine rrtmgpnn_set_context(ctx)
@@ -277,70 +362,105 @@ contains
     if (rc /= 0) error_msg = trim(what) // ": " // trim(rrtmgpnn_error_message())
   end function rrtmgpnn_check
 
-  function dev_alloc(nfloats) result(d)
-    integer, intent(in) :: nfloats
-    type(c_ptr) :: d
-    integer(c_int) :: rc
-    rc = c_rrtmgpnn_malloc(rrtmgpnn_ctx(), int(max(nfloats, 1), c_long_long) * 4_c_long_long, d)
-    if (rc /= 0) then
-      write(*, '(a)') "rrtmgpnn: device allocation failed: " // trim(rrtmgpnn_error_message())
-      error stop 1
-    end if
-  end function dev_alloc
+  ! Wait for the context's stream; keeps an earlier error message.
+  subroutine rrtmgpnn_sync(error_msg, what)
+    character(len=128), intent(inout) :: error_msg
+    character(len=*), intent(in) :: what
+    character(len=128) :: e
+    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), what)
+    if (error_msg == '') error_msg = e
+  end subroutine rrtmgpnn_sync
 
-  subroutine dev_free(d)
-    type(c_ptr), intent(inout) :: d
-    integer(c_int) :: rc
-    if (c_associated(d)) rc = c_rrtmgpnn_free(rrtmgpnn_ctx(), d)
+  ! ---- device data environment.  Sizes are element counts (4-byte reals or integers) in 64-bit integers: a C5
+  ! shard's g-point arrays hold more than 2**31 elements.  h is any contiguous host array (sequence association).
+  ! The device copy of h(1:n) in the context's data environment (mode PRESENT_READ: current data, uploaded when
+  ! the host copy is newer; PRESENT_WRITE: the caller's kernel writes it).
+  function dev_present(h, n, mode) result(d)
+    real(c_float), dimension(*), intent(in), target :: h
+    integer(c_long_long), intent(in) :: n
+    integer(c_int), intent(in) :: mode
+    type(c_ptr) :: d
     d = c_null_ptr
-  end subroutine dev_free
+    if (n <= 0) call fatal("present: non-positive size")
+    if (c_rrtmgpnn_present(rrtmgpnn_ctx(), c_loc(h), 4_c_long_long * n, mode, d) /= 0) call fatal("present")
+  end function dev_present
 
-  subroutine h2d(d, h, nfloats)
-    type(c_ptr), intent(in) :: d, h
-    integer, intent(in) :: nfloats
-    integer(c_int) :: rc
-    if (nfloats <= 0) return
-    rc = c_rrtmgpnn_memcpy_h2d(rrtmgpnn_ctx(), d, h, int(nfloats, c_long_long) * 4_c_long_long)
-    if (rc /= 0) call fatal("host-to-device copy failed")
-  end subroutine h2d
+  ! `!$acc update host`: copy a device-newer array back into h and wait for it.
+  subroutine dev_update_host(h)
+    real(c_float), dimension(*), intent(inout), target :: h
+    if (.not. c_associated(ctx_)) return  ! no context yet: nothing is on the device
+    if (c_rrtmgpnn_present_update_host(ctx_, c_loc(h)) /= 0) call fatal("update host")
+  end subroutine dev_update_host
 
-  subroutine d2h(h, d, nfloats)
-    type(c_ptr), intent(in) :: h, d
-    integer, intent(in) :: nfloats
-    integer(c_int) :: rc
-    if (nfloats <= 0) return
-    rc = c_rrtmgpnn_memcpy_d2h(rrtmgpnn_ctx(), h, d, int(nfloats, c_long_long) * 4_c_long_long)
-    if (rc /= 0) call fatal("device-to-host copy failed")
-  end subroutine d2h
+  ! `!$acc update device`: h changed on the host; it is uploaded when a kernel next reads it.
+  subroutine dev_update_device(h)
+    real(c_float), dimension(*), intent(in), target :: h
+    if (.not. c_associated(ctx_)) return  ! no context yet: nothing is on the device
+    if (c_rrtmgpnn_present_update_device(ctx_, c_loc(h)) /= 0) call fatal("update device")
+  end subroutine dev_update_device
 
-  ! Allocate n floats on the device and copy h(1:n) there (sequence association: any rank).
-  function dev_upload(h, n) result(d)
-    integer, intent(in) :: n
-    real(c_float), dimension(n), intent(in), target :: h
+  ! `!$acc exit data delete`: drop h's device copy (its buffer returns to the pool).
+  subroutine dev_delete(h)
+    real(c_float), dimension(*), intent(in), target :: h
+    if (.not. c_associated(ctx_)) return  ! no context yet: nothing is on the device
+    if (c_rrtmgpnn_present_delete(ctx_, c_loc(h)) /= 0) call fatal("delete")
+  end subroutine dev_delete
+
+  ! A pool buffer holding a copy of h(1:n) (a call's input; release it when the call's kernels are enqueued).
+  function dev_stage(h, n) result(d)
+    real(c_float), dimension(*), intent(in), target :: h
+    integer(c_long_long), intent(in) :: n
     type(c_ptr) :: d
-    d = dev_alloc(n)
-    call h2d(d, c_loc(h), n)
-  end function dev_upload
+    d = c_null_ptr
+    if (n <= 0) call fatal("stage: non-positive size")
+    if (c_rrtmgpnn_stage_h2d(rrtmgpnn_ctx(), c_loc(h), 4_c_long_long * n, d) /= 0) call fatal("host-to-device copy")
+  end function dev_stage
 
-  function dev_upload_int(h, n) result(d)
-    integer, intent(in) :: n
-    integer(c_int), dimension(n), intent(in), target :: h
+  ! An uninitialised pool buffer of n floats.
+  function dev_scratch(n) result(d)
+    integer(c_long_long), intent(in) :: n
     type(c_ptr) :: d
-    d = dev_alloc(n)
-    call h2d(d, c_loc(h), n)
-  end function dev_upload_int
+    d = c_null_ptr
+    if (n <= 0) call fatal("scratch: non-positive size")
+    if (c_rrtmgpnn_scratch(rrtmgpnn_ctx(), 4_c_long_long * n, d) /= 0) call fatal("device allocation")
+  end function dev_scratch
 
-  ! Copy n floats from device d into h(1:n); frees d when `release` is present and true.
-  subroutine dev_download(h, d, n, release)
-    integer, intent(in) :: n
-    real(c_float), dimension(n), intent(inout), target :: h
+  subroutine dev_release(d)
     type(c_ptr), intent(inout) :: d
-    logical, optional, intent(in) :: release
-    call d2h(c_loc(h), d, n)
-    if (present(release)) then
-      if (release) call dev_free(d)
+    if (c_associated(d)) then
+      if (c_rrtmgpnn_release(rrtmgpnn_ctx(), d) /= 0) call fatal("release")
     end if
-  end subroutine dev_download
+    d = c_null_ptr
+  end subroutine dev_release
+
+  ! Enqueue the copy of n floats from d into h (complete after rrtmgpnn_sync).
+  subroutine dev_copy_out(h, d, n)
+    real(c_float), dimension(*), intent(inout), target :: h
+    type(c_ptr), intent(in) :: d
+    integer(c_long_long), intent(in) :: n
+    if (c_rrtmgpnn_copy_d2h(rrtmgpnn_ctx(), c_loc(h), d, 4_c_long_long * n) /= 0) call fatal("device-to-host copy")
+  end subroutine dev_copy_out
+
+  ! Enqueue the copy of h(1:n) into the device buffer d.
+  subroutine dev_copy_in(d, h, n)
+    type(c_ptr), intent(in) :: d
+    real(c_float), dimension(*), intent(in), target :: h
+    integer(c_long_long), intent(in) :: n
+    if (c_rrtmgpnn_copy_h2d(rrtmgpnn_ctx(), d, c_loc(h), 4_c_long_long * n) /= 0) call fatal("host-to-device copy")
+  end subroutine dev_copy_in
+
+  ! Enqueue the copy of n floats from device buffer s into device buffer d.
+  subroutine dev_copy_dd(d, src, n)
+    type(c_ptr), intent(in) :: d, src
+    integer(c_long_long), intent(in) :: n
+    if (c_rrtmgpnn_copy_d2d(rrtmgpnn_ctx(), d, src, 4_c_long_long * n) /= 0) call fatal("device-to-device copy")
+  end subroutine dev_copy_dd
+
+  subroutine dev_zero(d, n)
+    type(c_ptr), intent(in) :: d
+    integer(c_long_long), intent(in) :: n
+    if (c_rrtmgpnn_memset_async(rrtmgpnn_ctx(), d, 0_c_int, 4_c_long_long * n) /= 0) call fatal("memset")
+  end subroutine dev_zero
 
   subroutine fatal(what)
     character(len=*), intent(in) :: what

@@ -1,13 +1,15 @@
 ! mo_rte_lw -- drop-in for rte/mo_rte_lw.F90 (rte_lw, :60-424) in the fork's configuration
 ! (compute_Jac = .false., rte/mo_rte_rrtmgp_config.F90:28).
-! Inputs are staged to the device, expand(sfc_emis) and the solver run as HIP kernels with the broadband
-! reduction fused in, and the broadband fluxes come back into the caller's flux_up / flux_dn / flux_net.
+! The optical properties and sources are read from their device copies (mo_optical_props, mo_source_functions);
+! sources gas_optics left unformed are formed inside the no-scattering solver from the Planck fraction
+! (rrtmgpnn_lw_solver_noscat_planck, emissivity expanded by band in-kernel); the broadband reduction is fused into
+! every solver, and the fluxes come back into the caller's flux_up / flux_dn / flux_net.
 ! 1scl: lw_solver_noscat_GaussQuad; 2str: the rescaled solution (default) or lw_solver_2stream
 ! (use_2stream).  g-point fluxes, lw_Ds and the Jacobians return an error string.
 module mo_rte_lw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,         only: wp
-  use mo_optical_props,    only: ty_optical_props_arry, ty_optical_props_1scl, ty_optical_props_2str
+  use mo_optical_props,    only: ty_optical_props_arry, ty_optical_props_1scl, ty_optical_props_2str, dev_g_read
   use mo_source_functions, only: ty_source_func_lw
   use mo_fluxes,           only: ty_fluxes_flexible
   use mo_rte_rrtmgp_config, only: check_values
@@ -44,11 +46,11 @@ contains
     real(wp), dimension(:,:), target, optional, intent(inout) :: flux_up_Jac, flux_dn_Jac
     character(len=128) :: error_msg
     integer :: ncol, nlay, ngpt, nband, nmus
+    integer(c_long_long) :: ng, nv, nsfc
     integer(c_int), allocatable :: lims(:,:)
-    type(c_ptr) :: d_tau, d_ssa, d_g, d_lay, d_lev, d_sfc, d_emis, d_emis_gpt, d_inc, d_up, d_dn
-    logical :: two_str, use_2s
+    type(c_ptr) :: d_tau, d_ssa, d_g, d_lay, d_lev, d_sfc, d_jac, d_emis, d_emis_gpt, d_inc, d_up, d_dn
+    logical :: two_str, use_2s, src_tmp, g_tmp
     real(wp), allocatable :: up(:,:), dn(:,:)
-    character(len=128) :: e
 
     ncol  = optical_props%get_ncol()
     nlay  = optical_props%get_nlay()
@@ -111,55 +113,81 @@ contains
       if (use_2s .or. check_values) error_msg = optical_props%validate()  ! unconditional for 2-stream (:360)
       if (error_msg /= '') return
       two_str = .true.
-      d_ssa = dev_upload(optical_props%ssa, ngpt * nlay * ncol)
-      d_g   = dev_upload(optical_props%g, ngpt * nlay * ncol)
     class default
       error_msg = "lw_solver(...ty_optical_props_nstr...) not yet implemented"; return
     end select
 
     lims = optical_props%get_band_lims_gpoint()
-    d_tau = dev_upload(optical_props%tau, ngpt * nlay * ncol)
-    d_lay = dev_upload(sources%lay_source, ngpt * nlay * ncol)
-    d_lev = dev_upload(sources%lev_source, ngpt * (nlay + 1) * ncol)
-    d_sfc = dev_upload(sources%sfc_source, ngpt * ncol)
-    d_emis = dev_upload(sfc_emis, nband * ncol)
-    d_emis_gpt = dev_alloc(ngpt * ncol)
+    ng = int(ngpt, c_long_long) * nlay * ncol
+    nv = int(nlay + 1, c_long_long) * ncol
+    nsfc = int(ngpt, c_long_long) * ncol
+    d_tau = dev_present(optical_props%tau, ng, PRESENT_READ)
+    d_emis = dev_stage(sfc_emis, int(nband, c_long_long) * ncol)
     d_inc = c_null_ptr
-    if (present(inc_flux)) d_inc = dev_upload(inc_flux, ngpt * ncol)
-    d_up = dev_alloc((nlay + 1) * ncol)
-    d_dn = dev_alloc((nlay + 1) * ncol)
-    ! sfc_emis expanded to g-points (:429-447), then the solver (:326-387)
-    error_msg = rrtmgpnn_check(c_rrtmgpnn_expand_band_to_gpt(rrtmgpnn_ctx(), nband, ngpt, ncol, lims, d_emis, &
-                                                             d_emis_gpt), "rte_lw: expand")
-    if (error_msg == '') then
-      if (two_str .and. use_2s) then
-        error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                                   merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_ssa, d_g, d_lev, d_emis_gpt, &
-                                   d_sfc, d_up, d_dn), "rte_lw: lw_solver_2stream")
-      else if (two_str) then
-        error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_1rescl(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                                   merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
-                                   gauss_wts(1:nmus, nmus), d_inc, d_tau, d_ssa, d_g, d_lay, d_lev, d_emis_gpt, &
-                                   d_sfc, d_up, d_dn), "rte_lw: lw_solver_noscat (rescaled)")
-      else
-        error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                                   merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
-                                   gauss_wts(1:nmus, nmus), d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, d_up, &
-                                   d_dn), "rte_lw: lw_solver_noscat")
+    if (present(inc_flux)) d_inc = dev_stage(inc_flux, nsfc)
+    d_up = dev_scratch(nv)
+    d_dn = dev_scratch(nv)
+    d_emis_gpt = c_null_ptr
+    if (.not. two_str .and. sources%planck_deferred) then
+      ! lw_solver_noscat_GaussQuad (:326-353) with compute_Planck_source_nn (gas_optics, :398-404) and expand(sfc_emis)
+      ! (:429-447) inside the solver
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                    merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), gauss_wts(1:nmus, nmus), d_inc, &
+                    d_tau, dev_present(sources%lay_source, ng, PRESENT_READ), nband, sources%pk_ntemp, &
+                    dev_present(sources%pk_tlay, size(sources%pk_tlay, kind=c_long_long), PRESENT_READ), &
+                    dev_present(sources%pk_tlev, size(sources%pk_tlev, kind=c_long_long), PRESENT_READ), &
+                    dev_present(sources%pk_tsfc, size(sources%pk_tsfc, kind=c_long_long), PRESENT_READ), &
+                    sources%pk_sfc_lay, lims, sources%pk_tmin, sources%pk_tdelta, sources%pk_totplnk, 1_c_int, d_emis, &
+                    d_up, d_dn), "rte_lw: lw_solver_noscat")
+    else
+      src_tmp = .false.
+      g_tmp = .false.
+      error_msg = sources%device_sources(d_lay, d_lev, d_sfc, d_jac, src_tmp)
+      if (error_msg == '') then
+        d_emis_gpt = dev_scratch(nsfc)
+        ! sfc_emis expanded to g-points (:429-447), then the solver (:326-387)
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_expand_band_to_gpt(rrtmgpnn_ctx(), nband, ngpt, ncol, lims, d_emis, &
+                                                                 d_emis_gpt), "rte_lw: expand")
       end if
+      if (error_msg == '') then
+        select type (optical_props)
+        type is (ty_optical_props_2str)
+          d_ssa = dev_present(optical_props%ssa, ng, PRESENT_READ)
+          d_g = dev_g_read(optical_props, g_tmp)
+        end select
+        if (two_str .and. use_2s) then
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                     merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_ssa, d_g, d_lev, d_emis_gpt, &
+                                     d_sfc, d_up, d_dn), "rte_lw: lw_solver_2stream")
+        else if (two_str) then
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_1rescl(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                     merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
+                                     gauss_wts(1:nmus, nmus), d_inc, d_tau, d_ssa, d_g, d_lay, d_lev, d_emis_gpt, &
+                                     d_sfc, d_up, d_dn), "rte_lw: lw_solver_noscat (rescaled)")
+        else
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                     merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
+                                     gauss_wts(1:nmus, nmus), d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, d_up, &
+                                     d_dn), "rte_lw: lw_solver_noscat")
+        end if
+      end if
+      if (src_tmp) then
+        call dev_release(d_lay); call dev_release(d_lev); call dev_release(d_sfc); call dev_release(d_jac)
+      end if
+      if (g_tmp) call dev_release(d_g)
     end if
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "rte_lw")
-    if (error_msg == '') error_msg = e
+    allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol))
     if (error_msg == '') then
-      allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol))
-      call dev_download(up, d_up, (nlay + 1) * ncol)
-      call dev_download(dn, d_dn, (nlay + 1) * ncol)
+      call dev_copy_out(up, d_up, nv)
+      call dev_copy_out(dn, d_dn, nv)
+    end if
+    call rrtmgpnn_sync(error_msg, "rte_lw")
+    if (error_msg == '') then
       if (associated(fluxes%flux_up)) fluxes%flux_up = up
       if (associated(fluxes%flux_dn)) fluxes%flux_dn = dn
       if (associated(fluxes%flux_net)) fluxes%flux_net = dn - up
     end if
-    call dev_free(d_ssa); call dev_free(d_g)
-    call dev_free(d_tau); call dev_free(d_lay); call dev_free(d_lev); call dev_free(d_sfc)
-    call dev_free(d_emis); call dev_free(d_emis_gpt); call dev_free(d_inc); call dev_free(d_up); call dev_free(d_dn)
+    call dev_release(d_emis); call dev_release(d_emis_gpt); call dev_release(d_inc)
+    call dev_release(d_up); call dev_release(d_dn)
   end function rte_lw
 end module mo_rte_lw

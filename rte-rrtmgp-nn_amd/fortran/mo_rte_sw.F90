@@ -1,7 +1,8 @@
 ! mo_rte_sw -- drop-in for rte/mo_rte_sw.F90 (rte_sw, :48-266; the fork passes surface albedos per
-! g-point).  The two-stream solver (sw_solver_2stream, rte/kernels/mo_rte_solver_kernels.F90:541-692)
-! runs as one HIP kernel per call with the broadband reduction fused in; the no-scattering (1scl)
-! shortwave path and g-point fluxes return an error string.
+! g-point).  The optical properties are read from their device copies (mo_optical_props).  2str: the two-stream
+! solver (sw_solver_2stream, rte/kernels/mo_rte_solver_kernels.F90:541-692) as one HIP kernel with the broadband
+! reduction fused in; 1scl: apply_BC + sw_solver_noscat (:213-222), the direct beam only (flux_dn_dir; flux_up /
+! flux_dn are left as they are, as in the reference).  g-point fluxes return an error string.
 module mo_rte_sw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,      only: wp
@@ -25,9 +26,10 @@ contains
     real(wp), dimension(:,:), optional, contiguous, target, intent(in) :: inc_flux_dif      ! (ngpt, ncol)
     character(len=128) :: error_msg
     integer :: ncol, nlay, ngpt
+    integer(c_long_long) :: ng, nv, nsfc
     type(c_ptr) :: d_tau, d_ssa, d_g, d_mu0, d_inc, d_dif, d_adir, d_adif, d_up, d_dn, d_dir
     real(wp), allocatable :: up(:,:), dn(:,:), dir(:,:)
-    character(len=128) :: e
+    logical :: two_str
 
     ncol = atmos%get_ncol()
     nlay = atmos%get_nlay()
@@ -72,40 +74,62 @@ contains
       error_msg = "rte_sw: sfc_alb_dif out of bounds [0,1]"; return
     end if
 
+    ng = int(ngpt, c_long_long) * nlay * ncol
+    nv = int(nlay + 1, c_long_long) * ncol
+    nsfc = int(ngpt, c_long_long) * ncol
+    d_tau = dev_present(atmos%tau, ng, PRESENT_READ)
+    d_mu0 = dev_stage(mu0, int(ncol, c_long_long))
+    d_inc = dev_stage(inc_flux, nsfc)
+    d_adir = dev_stage(sfc_alb_dir_gpt, nsfc)
+    if (same_array(sfc_alb_dir_gpt, sfc_alb_dif_gpt)) then  ! the drivers pass one array for both
+      d_adif = d_adir
+    else
+      d_adif = dev_stage(sfc_alb_dif_gpt, nsfc)
+    end if
+    d_dif = c_null_ptr
+    if (present(inc_flux_dif)) d_dif = dev_stage(inc_flux_dif, nsfc)
+    d_up = dev_scratch(nv)
+    d_dn = dev_scratch(nv)
+    d_dir = dev_scratch(nv)
+    two_str = .false.
     select type (atmos)
     class is (ty_optical_props_2str)
-      d_tau = dev_upload(atmos%tau, ngpt * nlay * ncol)
-      d_ssa = dev_upload(atmos%ssa, ngpt * nlay * ncol)
-      d_g   = dev_upload(atmos%g, ngpt * nlay * ncol)
+      two_str = .true.
+      d_ssa = dev_present(atmos%ssa, ng, PRESENT_READ)
+      d_g = c_null_ptr  ! NULL: g is identically zero (the solver takes it as a literal 0, same fluxes)
+      if (.not. atmos%g_zero) d_g = dev_present(atmos%g, ng, PRESENT_READ)
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                 merge(1_c_int, 0_c_int, top_at_1), d_inc, d_dif, d_tau, d_ssa, d_g, d_mu0, &
+                                 d_adir, d_adif, d_up, d_dn, d_dir), "rte_sw: sw_solver_2stream")
     class default
-      error_msg = "rte_sw: the no-scattering (1scl) shortwave solver is not implemented (2str only)"; return
+      ! 1scl: apply_BC(inc_flux, mu0) + sw_solver_noscat (:213-222): the direct beam only, no diffuse flux
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                 merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_mu0, d_dir), &
+                                 "rte_sw: sw_solver_noscat")
     end select
-    d_mu0  = dev_upload(mu0, ncol)
-    d_inc  = dev_upload(inc_flux, ngpt * ncol)
-    d_dif  = c_null_ptr
-    if (present(inc_flux_dif)) d_dif = dev_upload(inc_flux_dif, ngpt * ncol)
-    d_adir = dev_upload(sfc_alb_dir_gpt, ngpt * ncol)
-    d_adif = dev_upload(sfc_alb_dif_gpt, ngpt * ncol)
-    d_up  = dev_alloc((nlay + 1) * ncol)
-    d_dn  = dev_alloc((nlay + 1) * ncol)
-    d_dir = dev_alloc((nlay + 1) * ncol)
-    error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                               merge(1_c_int, 0_c_int, top_at_1), d_inc, d_dif, d_tau, d_ssa, d_g, d_mu0, &
-                               d_adir, d_adif, d_up, d_dn, d_dir), "rte_sw: sw_solver_2stream")
-    e = rrtmgpnn_check(c_rrtmgpnn_context_synchronize(rrtmgpnn_ctx()), "rte_sw")
-    if (error_msg == '') error_msg = e
+    allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol), dir(nlay + 1, ncol))
     if (error_msg == '') then
-      allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol), dir(nlay + 1, ncol))
-      call dev_download(up, d_up, (nlay + 1) * ncol)
-      call dev_download(dn, d_dn, (nlay + 1) * ncol)
-      call dev_download(dir, d_dir, (nlay + 1) * ncol)
-      if (associated(fluxes%flux_up))     fluxes%flux_up = up
-      if (associated(fluxes%flux_dn))     fluxes%flux_dn = dn
-      if (associated(fluxes%flux_dn_dir)) fluxes%flux_dn_dir = dir
-      if (associated(fluxes%flux_net))    fluxes%flux_net = dn - up
+      if (two_str) call dev_copy_out(up, d_up, nv)
+      if (two_str) call dev_copy_out(dn, d_dn, nv)
+      call dev_copy_out(dir, d_dir, nv)
     end if
-    call dev_free(d_tau); call dev_free(d_ssa); call dev_free(d_g); call dev_free(d_mu0); call dev_free(d_inc)
-    call dev_free(d_dif); call dev_free(d_adir); call dev_free(d_adif)
-    call dev_free(d_up); call dev_free(d_dn); call dev_free(d_dir)
+    call rrtmgpnn_sync(error_msg, "rte_sw")
+    if (error_msg == '') then
+      if (associated(fluxes%flux_dn_dir)) fluxes%flux_dn_dir = dir
+      if (two_str) then
+        if (associated(fluxes%flux_up))   fluxes%flux_up = up
+        if (associated(fluxes%flux_dn))   fluxes%flux_dn = dn
+        if (associated(fluxes%flux_net))  fluxes%flux_net = dn - up
+      end if
+    end if
+    call dev_release(d_mu0); call dev_release(d_inc); call dev_release(d_dif); call dev_release(d_adir)
+    if (.not. same_array(sfc_alb_dir_gpt, sfc_alb_dif_gpt)) call dev_release(d_adif)
+    call dev_release(d_up); call dev_release(d_dn); call dev_release(d_dir)
   end function rte_sw
+
+  ! whether two dummy arrays are the same actual array (same first element, same shape)
+  logical function same_array(a, b)
+    real(wp), dimension(:,:), intent(in), target :: a, b
+    same_array = c_associated(c_loc(a), c_loc(b)) .and. all(shape(a) == shape(b))
+  end function same_array
 end module mo_rte_sw

@@ -3,10 +3,16 @@
 ! against the drop-in modules only: the same calls a reference user makes (ty_gas_concs%set_vmr,
 ! load_netcdf, gas_optics(..., neural_nets=...), rte_lw, rte_sw) now run on the GPU.
 !
-! usage: rrtmgpnn_rfmip_clear_sky <problem.rbin> <output.rbin> <data_dir> [block_size]
+! As there, the gas concentrations are set per block before the loop (read_and_block_gases_ty) and the blocks run
+! under OpenMP (`!$omp parallel do`, rrtmgp_rfmip_lw.F90:364-367): each thread owns its optical properties and
+! sources, and its own device context and stream (mo_rrtmgpnn_c), so blocks run concurrently on the GPU.
+!
+! usage: rrtmgpnn_rfmip_clear_sky <problem.rbin> <output.rbin> <data_dir> [block_size] [nrepeat]
 !   problem.rbin: play/tlay (ncol,nlay), plev/tlev (ncol,nlay+1), tsfc/sfc_emis/sfc_alb/mu0/tsi/usecol
 !   (ncol), gas_names (ngas,32) + vmr_<gas> (ncol,nlay), top_at_1 and n_gauss_angles (1).
 !   output.rbin:  lw_flux_up/dn, sw_flux_up/dn/dir (ncol,nlay+1), lw_heating_rate (ncol,nlay) [K/s].
+!   nrepeat > 1: the block loop runs nrepeat times; the first is a warm-up, the others are timed together and
+!   reported as "timing: <ms> ms per block loop" (system_clock, as the reference drivers time theirs).
 program rrtmgpnn_rfmip_clear_sky
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -19,6 +25,7 @@ program rrtmgpnn_rfmip_clear_sky
   use mo_rte_sw,             only: rte_sw
   use mo_rrtmgpnn_rbin
   use mo_heating_rates, only: compute_heating_rate
+  use omp_lib
   implicit none
 
   character(len=512) :: problem_file, output_file, data_dir, arg
@@ -27,7 +34,7 @@ program rrtmgpnn_rfmip_clear_sky
   character(len=32), allocatable :: gas_names(:)
   real(wp), allocatable, target :: lw_up(:,:), lw_dn(:,:), sw_up(:,:), sw_dn(:,:), sw_dir(:,:)
   real(wp), allocatable :: sfc_emis_spec(:,:), toa_flux(:,:), sfc_alb_spec(:,:), def_tsi(:), lw_hr(:,:)
-  type(ty_gas_concs) :: gas_concs
+  type(ty_gas_concs), allocatable :: gas_concs(:)
   type(ty_gas_optics_rrtmgp) :: kdist_lw, kdist_sw
   type(rrtmgp_network_type), dimension(2) :: nets_lw, nets_sw
   type(ty_optical_props_1scl) :: op_lw
@@ -36,7 +43,9 @@ program rrtmgpnn_rfmip_clear_sky
   type(ty_fluxes_flexible) :: fluxes
   character(len=128) :: e
   logical :: top_at_1
-  integer :: ncol, nlay, ngas, nmus, block_size, b0, b1, nb, icol, igpt, ig, u
+  integer :: ncol, nlay, ngas, nmus, block_size, b0, b1, nb, icol, igpt, ig, u, nblocks, b, nrepeat, rep
+  integer(8) :: t0, t1, rate
+  real(wp), allocatable :: vmr_all(:,:,:)
 
   if (command_argument_count() < 3) then
     write(*, '(a)') "usage: rrtmgpnn_rfmip_clear_sky <problem.rbin> <output.rbin> <data_dir> [block_size]"
@@ -49,6 +58,11 @@ program rrtmgpnn_rfmip_clear_sky
   if (command_argument_count() >= 4) then
     call get_command_argument(4, arg)
     read(arg, *) block_size
+  end if
+  nrepeat = 1
+  if (command_argument_count() >= 5) then
+    call get_command_argument(5, arg)
+    read(arg, *) nrepeat
   end if
 
   call rbin_real2(problem_file, "play", play, e); call stop_on_err(e)
@@ -82,57 +96,87 @@ program rrtmgpnn_rfmip_clear_sky
   allocate(lw_up(nlay + 1, ncol), lw_dn(nlay + 1, ncol), sw_up(nlay + 1, ncol), sw_dn(nlay + 1, ncol), &
            sw_dir(nlay + 1, ncol))
 
-  do b0 = 1, ncol, block_size
-    b1 = min(ncol, b0 + block_size - 1)
-    nb = b1 - b0 + 1
-    call stop_on_err(gas_concs%init(gas_names))
-    do ig = 1, ngas
-      call rbin_real2(problem_file, "vmr_" // trim(gas_names(ig)), vmr, e); call stop_on_err(e)
-      call stop_on_err(gas_concs%set_vmr(gas_names(ig), vmr(:, b0:b1)))
-    end do
-
-    ! ---- longwave (rrtmgp_rfmip_lw.F90:385-420) ----
-    call stop_on_err(op_lw%alloc_1scl(nb, nlay, kdist_lw))
-    call stop_on_err(sources%alloc(nb, nlay, kdist_lw))
-    allocate(sfc_emis_spec(kdist_lw%get_nband(), nb))
-    do icol = 1, nb
-      sfc_emis_spec(:, icol) = sfc_emis(b0 + icol - 1)
-    end do
-    call stop_on_err(kdist_lw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), tsfc(b0:b1), gas_concs, &
-                                         op_lw, sources, tlev=tlev(:, b0:b1), neural_nets=nets_lw))
-    fluxes%flux_up => lw_up(:, b0:b1)
-    fluxes%flux_dn => lw_dn(:, b0:b1)
-    fluxes%flux_dn_dir => NULL()
-    call stop_on_err(rte_lw(op_lw, top_at_1, sources, sfc_emis_spec, fluxes, n_gauss_angles=nmus))
-    deallocate(sfc_emis_spec)
-
-    ! ---- shortwave (rrtmgp_rfmip_sw.F90:370-470) ----
-    call stop_on_err(op_sw%alloc_2str(nb, nlay, kdist_sw))
-    allocate(toa_flux(kdist_sw%get_ngpt(), nb), sfc_alb_spec(kdist_sw%get_ngpt(), nb), def_tsi(nb))
-    call stop_on_err(kdist_sw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), gas_concs, op_sw, toa_flux, &
-                                         neural_nets=nets_sw))
-    do icol = 1, nb
-      def_tsi(icol) = 0._wp
-      do igpt = 1, kdist_sw%get_ngpt()
-        def_tsi(icol) = def_tsi(icol) + toa_flux(igpt, icol)
-      end do
-      do igpt = 1, kdist_sw%get_ngpt()
-        toa_flux(igpt, icol) = toa_flux(igpt, icol) * tsi(b0 + icol - 1) / def_tsi(icol)
-      end do
-      sfc_alb_spec(:, icol) = sfc_alb(b0 + icol - 1)
-    end do
-    fluxes%flux_up => sw_up(:, b0:b1)
-    fluxes%flux_dn => sw_dn(:, b0:b1)
-    fluxes%flux_dn_dir => sw_dir(:, b0:b1)
-    call stop_on_err(rte_sw(op_sw, top_at_1, mu0(b0:b1), toa_flux, sfc_alb_spec, sfc_alb_spec, fluxes))
-    do icol = 1, nb
-      if (usecol(b0 + icol - 1) == 0._wp) then
-        sw_up(:, b0 + icol - 1) = 0._wp
-        sw_dn(:, b0 + icol - 1) = 0._wp
-      end if
-    end do
-    deallocate(toa_flux, sfc_alb_spec, def_tsi)
+  ! gas concentrations by block, set once (rrtmgp_rfmip_lw.F90:270, read_and_block_gases_ty)
+  nblocks = (ncol + block_size - 1) / block_size
+  allocate(gas_concs(nblocks), vmr_all(nlay, ncol, ngas))
+  do ig = 1, ngas
+    call rbin_real2(problem_file, "vmr_" // trim(gas_names(ig)), vmr, e); call stop_on_err(e)
+    vmr_all(:, :, ig) = vmr
   end do
+  do b = 1, nblocks
+    b0 = (b - 1) * block_size + 1
+    b1 = min(ncol, b0 + block_size - 1)
+    call stop_on_err(gas_concs(b)%init(gas_names))
+    do ig = 1, ngas
+      call stop_on_err(gas_concs(b)%set_vmr(gas_names(ig), vmr_all(:, b0:b1, ig)))
+    end do
+  end do
+
+  call system_clock(count_rate=rate)
+  do rep = 1, nrepeat
+    if (rep == 2) call system_clock(t0)
+    !$omp parallel do schedule(static) default(shared) &
+    !$omp   private(b, b0, b1, nb, icol, igpt, op_lw, op_sw, sources, fluxes, sfc_emis_spec, toa_flux, sfc_alb_spec, def_tsi)
+    do b = 1, nblocks
+      b0 = (b - 1) * block_size + 1
+      b1 = min(ncol, b0 + block_size - 1)
+      nb = b1 - b0 + 1
+
+      ! ---- longwave (rrtmgp_rfmip_lw.F90:385-420) ----
+      call stop_on_err(op_lw%alloc_1scl(nb, nlay, kdist_lw))
+      call stop_on_err(sources%alloc(nb, nlay, kdist_lw))
+      allocate(sfc_emis_spec(kdist_lw%get_nband(), nb))
+      do icol = 1, nb
+        sfc_emis_spec(:, icol) = sfc_emis(b0 + icol - 1)
+      end do
+      call stop_on_err(kdist_lw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), tsfc(b0:b1), gas_concs(b), &
+                                           op_lw, sources, tlev=tlev(:, b0:b1), neural_nets=nets_lw))
+      fluxes%flux_up => lw_up(:, b0:b1)
+      fluxes%flux_dn => lw_dn(:, b0:b1)
+      fluxes%flux_dn_dir => NULL()
+      call stop_on_err(rte_lw(op_lw, top_at_1, sources, sfc_emis_spec, fluxes, n_gauss_angles=nmus))
+      deallocate(sfc_emis_spec)
+
+      ! ---- shortwave (rrtmgp_rfmip_sw.F90:370-470) ----
+      call stop_on_err(op_sw%alloc_2str(nb, nlay, kdist_sw))
+      allocate(toa_flux(kdist_sw%get_ngpt(), nb), sfc_alb_spec(kdist_sw%get_ngpt(), nb), def_tsi(nb))
+      call stop_on_err(kdist_sw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), gas_concs(b), op_sw, &
+                                           toa_flux, neural_nets=nets_sw))
+      do icol = 1, nb
+        def_tsi(icol) = 0._wp
+        do igpt = 1, kdist_sw%get_ngpt()
+          def_tsi(icol) = def_tsi(icol) + toa_flux(igpt, icol)
+        end do
+        do igpt = 1, kdist_sw%get_ngpt()
+          toa_flux(igpt, icol) = toa_flux(igpt, icol) * tsi(b0 + icol - 1) / def_tsi(icol)
+        end do
+        sfc_alb_spec(:, icol) = sfc_alb(b0 + icol - 1)
+      end do
+      fluxes%flux_up => sw_up(:, b0:b1)
+      fluxes%flux_dn => sw_dn(:, b0:b1)
+      fluxes%flux_dn_dir => sw_dir(:, b0:b1)
+      call stop_on_err(rte_sw(op_sw, top_at_1, mu0(b0:b1), toa_flux, sfc_alb_spec, sfc_alb_spec, fluxes))
+      do icol = 1, nb
+        if (usecol(b0 + icol - 1) == 0._wp) then
+          sw_up(:, b0 + icol - 1) = 0._wp
+          sw_dn(:, b0 + icol - 1) = 0._wp
+        end if
+      end do
+      deallocate(toa_flux, sfc_alb_spec, def_tsi)
+      ! the thread's private objects give their device copies back to the context's pool (`!$acc exit data`): the
+      ! compiler does not finalise OpenMP private copies
+      call op_lw%finalize()
+      call sources%finalize()
+      call op_sw%finalize()
+    end do
+    !$omp end parallel do
+  end do
+  if (nrepeat > 1) then
+    call system_clock(t1)
+    write(*, '(a,f12.4,a,i0,a,i0,a,i0,a)') "rrtmgpnn_rfmip_clear_sky: timing: ", &
+      1000.0d0 * real(t1 - t0, 8) / real(rate, 8) / real(nrepeat - 1, 8), " ms per block loop (", nblocks, &
+      " blocks of ", block_size, " columns, ", omp_get_max_threads(), " threads)"
+  end if
 
   ! heating rates of the longwave fluxes (extensions/mo_heating_rates), K/s
   allocate(lw_hr(nlay, ncol))

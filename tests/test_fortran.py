@@ -53,8 +53,11 @@ def test_fortran_rbin_roundtrip_and_gas_concs(tmp_path, rfmip):
     from rrtmgpnn import rbin
     _make()
     exe = str(tmp_path / "rbin_roundtrip")
+    lib = os.path.join(ROOT, "rte-rrtmgp-nn_amd")
     subprocess.run([FC, "-O1", "-I", FBUILD, os.path.join(ROOT, "tests", "fortran", "rbin_roundtrip.F90"), "-o", exe,
-                    os.path.join(FBUILD, "librrtmgpnn_fortran.a")], check=True, capture_output=True)
+                    os.path.join(FBUILD, "librrtmgpnn_fortran.a"), "-fopenmp", "-L" + lib, "-lrrtmgpnn",
+                    "-Wl,-rpath," + lib],
+                   check=True, capture_output=True)
     prob = subset(rfmip, np.arange(0, 1800, 97))
     fin, fout = str(tmp_path / "in.rbin"), str(tmp_path / "out.rbin")
     write_problem(prob, fin)
@@ -67,16 +70,22 @@ def test_fortran_rbin_roundtrip_and_gas_concs(tmp_path, rfmip):
 
 @pytest.mark.gpu
 @needs_fc
-def test_fortran_rfmip_driver_matches_oracle(tmp_path, orc, rfmip):
-    """The reference-shaped host program, blocked (64 columns, ragged last block), vs the oracle."""
+@pytest.mark.parametrize("threads,repeat", [(1, 1), (4, 3)])
+def test_fortran_rfmip_driver_matches_oracle(tmp_path, orc, rfmip, threads, repeat):
+    """The reference-shaped host program, blocked (64 columns, ragged last block), vs the oracle.  threads > 1: the
+    blocks run concurrently under OpenMP, each thread with its own device context and stream; repeat > 1: the block
+    loop runs again over the device-resident gas concentrations (cached device copies) and the timing line appears."""
     from rrtmgpnn import data, rbin
     if not os.path.exists(EXE):
         _make()
     prob = subset(rfmip, np.arange(0, 1800, 9))
     fin, fout = str(tmp_path / "prob.rbin"), str(tmp_path / "flux.rbin")
     write_problem(prob, fin)
-    r = subprocess.run(["timeout", "-k", "10", "300", EXE, fin, fout, data.DATA_DIR, "64"], capture_output=True,
-                       text=True)
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    r = subprocess.run(["timeout", "-k", "10", "300", EXE, fin, fout, data.DATA_DIR, "64", str(repeat)],
+                       capture_output=True, text=True, env=env)
+    if repeat > 1:
+        assert "ms per block loop" in r.stdout and "%d threads" % threads in r.stdout, r.stdout
     assert r.returncode == 0, r.stdout + r.stderr
     got = rbin.read(fout)
     lu, ld, _ = orc.clear_sky_lw(prob, [data.load_model("lw_abs"), data.load_model("lw_pfrac")],
