@@ -30,6 +30,18 @@ SIGNATURES = {
     "rrtmgpnn_free": (c_int, [c_vp, c_vp]),
     "rrtmgpnn_memcpy_h2d": (c_int, [c_vp, c_vp, c_vp, c_ll]),
     "rrtmgpnn_memcpy_d2h": (c_int, [c_vp, c_vp, c_vp, c_ll]),
+    "rrtmgpnn_context_create_owned": (c_int, [c_int, P(c_vp)]),
+    "rrtmgpnn_present": (c_int, [c_vp, c_vp, c_ll, c_int, P(c_vp)]),
+    "rrtmgpnn_present_update_host": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_present_update_device": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_present_delete": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_stage_h2d": (c_int, [c_vp, c_vp, c_ll, P(c_vp)]),
+    "rrtmgpnn_scratch": (c_int, [c_vp, c_ll, P(c_vp)]),
+    "rrtmgpnn_release": (c_int, [c_vp, c_vp]),
+    "rrtmgpnn_copy_d2h": (c_int, [c_vp, c_vp, c_vp, c_ll]),
+    "rrtmgpnn_copy_h2d": (c_int, [c_vp, c_vp, c_vp, c_ll]),
+    "rrtmgpnn_copy_d2d": (c_int, [c_vp, c_vp, c_vp, c_ll]),
+    "rrtmgpnn_memset_async": (c_int, [c_vp, c_vp, c_int, c_ll]),
     "rrtmgpnn_network_load": (c_int, [c_vp, c_char_p, P(c_vp)]),
     "rrtmgpnn_network_create": (c_int, [c_vp, c_int, P(c_int), P(c_int), P(c_vp), P(c_vp), c_vp, c_vp, c_vp, c_vp,
                                         c_char_p, P(c_vp)]),

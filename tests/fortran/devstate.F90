@@ -1,0 +1,97 @@
+! devstate.F90 -- exercises the Fortran drop-in's device data environment (tests/test_fortran.py):
+! gas_optics leaves tau and the (deferred) Planck sources on the device; update_host() brings them back; a host write
+! followed by update_device() is what the next rte_lw reads.
+! usage: devstate <problem.rbin> <output.rbin> <data_dir>
+!   output: tau, lay_source, lev_source, sfc_source (as gas_optics produced them), and the LW fluxes of rte_lw run
+!   twice: on the gas-optics tau (flux_up/dn_a) and on 0.5 * tau written on the host (flux_up/dn_b).
+program devstate
+  use mo_rte_kind,           only: wp
+  use mo_optical_props,      only: ty_optical_props_1scl
+  use mo_source_functions,   only: ty_source_func_lw
+  use mo_fluxes,             only: ty_fluxes_flexible
+  use mo_gas_concentrations, only: ty_gas_concs
+  use mo_gas_optics_rrtmgp,  only: ty_gas_optics_rrtmgp
+  use mod_network_rrtmgp,    only: rrtmgp_network_type
+  use mo_rte_lw,             only: rte_lw
+  use mo_rrtmgpnn_rbin
+  implicit none
+  character(len=512) :: pfile, ofile, ddir
+  real(wp), allocatable :: play(:,:), plev(:,:), tlay(:,:), tlev(:,:), tsfc(:), sfc_emis(:), scal(:), vmr(:,:)
+  real(wp), allocatable :: emis(:,:), tau0(:,:,:), lay0(:,:,:), lev0(:,:,:), sfc0(:,:)
+  real(wp), allocatable, target :: up_a(:,:), dn_a(:,:), up_b(:,:), dn_b(:,:)
+  character(len=32), allocatable :: gas_names(:)
+  type(ty_gas_concs) :: gas_concs
+  type(ty_gas_optics_rrtmgp) :: kdist
+  type(rrtmgp_network_type), dimension(2) :: nets
+  type(ty_optical_props_1scl) :: op
+  type(ty_source_func_lw) :: src
+  type(ty_fluxes_flexible) :: fl
+  character(len=128) :: e
+  integer :: ncol, nlay, ig, icol, u
+  logical :: top_at_1
+
+  call get_command_argument(1, pfile)
+  call get_command_argument(2, ofile)
+  call get_command_argument(3, ddir)
+  call rbin_real2(pfile, "play", play, e); call chk(e)
+  call rbin_real2(pfile, "plev", plev, e); call chk(e)
+  call rbin_real2(pfile, "tlay", tlay, e); call chk(e)
+  call rbin_real2(pfile, "tlev", tlev, e); call chk(e)
+  call rbin_real1(pfile, "tsfc", tsfc, e); call chk(e)
+  call rbin_real1(pfile, "sfc_emis", sfc_emis, e); call chk(e)
+  call rbin_real1(pfile, "top_at_1", scal, e); call chk(e)
+  top_at_1 = scal(1) /= 0._wp
+  call rbin_strings(pfile, "gas_names", gas_names, e); call chk(e)
+  nlay = size(play, 1)
+  ncol = size(play, 2)
+  call chk(gas_concs%init(gas_names))
+  do ig = 1, size(gas_names)
+    call rbin_real2(pfile, "vmr_" // trim(gas_names(ig)), vmr, e); call chk(e)
+    call chk(gas_concs%set_vmr(gas_names(ig), vmr))
+  end do
+  call nets(1)%load_netcdf(trim(ddir) // "/nn_lw_g256_abs.rbin")
+  call nets(2)%load_netcdf(trim(ddir) // "/nn_lw_g256_pfrac.rbin")
+  call chk(kdist%load_rbin(trim(ddir) // "/kdist_lw_g256.rbin", gas_names))
+  call chk(op%alloc_1scl(ncol, nlay, kdist))
+  call chk(src%alloc(ncol, nlay, kdist))
+  allocate(emis(kdist%get_nband(), ncol))
+  do icol = 1, ncol
+    emis(:, icol) = sfc_emis(icol)
+  end do
+  call chk(kdist%gas_optics(play, plev, tlay, tsfc, gas_concs, op, src, tlev=tlev, neural_nets=nets))
+  ! the device results, copied back
+  call op%update_host()
+  call src%update_host()
+  tau0 = op%tau
+  lay0 = src%lay_source
+  lev0 = src%lev_source
+  sfc0 = src%sfc_source
+  allocate(up_a(nlay + 1, ncol), dn_a(nlay + 1, ncol), up_b(nlay + 1, ncol), dn_b(nlay + 1, ncol))
+  fl%flux_up => up_a
+  fl%flux_dn => dn_a
+  call chk(rte_lw(op, top_at_1, src, emis, fl))
+  ! a host write, announced with update_device, is what the solver reads next
+  op%tau = 0.5_wp * op%tau
+  call op%update_device()
+  fl%flux_up => up_b
+  fl%flux_dn => dn_b
+  call chk(rte_lw(op, top_at_1, src, emis, fl))
+  u = rbin_write_begin(ofile, 8)
+  call rbin_write_real(u, "tau", tau0, shape(tau0))
+  call rbin_write_real(u, "lay_source", lay0, shape(lay0))
+  call rbin_write_real(u, "lev_source", lev0, shape(lev0))
+  call rbin_write_real(u, "sfc_source", sfc0, shape(sfc0))
+  call rbin_write_real(u, "flux_up_a", up_a, shape(up_a))
+  call rbin_write_real(u, "flux_dn_a", dn_a, shape(dn_a))
+  call rbin_write_real(u, "flux_up_b", up_b, shape(up_b))
+  call rbin_write_real(u, "flux_dn_b", dn_b, shape(dn_b))
+  call rbin_write_end(u)
+contains
+  subroutine chk(msg)
+    character(len=*), intent(in) :: msg
+    if (len_trim(msg) > 0) then
+      write(*, '(a)') trim(msg)
+      error stop 1
+    end if
+  end subroutine chk
+end program devstate

@@ -148,3 +148,38 @@ def test_fortran_allsky_driver_matches_oracle(tmp_path, orc, rfmip, files):
                       ("sw_up", su, got["sw_flux_up"]), ("sw_dn", sd, got["sw_flux_dn"]),
                       ("sw_dir", sr[use], got["sw_flux_dir"][use])):
         np.testing.assert_array_equal(g, ref, err_msg=k + ": not bit-identical")
+
+
+@pytest.mark.gpu
+@needs_fc
+def test_fortran_device_state_update_host_and_device(tmp_path, orc, rfmip):
+    """The device data environment as a reference user sees it (tests/fortran/devstate.F90): after gas_optics,
+    update_host() returns tau and the Planck sources (formed from the deferred Planck fraction) bit-identical to the
+    oracle's; rte_lw on the device copies equals the oracle; a host write to tau followed by update_device() is what
+    the next rte_lw reads (0.5 * tau through the oracle's solver, bit for bit)."""
+    from rrtmgpnn import data, rbin
+    _make()
+    lib = os.path.join(ROOT, "rte-rrtmgp-nn_amd")
+    exe = str(tmp_path / "devstate")
+    r = subprocess.run([FC, "-O1", "-fopenmp", "-I", FBUILD, os.path.join(ROOT, "tests", "fortran", "devstate.F90"),
+                        "-o", exe, os.path.join(FBUILD, "librrtmgpnn_fortran.a"), "-L" + lib, "-lrrtmgpnn",
+                        "-Wl,-rpath," + lib], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    prob = subset(rfmip, np.arange(5, 1800, 45))
+    fin, fout = str(tmp_path / "in.rbin"), str(tmp_path / "out.rbin")
+    write_problem(prob, fin)
+    r = subprocess.run(["timeout", "-k", "10", "120", exe, fin, fout, data.DATA_DIR], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = rbin.read(fout)
+    kd = data.load_kdist("lw")
+    go = orc.lw_gas_optics(prob, [data.load_model("lw_abs"), data.load_model("lw_pfrac")], kd)
+    np.testing.assert_array_equal(got["tau"], go["tau"])
+    np.testing.assert_array_equal(got["lay_source"], go["lay_source"])
+    np.testing.assert_array_equal(got["lev_source"], go["lev_source"])
+    np.testing.assert_array_equal(got["sfc_source"], go["sfc_source"])
+    ngpt = go["tau"].shape[-1]
+    emis = np.repeat(np.asarray(prob["sfc_emis"], np.float32)[:, None], ngpt, axis=1)
+    for tag, tau in (("a", go["tau"]), ("b", (np.float32(0.5) * go["tau"]).astype(np.float32))):
+        up, dn = orc.lw_solver(tau, go["lay_source"], go["lev_source"], emis, go["sfc_source"], prob["top_at_1"])
+        np.testing.assert_array_equal(got["flux_up_" + tag], up, err_msg=tag)
+        np.testing.assert_array_equal(got["flux_dn_" + tag], dn, err_msg=tag)
