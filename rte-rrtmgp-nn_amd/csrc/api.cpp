@@ -71,7 +71,8 @@ static int finalize_network(rrtmgpnn_network *net)
   RRTMGPNN_HIP(hipSetDevice(net->device));
   RRTMGPNN_HIP(hipMalloc(&net->d_raw, total * 4));
   RRTMGPNN_HIP(hipMemcpy(net->d_raw, raw.data(), total * 4, hipMemcpyHostToDevice));
-  return pack_network(net);
+  if (int rc = pack_network(net)) return rc;
+  return pack_network32(net);
 }
 
 static int check_ctx(rrtmgpnn_context *ctx)
@@ -357,6 +358,7 @@ int rrtmgpnn_network_destroy(rrtmgpnn_network *net)
   (void)hipSetDevice(net->device);
   if (net->d_raw) (void)hipFree(net->d_raw);
   if (net->d_packed) (void)hipFree(net->d_packed);
+  if (net->d_packed32) (void)hipFree(net->d_packed32);
   delete net;
   return RRTMGPNN_OK;
 }

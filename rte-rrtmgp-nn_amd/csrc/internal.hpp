@@ -103,6 +103,11 @@ struct rrtmgpnn_network {
   int packed_floats = 0;
   int k1s = 0, h1t = 0, h2t = 0, ngt = 0;
   int off_l1 = 0, off_l2 = 0, off_l3 = 0, off_b1 = 0, off_b2 = 0, off_b3 = 0, off_std = 0, off_mean = 0;
+  // packed image of the 32x32x2 kernel (kernels_nn32.hip; 3-layer networks with hidden widths <= 64):
+  // s32 = KS, HT1, N2, HT2, N3, NGT
+  float *d_packed32 = nullptr;
+  int packed32_floats = 0;
+  int s32[6] = {0};
   bool has_out_scaling() const { return !out_mean.empty(); }
 };
 
@@ -156,6 +161,12 @@ int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, c
 int launch_mlp_generic(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch, const float *x,
                        float *out);
 int pack_network(rrtmgpnn_network *net);
+// kernels_nn32.hip: the LW modes on v_mfma_f32_32x32x2_f32; RRTMGPNN_ERR_UNSUPPORTED (no error set) when no instance
+// exists for the networks (launch_mlp then runs the 16x16x4 kernel)
+int pack_network32(rrtmgpnn_network *net);
+int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
+                 long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
+                 const MlpInputs *in);
 // kernels_rte.hip
 struct BandArgs {
   int lims[2 * kMaxBands];

@@ -26,8 +26,7 @@
 //   holds logical unit u = 16m + 4r + q.  With that permutation, K-step (m, t) of the next
 //   layer feeds unit 16m + 4t + q from lane group q, i.e. every dot product is accumulated in
 //   ascending k order -- bit-identical to a sequential fmaf chain (the oracle's order).
-#include "internal.hpp"
-#include "libm_ref.hpp"
+#include "nn_device.hpp"
 
 #include <algorithm>
 #include <cmath>
@@ -39,11 +38,6 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // ------------------------------------------------------------------------------------------
 // compute_nn_inputs + col_dry are elementwise over (lay, col).
 // ------------------------------------------------------------------------------------------
-struct NnInArgs {
-  float mn[kMaxInputs];
-  float mx[kMaxInputs];
-};
-
 // One thread per (lay, col) sample.  The gas loop is unrolled over kMaxInputs so every gas pointer and
 // scaling constant stays a kernel-argument SGPR (a runtime index would put them in scratch), and the
 // block's (nx x 256) outputs are staged in LDS so the store to `out` is one contiguous stream.
@@ -82,17 +76,6 @@ __global__ void __launch_bounds__(kInThreads) nn_inputs_kernel(int ncol, int nla
   __syncthreads();
   float *dst = out + (size_t)nx * s0;
   for (int i = threadIdx.x; i < nx * ns; i += kInThreads) dst[i] = st[i];
-}
-
-// get_col_dry for one (layer, column): h2o vmr v and the layer's two level pressures (shared by col_dry_kernel and
-// the MLP kernel's in-kernel form, so both give the same bits)
-__device__ __forceinline__ float col_dry_of(float v, float p_a, float p_b)
-{
-  const float m_dry = 0.028964f, m_h2o = 0.018016f, avogad = 6.02214076e23f, grav = 9.80665f;
-  float delta_plev = fabsf(p_a - p_b);
-  float fact = 1.0f / (1.0f + v);
-  float m_air = (m_dry + m_h2o * v) * fact;
-  return 10.0f * delta_plev * avogad * fact / (1000.0f * m_air * 100.0f * grav);
 }
 
 __global__ void col_dry_kernel(int ncol, int nlay, const float *__restrict__ h2o, const float *__restrict__ plev,
@@ -175,10 +158,6 @@ __device__ __forceinline__ float activate(int act, float x)
   }
 }
 
-#ifndef RRTMGPNN_MLP_FASTDIV
-#define RRTMGPNN_MLP_FASTDIV 1
-#endif
-
 // Compile-time activation sets of the fused kernel: ACTS == 1 is the shipped models' softsign,
 // softsign, linear (Appendix A of SURVEY.md), inlined straight-line; ACTS == 0 dispatches on the
 // runtime codes (any other combination).
@@ -188,13 +167,7 @@ __device__ __forceinline__ float act_hidden(int act, float x)
 #ifdef RRTMGPNN_ABL_MLP_CHEAP_ACT  // ablation only: breaks parity
   if constexpr (ACTS == 1) return x * 0.5f;
 #endif
-#if RRTMGPNN_MLP_FASTDIV
-  // softsign with the division sequence minus v_div_scale/v_div_fixup (libm_ref.hpp div_rn_normal): exact for
-  // |x| < 2^126 -- below 2^-24, |x| + 1 rounds to 1 and the quotient is x itself; above, both operands and the
-  // quotient are normal
-  if constexpr (ACTS == 1) return div_rn_normal(x, fabsf(x) + 1.0f);
-#endif
-  if constexpr (ACTS == 1) return x / (fabsf(x) + 1.0f);  // softsign (mod_activation.F90:107-128)
+  if constexpr (ACTS == 1) return softsign(x);  // nn_device.hpp (mod_activation.F90:107-128)
   else return activate(act, x);
 }
 template <int ACTS>
@@ -306,12 +279,6 @@ struct MlpArgs {
   GasArgs gas;
   NnInArgs sc;
 };
-
-__device__ __forceinline__ float pow8(float t)
-{
-  float t2 = t * t, t4 = t2 * t2;
-  return t4 * t4;
-}
 
 // Hidden layers of one network for a 16-sample tile: returns H2 accumulators.
 template <int K1S, int H1T, int H2T, int ACTS>
@@ -696,6 +663,10 @@ int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, c
                const MlpInputs *in)
 {
   if (nbatch <= 0) return RRTMGPNN_OK;
+  if (mode == MLP_LW_PAIR || mode == MLP_LW_BOTH) {  // the 32x32x2 kernel first (kernels_nn32.hip)
+    const int rc = launch_mlp32(ctx, mode, A, B, nbatch, ngpt, x, col_dry, out0, out1, in);
+    if (rc != RRTMGPNN_ERR_UNSUPPORTED) return rc;
+  }
   if (!A || !A->d_packed) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: network has no MFMA image (needs 3 layers)");
   bool paired = (mode == MLP_LW_PAIR || mode == MLP_SW_PAIR);
   if (paired && (!B || !B->d_packed)) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: second network has no MFMA image");

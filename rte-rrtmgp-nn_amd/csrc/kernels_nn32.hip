@@ -1,0 +1,488 @@
+// kernels_nn32.hip -- the LW gas-optics networks on v_mfma_f32_32x32x2_f32 (gfx950), 32 samples per wave tile.
+//
+// Same networks, epilogues and bits as mlp_pair_kernel's LW modes (kernels_nn.hip):
+//   LW pair : tau = (std*(y+b)+mean)^8 * col_dry  and  pfrac = (y+b)^2
+//             (predict_nn_lw_blas_sp, rrtmgp/kernels/mo_gas_optics_kernels.F90:690-774;
+//              neural/mod_network_rrtmgp.F90:125-317)
+//   LW both : one model with 2*ngpt outputs (output_sgemm_lw, mod_network_rrtmgp.F90:319-409;
+//             mo_gas_optics_kernels.F90:744-772)
+// optionally with the inputs formed in-kernel (compute_nn_inputs + get_col_dry, the fused gas-optics entry).
+//
+// Why a second tiling: the 16x16x4 f32 MFMA issues every 32 cycles but its dependent-accumulator latency is 40, and
+// each instruction takes its weight operand from LDS (one ds_read per 2 048 flop).  The 32x32x2 form issues every 64
+// cycles with a 64-cycle dependent latency, so a single accumulation chain runs at the issue rate, and it does
+// 4 096 flop per operand; the weight images are packed so one ds_read_b128 feeds 4 MFMAs.  The shipped sizes also
+// divide evenly: 18 inputs = 9 K-steps, 58 hidden units = 29 K-steps (the 16x16x4 tiling pads 18 -> 20, 58 -> 64).
+//
+// MFMA mapping (v_mfma_f32_32x32x2_f32: exact f32, D = (C + a0*b0) + a1*b1 as an fmaf chain):
+//   lane l: j = l & 31 (sample / output row), h = l >> 5 (k within the step).
+//   A[i = j][k = h], B[k = h][col = j]; accumulator register r holds D[row (r&3) + 8(r>>2) + 4h][col j].
+//   Hidden layers compute H^T (units x samples): A = packed W^T, B = activations.  Physical row R of hidden tile mo
+//   holds logical unit u = 32mo + 2((R&3) + 4(R>>3)) + ((R>>2)&1), so register r of lane half h holds unit
+//   32mo + 2r + h: K-step S = 16mo + r of the next layer takes units 2S (h = 0) and 2S+1 (h = 1) from the lanes'
+//   own registers, and every dot product accumulates in ascending k -- the oracle's fmaf order, bit for bit.
+//   The output layer computes Y^T (g-points x samples) with the weights as A: lane (j, h) holds g = 32go + 8b + 4h + i
+//   (b, i = 0..3) of sample j, 4 float4 stores per output array and g-tile.
+#include "nn_device.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+namespace rrtmgpnn {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------
+// Packed image (floats) of a 3-layer network [nx, h1, h2, ny]:
+//   KS = ceil(nx/2), HT1 = ceil(h1/32), N2 = ceil(h1/2), HT2 = ceil(h2/32), N3 = ceil(h2/2), NGT = ceil(ny/32);
+//   q(n) = ceil(n/4): operand steps are grouped by 4, [group][lane][4], one 16-byte LDS read per lane per group.
+//   L1 [HT1][q(KS)][64][4]  lane (i, h), step s: W1[k = 2s+h][u(mo, i)]
+//   L2 [HT2][q(N2)][64][4]  step S: W2[k = 2S+h][u(mo, i)]
+//   L3 [NGT][q(N3)][64][4]  step S: W3[k = 2S+h][g = 32go + i]
+//   B1 [HT1][2][16], B2 [HT2][2][16]: b[32mo + 2r + h] at [mo][h][r] (a lane's 16 biases are contiguous)
+//   B3, STD, MEAN [NGT*32] by g
+//   XS [2][16] input minimum, then [2][16] input range (max - min) of input k = 2t + h at [h][t] (compute_nn_inputs'
+//      scaling, in the fused entry); past nx: minimum 0, range 1, so a zero raw value scales to 0
+// ------------------------------------------------------------------------------------------
+struct Img32 {
+  int l1, l2, l3, b1, b2, b3, sd, mn, xs, total;
+};
+__host__ __device__ constexpr Img32 img32_layout(int KS, int HT1, int N2, int HT2, int N3, int NGT)
+{
+  Img32 L{};
+  L.l1 = 0;
+  L.l2 = L.l1 + HT1 * ((KS + 3) / 4) * 256;
+  L.l3 = L.l2 + HT2 * ((N2 + 3) / 4) * 256;
+  L.b1 = L.l3 + NGT * ((N3 + 3) / 4) * 256;
+  L.b2 = L.b1 + HT1 * 32;
+  L.b3 = L.b2 + HT2 * 32;
+  L.sd = L.b3 + NGT * 32;
+  L.mn = L.sd + NGT * 32;
+  L.xs = L.mn + NGT * 32;
+  L.total = L.xs + 64;
+  return L;
+}
+
+int pack_network32(rrtmgpnn_network *net)
+{
+  if (net->nlayers != 3) return RRTMGPNN_OK;
+  const int nx = net->dims[0], h1 = net->dims[1], h2 = net->dims[2], ny = net->dims[3];
+  if (nx > kMaxInputs || h1 > 64 || h2 > 64) return RRTMGPNN_OK;  // the 16x16x4 kernel covers the rest
+  const int KS = (nx + 1) / 2, HT1 = (h1 + 31) / 32, N2 = (h1 + 1) / 2, HT2 = (h2 + 31) / 32, N3 = (h2 + 1) / 2,
+            NGT = (ny + 31) / 32;
+  const Img32 L = img32_layout(KS, HT1, N2, HT2, N3, NGT);
+  std::vector<float> img(L.total, 0.0f);
+  const std::vector<float> &W1 = net->w[0], &W2 = net->w[1], &W3 = net->w[2];
+  auto unit = [](int mo, int R) { return 32 * mo + 2 * ((R & 3) + 4 * (R >> 3)) + ((R >> 2) & 1); };
+  // operand arrays: [tile][step group][lane][4]
+  auto put = [&](int base, int nsteps, int tile, int S, int l, float v) {
+    const int q = (nsteps + 3) / 4;
+    img[base + ((tile * q + S / 4) * 64 + l) * 4 + (S & 3)] = v;
+  };
+  for (int mo = 0; mo < HT1; mo++)
+    for (int s = 0; s < KS; s++)
+      for (int l = 0; l < 64; l++) {
+        const int i = l & 31, h = l >> 5, k = 2 * s + h, u = unit(mo, i);
+        put(L.l1, KS, mo, s, l, (k < nx && u < h1) ? W1[(size_t)k * h1 + u] : 0.0f);
+      }
+  for (int mo = 0; mo < HT2; mo++)
+    for (int S = 0; S < N2; S++)
+      for (int l = 0; l < 64; l++) {
+        const int i = l & 31, h = l >> 5, k = 2 * S + h, u = unit(mo, i);
+        put(L.l2, N2, mo, S, l, (k < h1 && u < h2) ? W2[(size_t)k * h2 + u] : 0.0f);
+      }
+  for (int go = 0; go < NGT; go++)
+    for (int S = 0; S < N3; S++)
+      for (int l = 0; l < 64; l++) {
+        const int i = l & 31, h = l >> 5, k = 2 * S + h, g = 32 * go + i;
+        put(L.l3, N3, go, S, l, (k < h2 && g < ny) ? W3[(size_t)k * ny + g] : 0.0f);
+      }
+  for (int mo = 0; mo < HT1; mo++)
+    for (int h = 0; h < 2; h++)
+      for (int r = 0; r < 16; r++) {
+        const int u = 32 * mo + 2 * r + h;
+        img[L.b1 + (mo * 2 + h) * 16 + r] = u < h1 ? net->b[0][u] : 0.0f;
+      }
+  for (int mo = 0; mo < HT2; mo++)
+    for (int h = 0; h < 2; h++)
+      for (int r = 0; r < 16; r++) {
+        const int u = 32 * mo + 2 * r + h;
+        img[L.b2 + (mo * 2 + h) * 16 + r] = u < h2 ? net->b[1][u] : 0.0f;
+      }
+  for (int g = 0; g < NGT * 32; g++) {
+    img[L.b3 + g] = g < ny ? net->b[2][g] : 0.0f;
+    img[L.sd + g] = (g < ny && net->has_out_scaling()) ? net->out_std[g] : 0.0f;
+    img[L.mn + g] = (g < ny && net->has_out_scaling()) ? net->out_mean[g] : 0.0f;
+  }
+  for (int h = 0; h < 2; h++)
+    for (int t = 0; t < 16; t++) {
+      const int k = 2 * t + h;
+      const bool on = k < nx && k < (int)net->in_min.size() && k < (int)net->in_max.size();
+      img[L.xs + h * 16 + t] = on ? net->in_min[k] : 0.0f;
+      img[L.xs + 32 + h * 16 + t] = on ? net->in_max[k] - net->in_min[k] : 1.0f;
+    }
+  float *d = nullptr;
+  RRTMGPNN_HIP(hipMalloc(&d, sizeof(float) * img.size()));
+  RRTMGPNN_HIP(hipMemcpy(d, img.data(), sizeof(float) * img.size(), hipMemcpyHostToDevice));
+  net->d_packed32 = d;
+  net->packed32_floats = L.total;
+  net->s32[0] = KS; net->s32[1] = HT1; net->s32[2] = N2; net->s32[3] = HT2; net->s32[4] = N3; net->s32[5] = NGT;
+  return RRTMGPNN_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel
+// ------------------------------------------------------------------------------------------
+// Every load and store of a tile goes through a raw buffer descriptor: a lane past the batch (or the lane half an
+// input does not belong to) uses an offset past the descriptor's range, where loads return 0 and stores are dropped.
+// The tile body then has no branch, so it is one basic block and the scheduler can interleave the output tiles'
+// epilogues and stores with the next tiles' MFMA chains, and one network's activations with the other's MFMAs.
+static constexpr uint32_t kOOB = 0x7ffff000u;  // past every descriptor's range (the host checks the sizes)
+static constexpr uint32_t kMaxRecords = 0x7ff00000u;
+
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Buf(const void *base, uint32_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)bytes, 0x00020000)) {}
+  __device__ __forceinline__ float ld(uint32_t voff) const
+  {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
+  }
+  __device__ __forceinline__ void st4(const floatx4 &v, uint32_t voff) const
+  {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), r, voff, 0, 0);
+  }
+};
+
+struct Mlp32Args {
+  const float *x;        // (nx, nbatch)
+  const float *col_dry;  // (nbatch)
+  float *out0, *out1;
+  const float *imgA, *imgB;
+  int imgA_floats, imgB_floats;
+  int nx, ngpt;
+  int nbatch;
+  // in-kernel inputs (the fused gas-optics entry)
+  const float *play, *tlay, *plev, *h2o;
+  int nlay, ncol;
+  GasArgs gas;
+  // per input k (host-made, so the device offsets need no branch): byte offset of sample s, layer ilay =
+  // s * gsm[k] + ilay * glm[k] (2-D: 4, 0; 1-D: 0, 4; scalar: 0, 0); grec[k] = the array's bytes (0: absent or k >= nx)
+  uint32_t gsm[kMaxInputs], glm[kMaxInputs], grec[kMaxInputs];
+};
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, const floatx16 &c)
+{
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// D += sum over steps s < NS of W[tile][s] * v[s]  (v[s]: the lane's B operand of step s)
+template <int NS>
+__device__ __forceinline__ floatx16 mfma_chain(const float *__restrict__ w, int tile, const float (&v)[NS], int lane)
+{
+  constexpr int Q = (NS + 3) / 4;
+  floatx16 acc = {};
+  const floatx4 *wp = (const floatx4 *)w + (size_t)tile * Q * 64 + lane;
+#pragma unroll
+  for (int g4 = 0; g4 < Q; g4++) {
+    const floatx4 wv = wp[g4 * 64];
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if (4 * g4 + e < NS) acc = mfma32(wv[e], v[4 * g4 + e], acc);
+  }
+  return acc;
+}
+
+// Hidden layers of one network for a 32-sample tile: returns the layer-2 activations as the output layer's B
+// operands (N3 K-steps)
+template <int KS, int HT1, int N2, int HT2, int N3, int NGT>
+__device__ __forceinline__ void mlp32_hidden(const float *__restrict__ img, const float (&x)[KS], int lane,
+                                             float (&h2)[N3])
+{
+  constexpr Img32 L = img32_layout(KS, HT1, N2, HT2, N3, NGT);
+  const int h = lane >> 5;
+  float h1[N2];
+#pragma unroll
+  for (int mo = 0; mo < HT1; mo++) {
+    const floatx16 acc = mfma_chain<KS>(img + L.l1, mo, x, lane);
+    const float *bb = img + L.b1 + (mo * 2 + h) * 16;
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+      if (16 * mo + r < N2) h1[16 * mo + r] = softsign(acc[r] + bb[r]);
+  }
+#pragma unroll
+  for (int mo = 0; mo < HT2; mo++) {
+    const floatx16 acc = mfma_chain<N2>(img + L.l2, mo, h1, lane);
+    const float *bb = img + L.b2 + (mo * 2 + h) * 16;
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+      if (16 * mo + r < N3) h2[16 * mo + r] = softsign(acc[r] + bb[r]);
+  }
+}
+
+#ifndef RRTMGPNN_MLP32_UNROLL
+#define RRTMGPNN_MLP32_UNROLL 2
+#endif
+#ifndef RRTMGPNN_MLP32_THREADS
+#define RRTMGPNN_MLP32_THREADS 512
+#endif
+constexpr int kMlp32Threads = RRTMGPNN_MLP32_THREADS;
+
+// A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  Outputs are stored 16 bytes
+// at a time: the host guarantees ngpt % 4 == 0 and 16-byte aligned output arrays.
+template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN>
+__global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
+{
+  constexpr bool kPair = MODE == MLP_LW_PAIR;
+  extern __shared__ floatx4 lds4[];
+  {
+    const int n4 = (a.imgA_floats + (kPair ? a.imgB_floats : 0)) / 4, nA4 = a.imgA_floats / 4;
+    const floatx4 *srcA = (const floatx4 *)a.imgA, *srcB = (const floatx4 *)a.imgB;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) lds4[i] = i < nA4 ? srcA[i] : srcB[i - nA4];
+  }
+  __syncthreads();
+  const float *imgA = (const float *)lds4;
+  const float *imgB = imgA + a.imgA_floats;
+  constexpr Img32 LA = img32_layout(KS, AH1, AN2, AH2, AN3, NGT);
+  constexpr Img32 LB = img32_layout(KS, BH1, BN2, BH2, BN3, NGT);
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;
+  const int nx = a.nx, ngpt = a.ngpt;
+  const int ntiles = (a.nbatch + 31) / 32;
+  const int tstride = gridDim.x * nwaves;
+  const uint32_t nb4 = 4u * (uint32_t)a.nbatch;
+
+  // Layer-1 B operand of step s: input k = 2s + h of sample s0 + j.  XIN: raw[s] holds the state value input k is
+  // formed from (s = 0: tlay / play; s = 1: h2o / o3; s > 1: gas k), raw[KS..KS+2] = h2o, p(lev ilay), p(lev ilay+1)
+  constexpr int NR = XIN ? KS + 3 : KS;
+  auto load_x = [&](int tl, float (&xv)[NR]) {
+    const uint32_t s = (uint32_t)tl * 32u + (uint32_t)j;  // loads past the batch return 0
+    if constexpr (XIN) {
+      const uint32_t nlay = (uint32_t)a.nlay;
+      const uint32_t icol = s / nlay, ilay = s - icol * nlay;
+      const uint32_t o2 = 4u * s;
+      // inputs 2t (lane half 0) and 2t+1 (half 1): one descriptor per array (uniform), each half reading its own
+      auto pair = [&](int k0, const float *p0, uint32_t r0, uint32_t f0, const float *p1, uint32_t r1, uint32_t f1) {
+        (void)k0;
+        const Buf b0(p0, r0), b1(p1, r1);
+        const float v0 = b0.ld(h ? kOOB : f0), v1 = b1.ld(h ? f1 : kOOB);
+        return h ? v1 : v0;
+      };
+      xv[0] = pair(0, a.tlay, nb4, o2, a.play, nb4, o2);
+      if constexpr (KS > 1) xv[1] = pair(2, a.gas.p[2], a.grec[2], o2, a.gas.p[3], a.grec[3], o2);
+#pragma unroll
+      for (int t = 2; t < KS; t++) {
+        const int k0 = 2 * t, k1 = 2 * t + 1;
+        xv[t] = pair(k0, a.gas.p[k0], a.grec[k0], s * a.gsm[k0] + ilay * a.glm[k0], a.gas.p[k1], a.grec[k1],
+                     s * a.gsm[k1] + ilay * a.glm[k1]);
+      }
+      const Buf bh(a.h2o, nb4), bl(a.plev, 4u * (nlay + 1u) * (uint32_t)a.ncol);
+      const uint32_t pl = 4u * (icol * (nlay + 1u) + ilay);
+      xv[KS] = bh.ld(o2);
+      xv[KS + 1] = bl.ld(s < (uint32_t)a.nbatch ? pl : kOOB);
+      const float p1 = bl.ld(s < (uint32_t)a.nbatch ? pl + 4u : kOOB);
+      xv[KS + 2] = s < (uint32_t)a.nbatch ? p1 : 1.0f;
+    } else {
+      const Buf bx(a.x, nb4 * (uint32_t)nx);
+#pragma unroll
+      for (int t = 0; t < KS; t++) {
+        const int k = 2 * t + h;
+        xv[t] = bx.ld(k < nx ? 4u * (s * (uint32_t)nx + (uint32_t)k) : kOOB);
+      }
+    }
+  };
+  // XIN: compute_nn_inputs (nn_inputs_kernel's expressions) in place, with the scaling constants of network A's image
+  // (the host checks that they are the ones it was given); returns col_dry.  No branch: log is formed on every lane
+  // and selected, and inputs past nx scale a zero raw value by (0 - 0) / 1.
+  auto form_x = [&](float (&xv)[NR], const float *xs) -> float {
+    if constexpr (XIN) {
+      const float *mn = xs + h * 16, *rg = xs + 32 + h * 16;
+      const float lg = ref_logf_nb(xv[0]);
+      xv[0] = ((h ? lg : xv[0]) - mn[0]) / rg[0];
+      if constexpr (KS > 1) xv[1] = (sqrtf(sqrtf(xv[1])) - mn[1]) / rg[1];
+#pragma unroll
+      for (int t = 2; t < KS; t++) xv[t] = (xv[t] - mn[t]) / rg[t];
+      return col_dry_of(xv[KS], xv[KS + 1], xv[KS + 2]);
+    } else {
+      return 0.0f;
+    }
+  };
+
+  float xn[NR];  // the next tile's inputs, loaded before this tile's stores
+  load_x(blockIdx.x * nwaves + wave, xn);
+  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += tstride) {
+    float xv[NR];
+#pragma unroll
+    for (int t = 0; t < NR; t++) xv[t] = xn[t];
+    load_x(tile + tstride, xn);
+    // The weight images are loop-invariant: left visible, their LDS reads are hoisted out of the tile loop and
+    // spilled to scratch.  An offset the compiler cannot see through keeps them inside, next to their MFMAs.
+    int lds_off = 0;
+    asm volatile("" : "+s"(lds_off));
+    const float *iA = imgA + lds_off, *iB = imgB + lds_off;
+    const float cd_in = form_x(xv, iA + LA.xs);
+    float x1[KS];
+#pragma unroll
+    for (int t = 0; t < KS; t++) x1[t] = xv[t];
+    float hA[AN3];
+    mlp32_hidden<KS, AH1, AN2, AH2, AN3, NGT>(iA, x1, lane, hA);
+    float hB[kPair ? BN3 : 1];
+    if constexpr (kPair) mlp32_hidden<KS, BH1, BN2, BH2, BN3, NGT>(iB, x1, lane, hB);
+    // wave-uniform by construction; readfirstlane lets the compiler keep the output descriptors in SGPRs (it treats
+    // the loop index as divergent and would wrap every store in a waterfall loop)
+    const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(tile * 32);
+    const uint32_t nvalid = min(32u, (uint32_t)a.nbatch - s0);
+    float cd;
+    if constexpr (XIN) {
+      cd = cd_in;
+    } else {
+      const Buf bc(a.col_dry, nb4);
+      cd = bc.ld(4u * (s0 + (uint32_t)j));
+    }
+    // this tile's rows of the outputs: (nvalid, ngpt) floats; rows past the batch fall outside and are dropped
+    const uint32_t rows = nvalid * (uint32_t)ngpt * 4u;
+    const Buf o0(a.out0 + (size_t)s0 * ngpt, rows), o1(a.out1 + (size_t)s0 * ngpt, rows);
+    const uint32_t vrow = 4u * (uint32_t)j * (uint32_t)ngpt;
+    auto out_tile = [&](int go) {
+      const floatx16 yA = mfma_chain<AN3>(iA + LA.l3, go, hA, lane);
+      floatx16 yB = {};
+      if constexpr (kPair) yB = mfma_chain<BN3>(iB + LB.l3, go, hB, lane);
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int g0 = 32 * go + 8 * b + 4 * h;
+        const floatx4 bA = *(const floatx4 *)&iA[LA.b3 + g0];
+        const floatx4 sdA = *(const floatx4 *)&iA[LA.sd + g0], mnA = *(const floatx4 *)&iA[LA.mn + g0];
+        floatx4 tau, pf;
+        if constexpr (kPair) {
+          const floatx4 bB = *(const floatx4 *)&iB[LB.b3 + g0];
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            float t = sdA[i] * (yA[4 * b + i] + bA[i]);
+            t = t + mnA[i];
+            const float p = yB[4 * b + i] + bB[i];
+            tau[i] = pow8(t) * cd;
+            pf[i] = p * p;
+          }
+          const uint32_t off = g0 < ngpt ? vrow + 4u * (uint32_t)g0 : kOOB;
+#ifdef RRTMGPNN_ABL_MLP32_NOSTORE  // ablation only: stores dropped unless a value is a nan
+          const bool keep = tau[0] != tau[0] || pf[0] != pf[0];
+          o0.st4(tau, keep ? off : kOOB);
+          o1.st4(pf, keep ? off : kOOB);
+#else
+          o0.st4(tau, off);
+          o1.st4(pf, off);
+#endif
+        } else {  // MLP_LW_BOTH: outputs [0, ngpt) -> tau, [ngpt, 2 ngpt) -> pfrac (mo_gas_optics_kernels.F90:754-766)
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const float y = yA[4 * b + i] + bA[i];
+            float t = sdA[i] * y;
+            t = t + mnA[i];
+            tau[i] = pow8(t) * cd;
+            pf[i] = y * y;
+          }
+          o0.st4(tau, g0 < ngpt ? vrow + 4u * (uint32_t)g0 : kOOB);
+          o1.st4(pf, g0 >= ngpt && g0 < 2 * ngpt ? vrow + 4u * (uint32_t)(g0 - ngpt) : kOOB);
+        }
+      }
+    };
+#pragma unroll RRTMGPNN_MLP32_UNROLL
+    for (int go = 0; go < NGT; go++) out_tile(go);
+  }
+}
+
+template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN>
+static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
+{
+  auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN>;
+  const size_t lds = sizeof(float) * (size_t)(a.imgA_floats + (MODE == MLP_LW_PAIR ? a.imgB_floats : 0));
+  if (lds > 160 * 1024) return RRTMGPNN_ERR_UNSUPPORTED;
+  if (lds > 64 * 1024)
+    if (int rc = raise_lds_limit((const void *)kern)) return rc;
+  const long long ntiles = ((long long)a.nbatch + 31) / 32;
+  const int wpb = kMlp32Threads / 64;
+  const int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / kMlp32Threads);
+  const long long want = (ntiles + wpb - 1) / wpb;
+  const long long grid = std::max<long long>(1, std::min<long long>(want, (long long)ctx->num_cus * per_cu));
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kMlp32Threads), lds, ctx->stream, a);
+  RRTMGPNN_LAUNCH_CHECK("mlp32_kernel");
+  return RRTMGPNN_OK;
+}
+
+// RRTMGPNN_MLP32=0 in the environment selects the 16x16x4 kernel for every network (A/B runs); read once
+static bool mlp32_enabled()
+{
+  static const bool on = [] {
+    const char *e = std::getenv("RRTMGPNN_MLP32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static bool shape32(const rrtmgpnn_network *n, int KS, int HT1, int N2, int HT2, int N3, int NGT)
+{
+  return n && n->d_packed32 && n->s32[0] == KS && n->s32[1] == HT1 && n->s32[2] == N2 && n->s32[3] == HT2 &&
+         n->s32[4] == N3 && n->s32[5] == NGT;
+}
+
+// The LW modes on the 32x32x2 kernel for the shipped shapes with the shipped activations (softsign, softsign,
+// linear); RRTMGPNN_ERR_UNSUPPORTED (no error set) otherwise, and the caller runs the 16x16x4 kernel.
+int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
+                 long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
+                 const MlpInputs *in)
+{
+  if (!mlp32_enabled() || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH)) return RRTMGPNN_ERR_UNSUPPORTED;
+  auto std_acts = [](const rrtmgpnn_network *n) {
+    return n->act[0] == RRTMGPNN_ACT_SOFTSIGN && n->act[1] == RRTMGPNN_ACT_SOFTSIGN && n->act[2] == RRTMGPNN_ACT_LINEAR;
+  };
+  if (!A || !std_acts(A) || (mode == MLP_LW_PAIR && (!B || !std_acts(B)))) return RRTMGPNN_ERR_UNSUPPORTED;
+  Mlp32Args a{};
+  a.x = x; a.col_dry = col_dry; a.out0 = out0; a.out1 = out1;
+  a.imgA = A->d_packed32; a.imgA_floats = A->packed32_floats;
+  a.imgB = mode == MLP_LW_PAIR ? B->d_packed32 : nullptr;
+  a.imgB_floats = mode == MLP_LW_PAIR ? B->packed32_floats : 0;
+  a.nx = A->dims[0]; a.ngpt = ngpt;
+  if (in) {
+    a.play = in->play; a.tlay = in->tlay; a.plev = in->plev; a.h2o = in->h2o; a.nlay = in->nlay;
+    a.gas = in->gas;
+  }
+  a.ncol = in && in->nlay > 0 ? (int)(nbatch / in->nlay) : 0;
+  // 16-byte stores, and every descriptor's range below kOOB
+  auto al16 = [](const float *p) { return ((uintptr_t)p & 15) == 0; };
+  if (ngpt % 4 != 0 || !al16(out0) || !out1 || !al16(out1)) return RRTMGPNN_ERR_UNSUPPORTED;
+  if ((unsigned long long)nbatch * 4ull * (unsigned long long)std::max(1, A->dims[0]) >= kMaxRecords ||
+      32ull * 4ull * (unsigned long long)ngpt >= kMaxRecords)
+    return RRTMGPNN_ERR_UNSUPPORTED;
+  if (in && (unsigned long long)(nbatch / std::max(1, in->nlay) + 1) * (in->nlay + 1) * 4ull >= kMaxRecords)
+    return RRTMGPNN_ERR_UNSUPPORTED;
+  a.nbatch = (int)nbatch;
+  const bool xin = in != nullptr;
+  if (in)  // the kernel scales with A's image: it must hold the constants the caller passed
+    for (int k = 0; k < a.nx; k++)
+      if (k >= (int)A->in_min.size() || k >= (int)A->in_max.size() || A->in_min[k] != in->mn[k] ||
+          A->in_max[k] != in->mx[k])
+        return RRTMGPNN_ERR_UNSUPPORTED;
+  if (in)
+    for (int k = 0; k < kMaxInputs; k++) {
+      const int nd = in->gas.nd[k];
+      const bool on = k < a.nx && in->gas.p[k];
+      a.gsm[k] = nd == 2 ? 4u : 0u;
+      a.glm[k] = nd == 1 ? 4u : 0u;
+      a.grec[k] = !on ? 0u : (nd == 2 ? 4u * (uint32_t)nbatch : (nd == 1 ? 4u * (uint32_t)in->nlay : 4u));
+    }
+  if (mode == MLP_LW_PAIR && shape32(A, 9, 2, 29, 2, 29, 8) && shape32(B, 9, 1, 8, 1, 8, 8)) {
+    // the shipped g256 pair: absorption 18-58-58-256, Planck fraction 18-16-16-256
+    if (xin) return launch32<9, 2, 29, 2, 29, 1, 8, 1, 8, 8, MLP_LW_PAIR, true>(ctx, a);
+    return launch32<9, 2, 29, 2, 29, 1, 8, 1, 8, 8, MLP_LW_PAIR, false>(ctx, a);
+  }
+  if (mode == MLP_LW_BOTH && !xin && shape32(A, 9, 2, 32, 2, 32, 8)) {
+    // the shipped g128 single model: 18-64-64-256
+    return launch32<9, 2, 32, 2, 32, 1, 1, 1, 1, 8, MLP_LW_BOTH, false>(ctx, a);
+  }
+  return RRTMGPNN_ERR_UNSUPPORTED;
+}
+
+}  // namespace rrtmgpnn

@@ -188,4 +188,38 @@ __device__ __forceinline__ float ref_logf(float x)
   return (float)y;
 }
 
+// ref_logf without branches (the fused MLP kernel's input scaling, where a branch would split the tile body): glibc's
+// main path on the (normalised) argument, the special cases selected afterwards.  Same result as ref_logf for every
+// input.
+__device__ __forceinline__ float ref_logf_nb(float x)
+{
+  const double Ln2 = 0x1.62e42fefa39efp-1;
+  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  const uint32_t ix0 = __float_as_uint(x);
+  const bool special = ix0 - 0x00800000u >= 0x7f800000u - 0x00800000u;
+  // a positive subnormal is normalised as glibc does; other specials take the main path on a harmless value
+  const uint32_t ixs = __float_as_uint(x * 0x1p23f) - (23u << 23);
+  const bool subn = special && !(ix0 & 0x80000000u) && ix0 * 2 != 0 && ix0 < 0x00800000u;
+  const uint32_t ix = subn ? ixs : (special ? 0x3f800000u : ix0);
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> 19) % 16);
+  const int k = (int)tmp >> 23;
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  const double invc = kLogTab[i].invc, logc = kLogTab[i].logc;
+  const double z = (double)__uint_as_float(iz);
+  const double r = __fma_rn(z, invc, -1.0);
+  const double y0 = __fma_rn((double)k, Ln2, logc);
+  const double r2 = r * r;
+  double y = __fma_rn(A1, r, A2);
+  y = __fma_rn(A0, r2, y);
+  y = __fma_rn(y, r2, y0 + r);
+  float res = (float)y;
+  res = ix0 == 0x3f800000u ? 0.0f : res;
+  const float sp = ix0 * 2 == 0 ? __int_as_float(0xff800000)
+                   : ix0 == 0x7f800000u ? x
+                   : ((ix0 & 0x80000000u) || ix0 * 2 >= 0xff000000u) ? __int_as_float(0x7fc00000)
+                                                                      : res;
+  return special && !subn ? sp : res;
+}
+
 }  // namespace rrtmgpnn
