@@ -17,6 +17,7 @@ namespace rrtmgpnn {
 
 static thread_local std::string g_last_error;
 int g_sw_kernel_default = 0;
+int g_mlp_kernel_default = 0;
 
 void set_error(const std::string &msg) { g_last_error = msg; }
 
@@ -187,6 +188,18 @@ int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode)
   }
   if (int rc = check_ctx(ctx)) return rc;
   ctx->sw_kernel = mode;
+  return RRTMGPNN_OK;
+}
+
+int rrtmgpnn_context_set_mlp_kernel(rrtmgpnn_context *ctx, int mode)
+{
+  if (mode < 0 || mode > 1) return fail(RRTMGPNN_ERR_ARGUMENT, "mlp kernel mode must be 0 or 1");
+  if (!ctx) {
+    rrtmgpnn::g_mlp_kernel_default = mode;
+    return RRTMGPNN_OK;
+  }
+  if (int rc = check_ctx(ctx)) return rc;
+  ctx->mlp_kernel = mode;
   return RRTMGPNN_OK;
 }
 

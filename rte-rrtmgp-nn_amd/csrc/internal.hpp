@@ -35,6 +35,7 @@ constexpr int kMaxLayers = 7;   // network layers (excluding input)
 constexpr int kMaxInputs = 32;  // NN input features
 constexpr int kMaxBands = 64;
 extern int g_sw_kernel_default;  // rrtmgpnn_context_set_sw_kernel(NULL, mode)
+extern int g_mlp_kernel_default;  // rrtmgpnn_context_set_mlp_kernel(NULL, mode)
 // Raise a kernel's dynamic-LDS limit to 160 KiB on the current device, once per (kernel, device): a function
 // attribute is per device, so a second GPU of the same process gets its own call.  Thread-safe; after the first
 // call for a (kernel, device) pair it makes no HIP call (hipGraph captures stay attribute-free).
@@ -53,6 +54,7 @@ struct rrtmgpnn_context {
   bool own_stream = false;
   int num_cus = 256;
   int sw_kernel = -1;  // SW two-stream kernel: 0 by ngpt, 1 / 2 g-points per lane, -1 the library default
+  int mlp_kernel = -1;  // LW network tiling: 0 32x32x2 where instantiated, 1 16x16x4, -1 the library default
   void *ws = nullptr;
   size_t ws_bytes = 0;
   bool ws_pinned = false;

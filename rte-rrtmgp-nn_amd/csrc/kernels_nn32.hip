@@ -412,7 +412,8 @@ static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
   return RRTMGPNN_OK;
 }
 
-// RRTMGPNN_MLP32=0 in the environment selects the 16x16x4 kernel for every network (A/B runs); read once
+// RRTMGPNN_MLP32=0 in the environment selects the 16x16x4 kernel for every network (whole-process A/B runs; read
+// once); rrtmgpnn_context_set_mlp_kernel selects per context
 static bool mlp32_enabled()
 {
   static const bool on = [] {
@@ -434,7 +435,8 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
                  long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
                  const MlpInputs *in)
 {
-  if (!mlp32_enabled() || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH)) return RRTMGPNN_ERR_UNSUPPORTED;
+  const int kmode = ctx->mlp_kernel >= 0 ? ctx->mlp_kernel : g_mlp_kernel_default;
+  if (kmode == 1 || !mlp32_enabled() || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH)) return RRTMGPNN_ERR_UNSUPPORTED;
   auto std_acts = [](const rrtmgpnn_network *n) {
     return n->act[0] == RRTMGPNN_ACT_SOFTSIGN && n->act[1] == RRTMGPNN_ACT_SOFTSIGN && n->act[2] == RRTMGPNN_ACT_LINEAR;
   };

@@ -63,12 +63,22 @@ class Context:
         """0: SW two-stream kernel by ngpt (two g-points per lane when even; default); 1 / 2: one / two (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_sw_kernel(self.h, int(mode)), "context_set_sw_kernel")
 
+    def set_mlp_kernel(self, mode):
+        """0: the LW networks on 32x32x2 MFMA tiles where instantiated (default); 1: 16x16x4 (bit-identical)."""
+        check(_lib.lib().rrtmgpnn_context_set_mlp_kernel(self.h, int(mode)), "context_set_mlp_kernel")
+
     def __del__(self):
         try:
             if getattr(self, "h", None):
                 _lib.lib().rrtmgpnn_context_destroy(self.h)
         except Exception:
             pass
+
+
+def set_mlp_kernel_default(mode):
+    """The LW networks' MFMA tiling of every context not set itself: 0 32x32x2 where instantiated (the default),
+    1 16x16x4 (bit-identical outputs; tests force each)."""
+    check(_lib.lib().rrtmgpnn_context_set_mlp_kernel(None, int(mode)), "context_set_mlp_kernel")
 
 
 def set_sw_kernel_default(mode):

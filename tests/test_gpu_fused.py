@@ -107,7 +107,7 @@ def test_fused_step_equals_class_sequence(dev, rfmip):
 
 
 @pytest.mark.parametrize("ncol", [1, 37, 1800])
-def test_fused_gas_optics_equals_separate_calls(dev, rfmip, ncol):
+def test_fused_gas_optics_equals_separate_calls(dev, rfmip, ncol, mlp_kernel):
     """rrtmgpnn_gas_optics_{lw,sw}_nn (network inputs and col_dry formed inside the MLP kernel) == compute_nn_inputs +
     get_col_dry + predict_nn_{lw,sw}, bit for bit; the LW g128 'both' model (no in-kernel instance) takes the
     fallback through the context workspace and matches too."""

@@ -101,7 +101,7 @@ def test_gas_optics_without_tlev_matches_oracle(dev, orc, rfmip, models, top_at_
     np.testing.assert_array_equal(src.sfc_source.cpu().numpy(), ref["sfc_source"])
 
 
-def test_lw_gas_optics_user_col_dry(dev, orc, rfmip, models):
+def test_lw_gas_optics_user_col_dry(dev, orc, rfmip, models, mlp_kernel):
     from rrtmgpnn import data
     prob = subset(rfmip, np.arange(2, 1800, 11))
     rng = np.random.default_rng(5)
@@ -158,7 +158,7 @@ def test_class_layer_scalar_and_1d_gases(dev, orc, rfmip, models):
 
 
 @pytest.mark.parametrize("stream", ["lw", "sw"])
-def test_fused_gas_optics_scalar_and_1d_gases(dev, orc, rfmip, models, stream):
+def test_fused_gas_optics_scalar_and_1d_gases(dev, orc, rfmip, models, stream, mlp_kernel):
     """rrtmgpnn_gas_optics_{lw,sw}_nn (the benchmarked entries) with gas_ndims 0 and 1."""
     from rrtmgpnn import _lib, data
     from rrtmgpnn._lib import check, int_array, ptr_array
@@ -207,7 +207,7 @@ def test_fused_gas_optics_scalar_and_1d_gases(dev, orc, rfmip, models, stream):
 
 
 @pytest.mark.parametrize("fused", [False, True])
-def test_both_model_matches_oracle(dev, orc, rfmip, models, fused):
+def test_both_model_matches_oracle(dev, orc, rfmip, models, fused, mlp_kernel):
     """The g128 single-model network (2*128 outputs): tau and pfrac split as mo_gas_optics_kernels.F90:744-772."""
     from rrtmgpnn import _lib, data
     from rrtmgpnn._lib import check, int_array, ptr_array

@@ -62,7 +62,7 @@ def test_mlp_forward_matches_oracle(dev, orc, models, name, nbatch):
     np.testing.assert_array_equal(y, orc.mlp(m, x))  # bit-identical MFMA chain
 
 
-def test_lw_gas_optics_matches_oracle(dev, orc, rfmip, models):
+def test_lw_gas_optics_matches_oracle(dev, orc, rfmip, models, mlp_kernel):
     from rrtmgpnn import api, data
     prob = subset(rfmip, np.arange(0, 1800, 7))
     ncol, nlay = prob["ncol"], prob["nlay"]
@@ -219,7 +219,7 @@ def _check_pipeline(got, ref, usecol):
         assert_flux(g, r, k)
 
 
-def test_full_rfmip_clear_sky_lw_sw(dev, orc, rfmip, models, sw_kernel):
+def test_full_rfmip_clear_sky_lw_sw(dev, orc, rfmip, models, sw_kernel, mlp_kernel):
     """C3 (all 1800 RFMIP columns): the benchmarked step vs the oracle, plus heating-rate agreement."""
     from rrtmgpnn.pipeline import ClearSkyStep
     step = ClearSkyStep(rfmip, device=0)
