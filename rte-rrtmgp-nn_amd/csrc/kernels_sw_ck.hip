@@ -117,8 +117,15 @@ constexpr bool kCkKeepD = RRTMGPNN_SWCK_KEEPD != 0;
 constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
 static_assert(kCkRing % kCkK == 0, "the flux ring must hold whole chunks");
 
+// Waves per SIMD of the clear-sky NN instance (g = NULL, no increment), which needs fewer registers: at 4 (128 VGPRs,
+// 2 spilled) the C3 grid (900 blocks of 4 waves) is resident at once instead of 768 + a second round of 132; SW solver
+// -2.5 % at C3, step -0.7 %, C5 shard equal (tools/gpu_ab.sh, round 2)
+#ifndef RRTMGPNN_SWCK_WAVES_NN
+#define RRTMGPNN_SWCK_WAVES_NN 4
+#endif
+
 template <bool kHasG, bool kInc, int K>
-__global__ void __launch_bounds__(512, RRTMGPNN_SWCK_WAVES)
+__global__ void __launch_bounds__(512, (!kHasG && !kInc) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
                          const float *__restrict__ ssa, const float *__restrict__ gg, const float *__restrict__ mu0p,
