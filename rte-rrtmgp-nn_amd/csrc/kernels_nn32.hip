@@ -150,6 +150,10 @@ struct Buf {
   {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0));
   }
+  __device__ __forceinline__ void st(float v, uint32_t voff) const
+  {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, 0, 0);
+  }
   __device__ __forceinline__ void st4(const floatx4 &v, uint32_t voff) const
   {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
@@ -196,6 +200,26 @@ __device__ __forceinline__ floatx16 mfma_chain(const float *__restrict__ w, int 
   return acc;
 }
 
+// The output layer with the operands swapped: A = the layer-2 activations (lane (j, h): sample j, unit 2S+h, exactly
+// the registers the B operand takes), B = the weights (lane (i, h): unit 2S+h, g-point 32go+i, exactly the image the A
+// operand takes), so D = Y (samples x g-points): lane (c, h) holds g-point 32go + c of samples (r&3) + 8(r>>2) + 4h,
+// and a store of one register writes two 128-byte row segments instead of 32 pieces of 32 bytes.  Same k order.
+template <int NS>
+__device__ __forceinline__ floatx16 mfma_chain_t(const float *__restrict__ w, int tile, const float (&v)[NS], int lane)
+{
+  constexpr int Q = (NS + 3) / 4;
+  floatx16 acc = {};
+  const floatx4 *wp = (const floatx4 *)w + (size_t)tile * Q * 64 + lane;
+#pragma unroll
+  for (int g4 = 0; g4 < Q; g4++) {
+    const floatx4 wv = wp[g4 * 64];
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if (4 * g4 + e < NS) acc = mfma32(v[4 * g4 + e], wv[e], acc);
+  }
+  return acc;
+}
+
 // Hidden layers of one network for a 32-sample tile: returns the layer-2 activations as the output layer's B
 // operands (N3 K-steps)
 template <int KS, int HT1, int N2, int HT2, int N3, int NGT>
@@ -231,8 +255,9 @@ __device__ __forceinline__ void mlp32_hidden(const float *__restrict__ img, cons
 #endif
 constexpr int kMlp32Threads = RRTMGPNN_MLP32_THREADS;
 
-// A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  Outputs are stored 16 bytes
-// at a time: the host guarantees ngpt % 4 == 0 and 16-byte aligned output arrays.
+// A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  The host guarantees that the
+// g-tiles are full: ngpt = 32 NGT (LW pair) or 2 ngpt = 32 NGT (LW both).  Dynamic LDS: the weight images, then 32
+// floats per wave (the tile's column amounts, handed from the sample lanes to the row registers).
 template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN>
 __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
 {
@@ -246,6 +271,7 @@ __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
   __syncthreads();
   const float *imgA = (const float *)lds4;
   const float *imgB = imgA + a.imgA_floats;
+  float *cds = (float *)lds4 + a.imgA_floats + (kPair ? a.imgB_floats : 0);
   constexpr Img32 LA = img32_layout(KS, AH1, AN2, AH2, AN3, NGT);
   constexpr Img32 LB = img32_layout(KS, BH1, BN2, BH2, BN3, NGT);
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
@@ -342,50 +368,61 @@ __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
       const Buf bc(a.col_dry, nb4);
       cd = bc.ld(4u * (s0 + (uint32_t)j));
     }
-    // this tile's rows of the outputs: (nvalid, ngpt) floats; rows past the batch fall outside and are dropped
+    // this tile's rows of the outputs: (nvalid, ngpt) floats.  Lane (c, h) stores rows R(r) = (r&3) + 8(r>>2) + 4h at
+    // g-point 32go + c: vo[r] = its byte offset at go = 0 (go adds 128 bytes each), out of range past the batch
     const uint32_t rows = nvalid * (uint32_t)ngpt * 4u;
     const Buf o0(a.out0 + (size_t)s0 * ngpt, rows), o1(a.out1 + (size_t)s0 * ngpt, rows);
-    const uint32_t vrow = 4u * (uint32_t)j * (uint32_t)ngpt;
+    // the column amounts of rows R(r): sample j's lanes put theirs in the wave's slot, the row registers read them back
+    float *slot = cds + wave * 32;
+    slot[j] = cd;  // both lane halves write sample j's (equal) value
+    __builtin_amdgcn_wave_barrier();
+    float cdr[16];
+    uint32_t vo[16];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const floatx4 v = *(const floatx4 *)&slot[8 * b + 4 * h];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t R = (uint32_t)(8 * b + 4 * h + i);
+        cdr[4 * b + i] = v[i];
+        vo[4 * b + i] = R < nvalid ? 4u * (R * (uint32_t)ngpt + (uint32_t)j) : kOOB;
+      }
+    }
     auto out_tile = [&](int go) {
-      const floatx16 yA = mfma_chain<AN3>(iA + LA.l3, go, hA, lane);
+      const floatx16 yA = mfma_chain_t<AN3>(iA + LA.l3, go, hA, lane);
       floatx16 yB = {};
-      if constexpr (kPair) yB = mfma_chain<BN3>(iB + LB.l3, go, hB, lane);
+      if constexpr (kPair) yB = mfma_chain_t<BN3>(iB + LB.l3, go, hB, lane);
+      const int g = 32 * go + j;
+      const float bA = iA[LA.b3 + g], sdA = iA[LA.sd + g], mnA = iA[LA.mn + g];
+      if constexpr (kPair) {
+        const float bB = iB[LB.b3 + g];
 #pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int g0 = 32 * go + 8 * b + 4 * h;
-        const floatx4 bA = *(const floatx4 *)&iA[LA.b3 + g0];
-        const floatx4 sdA = *(const floatx4 *)&iA[LA.sd + g0], mnA = *(const floatx4 *)&iA[LA.mn + g0];
-        floatx4 tau, pf;
-        if constexpr (kPair) {
-          const floatx4 bB = *(const floatx4 *)&iB[LB.b3 + g0];
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            float t = sdA[i] * (yA[4 * b + i] + bA[i]);
-            t = t + mnA[i];
-            const float p = yB[4 * b + i] + bB[i];
-            tau[i] = pow8(t) * cd;
-            pf[i] = p * p;
-          }
-          const uint32_t off = g0 < ngpt ? vrow + 4u * (uint32_t)g0 : kOOB;
+        for (int r = 0; r < 16; r++) {
+          float t = sdA * (yA[r] + bA);
+          t = t + mnA;
+          const float p = yB[r] + bB;
+          const float tau = pow8(t) * cdr[r], pf = p * p;
 #ifdef RRTMGPNN_ABL_MLP32_NOSTORE  // ablation only: stores dropped unless a value is a nan
-          const bool keep = tau[0] != tau[0] || pf[0] != pf[0];
-          o0.st4(tau, keep ? off : kOOB);
-          o1.st4(pf, keep ? off : kOOB);
+          const uint32_t off = (tau != tau || pf != pf) ? vo[r] + 128u * go : kOOB;
 #else
-          o0.st4(tau, off);
-          o1.st4(pf, off);
+          const uint32_t off = vo[r] + 128u * go;
 #endif
-        } else {  // MLP_LW_BOTH: outputs [0, ngpt) -> tau, [ngpt, 2 ngpt) -> pfrac (mo_gas_optics_kernels.F90:754-766)
+          o0.st(tau, off);
+          o1.st(pf, off);
+        }
+      } else {  // MLP_LW_BOTH: outputs [0, ngpt) -> tau, [ngpt, 2 ngpt) -> pfrac (mo_gas_optics_kernels.F90:754-766);
+                // ngpt % 32 == 0, so a g-tile is all tau or all pfrac
+        const bool is_tau = 32 * go < ngpt;
+        const uint32_t gshift = is_tau ? 0u : 4u * (uint32_t)ngpt;
 #pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const float y = yA[4 * b + i] + bA[i];
-            float t = sdA[i] * y;
-            t = t + mnA[i];
-            tau[i] = pow8(t) * cd;
-            pf[i] = y * y;
-          }
-          o0.st4(tau, g0 < ngpt ? vrow + 4u * (uint32_t)g0 : kOOB);
-          o1.st4(pf, g0 >= ngpt && g0 < 2 * ngpt ? vrow + 4u * (uint32_t)(g0 - ngpt) : kOOB);
+        for (int r = 0; r < 16; r++) {
+          const float y = yA[r] + bA;
+          float t = sdA * y;
+          t = t + mnA;
+          const float tau = pow8(t) * cdr[r], pf = y * y;
+          const uint32_t off = vo[r] + 128u * go - gshift;
+          o0.st(tau, is_tau ? off : kOOB);
+          o1.st(pf, is_tau ? kOOB : off);
         }
       }
     };
@@ -398,7 +435,8 @@ template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2,
 static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
 {
   auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN>;
-  const size_t lds = sizeof(float) * (size_t)(a.imgA_floats + (MODE == MLP_LW_PAIR ? a.imgB_floats : 0));
+  const size_t lds = sizeof(float) * ((size_t)(a.imgA_floats + (MODE == MLP_LW_PAIR ? a.imgB_floats : 0)) +
+                                      32 * (kMlp32Threads / 64));
   if (lds > 160 * 1024) return RRTMGPNN_ERR_UNSUPPORTED;
   if (lds > 64 * 1024)
     if (int rc = raise_lds_limit((const void *)kern)) return rc;
@@ -454,7 +492,8 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
   a.ncol = in && in->nlay > 0 ? (int)(nbatch / in->nlay) : 0;
   // 16-byte stores, and every descriptor's range below kOOB
   auto al16 = [](const float *p) { return ((uintptr_t)p & 15) == 0; };
-  if (ngpt % 4 != 0 || !al16(out0) || !out1 || !al16(out1)) return RRTMGPNN_ERR_UNSUPPORTED;
+  if (ngpt % 32 != 0 || !al16(out0) || !out1 || !al16(out1)) return RRTMGPNN_ERR_UNSUPPORTED;
+  if (A->s32[5] * 32 != (mode == MLP_LW_PAIR ? ngpt : 2 * ngpt)) return RRTMGPNN_ERR_UNSUPPORTED;  // full g-tiles
   if ((unsigned long long)nbatch * 4ull * (unsigned long long)std::max(1, A->dims[0]) >= kMaxRecords ||
       32ull * 4ull * (unsigned long long)ngpt >= kMaxRecords)
     return RRTMGPNN_ERR_UNSUPPORTED;
