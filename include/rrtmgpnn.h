@@ -57,9 +57,10 @@ int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream);
  * checkpointed passes (beam / adding state stored every 3 levels instead of per level).  2 and 3 need even ngpt.
  * All kernels give bit-identical fluxes.  ctx == NULL sets the default of every context not set itself. */
 int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode);
-/* MI355X tuning, no reference counterpart: the MFMA tiling of the LW networks (rrtmgpnn_predict_nn_lw,
- * rrtmgpnn_gas_optics_lw_nn).  0 (default): v_mfma_f32_32x32x2_f32 tiles where an instance exists for the networks
- * (the shipped g256 pair and g128 single model, softsign/softsign/linear), 16x16x4 otherwise.  1: 16x16x4 tiles.
+/* MI355X tuning, no reference counterpart: the MFMA tiling of the gas-optics networks (rrtmgpnn_predict_nn_lw/_sw,
+ * rrtmgpnn_gas_optics_lw_nn/_sw_nn).  0 (default): v_mfma_f32_32x32x2_f32 tiles where an instance exists for the
+ * networks (the shipped LW g256 pair, LW g128 single model and SW g224 pair, softsign/softsign/linear), 16x16x4
+ * otherwise.  1: 16x16x4 tiles.
  * Bit-identical outputs either way.  ctx == NULL sets the default of every context not set itself. */
 int rrtmgpnn_context_set_mlp_kernel(rrtmgpnn_context *ctx, int mode);
 void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx);

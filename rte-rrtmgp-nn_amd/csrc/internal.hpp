@@ -163,12 +163,12 @@ int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, c
 int launch_mlp_generic(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch, const float *x,
                        float *out);
 int pack_network(rrtmgpnn_network *net);
-// kernels_nn32.hip: the LW modes on v_mfma_f32_32x32x2_f32; RRTMGPNN_ERR_UNSUPPORTED (no error set) when no instance
+// kernels_nn32.hip: the LW pair, LW both and SW pair modes on v_mfma_f32_32x32x2_f32; RRTMGPNN_ERR_UNSUPPORTED (no error set) when no instance
 // exists for the networks (launch_mlp then runs the 16x16x4 kernel)
 int pack_network32(rrtmgpnn_network *net);
 int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
                  long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
-                 const MlpInputs *in);
+                 float *out2, const MlpInputs *in);
 // kernels_rte.hip
 struct BandArgs {
   int lims[2 * kMaxBands];

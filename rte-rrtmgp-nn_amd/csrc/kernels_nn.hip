@@ -663,8 +663,8 @@ int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, c
                const MlpInputs *in)
 {
   if (nbatch <= 0) return RRTMGPNN_OK;
-  if (mode == MLP_LW_PAIR || mode == MLP_LW_BOTH) {  // the 32x32x2 kernel first (kernels_nn32.hip)
-    const int rc = launch_mlp32(ctx, mode, A, B, nbatch, ngpt, x, col_dry, out0, out1, in);
+  if (mode == MLP_LW_PAIR || mode == MLP_LW_BOTH || mode == MLP_SW_PAIR) {  // the 32x32x2 kernel first (kernels_nn32.hip)
+    const int rc = launch_mlp32(ctx, mode, A, B, nbatch, ngpt, x, col_dry, out0, out1, out2, in);
     if (rc != RRTMGPNN_ERR_UNSUPPORTED) return rc;
   }
   if (!A || !A->d_packed) return fail(RRTMGPNN_ERR_UNSUPPORTED, "mlp: network has no MFMA image (needs 3 layers)");

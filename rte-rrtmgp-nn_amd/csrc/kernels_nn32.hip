@@ -164,7 +164,7 @@ struct Buf {
 struct Mlp32Args {
   const float *x;        // (nx, nbatch)
   const float *col_dry;  // (nbatch)
-  float *out0, *out1;
+  float *out0, *out1, *out2;
   const float *imgA, *imgB;
   int imgA_floats, imgB_floats;
   int nx, ngpt;
@@ -261,7 +261,7 @@ constexpr int kMlp32Threads = RRTMGPNN_MLP32_THREADS;
 template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN>
 __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
 {
-  constexpr bool kPair = MODE == MLP_LW_PAIR;
+  constexpr bool kPair = MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR;
   extern __shared__ floatx4 lds4[];
   {
     const int n4 = (a.imgA_floats + (kPair ? a.imgB_floats : 0)) / 4, nA4 = a.imgA_floats / 4;
@@ -372,6 +372,8 @@ __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
     // g-point 32go + c: vo[r] = its byte offset at go = 0 (go adds 128 bytes each), out of range past the batch
     const uint32_t rows = nvalid * (uint32_t)ngpt * 4u;
     const Buf o0(a.out0 + (size_t)s0 * ngpt, rows), o1(a.out1 + (size_t)s0 * ngpt, rows);
+    // SW: g (zero) when the caller asked for it; an empty range drops the stores otherwise
+    const Buf o2(a.out2 ? a.out2 + (size_t)s0 * ngpt : a.out0, a.out2 ? rows : 0u);
     // the column amounts of rows R(r): sample j's lanes put theirs in the wave's slot, the row registers read them back
     float *slot = cds + wave * 32;
     slot[j] = cd;  // both lane halves write sample j's (equal) value
@@ -394,7 +396,25 @@ __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
       if constexpr (kPair) yB = mfma_chain_t<BN3>(iB + LB.l3, go, hB, lane);
       const int g = 32 * go + j;
       const float bA = iA[LA.b3 + g], sdA = iA[LA.sd + g], mnA = iA[LA.mn + g];
-      if constexpr (kPair) {
+      if constexpr (MODE == MLP_SW_PAIR) {
+        // tau = tau_abs + tau_ray, ssa = tau_ray / tau, g = 0 (predict_nn_sw_blas with the combine,
+        // rrtmgp/kernels/mo_gas_optics_kernels.F90:869-953; mo_gas_optics_rrtmgp.F90:560-567)
+        const float bB = iB[LB.b3 + g], sdB = iB[LB.sd + g], mnB = iB[LB.mn + g];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          float ta = sdA * (yA[r] + bA);
+          ta = ta + mnA;
+          const float vabs = pow8(ta) * cdr[r];
+          float tr = sdB * (yB[r] + bB);
+          tr = tr + mnB;
+          const float vray = pow8(tr) * cdr[r];
+          const float tot = vabs + vray, ssa = vray / tot;
+          const uint32_t off = vo[r] + 128u * go;
+          o0.st(tot, off);
+          o1.st(ssa, off);
+          o2.st(0.0f, off);
+        }
+      } else if constexpr (kPair) {
         const float bB = iB[LB.b3 + g];
 #pragma unroll
         for (int r = 0; r < 16; r++) {
@@ -435,7 +455,7 @@ template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2,
 static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
 {
   auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN>;
-  const size_t lds = sizeof(float) * ((size_t)(a.imgA_floats + (MODE == MLP_LW_PAIR ? a.imgB_floats : 0)) +
+  const size_t lds = sizeof(float) * ((size_t)(a.imgA_floats + (MODE != MLP_LW_BOTH ? a.imgB_floats : 0)) +
                                       32 * (kMlp32Threads / 64));
   if (lds > 160 * 1024) return RRTMGPNN_ERR_UNSUPPORTED;
   if (lds > 64 * 1024)
@@ -471,19 +491,21 @@ static bool shape32(const rrtmgpnn_network *n, int KS, int HT1, int N2, int HT2,
 // linear); RRTMGPNN_ERR_UNSUPPORTED (no error set) otherwise, and the caller runs the 16x16x4 kernel.
 int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
                  long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
-                 const MlpInputs *in)
+                 float *out2, const MlpInputs *in)
 {
   const int kmode = ctx->mlp_kernel >= 0 ? ctx->mlp_kernel : g_mlp_kernel_default;
-  if (kmode == 1 || !mlp32_enabled() || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH)) return RRTMGPNN_ERR_UNSUPPORTED;
+  if (kmode == 1 || !mlp32_enabled() || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH && mode != MLP_SW_PAIR))
+    return RRTMGPNN_ERR_UNSUPPORTED;
+  const bool pair = mode != MLP_LW_BOTH;
   auto std_acts = [](const rrtmgpnn_network *n) {
     return n->act[0] == RRTMGPNN_ACT_SOFTSIGN && n->act[1] == RRTMGPNN_ACT_SOFTSIGN && n->act[2] == RRTMGPNN_ACT_LINEAR;
   };
-  if (!A || !std_acts(A) || (mode == MLP_LW_PAIR && (!B || !std_acts(B)))) return RRTMGPNN_ERR_UNSUPPORTED;
+  if (!A || !std_acts(A) || (pair && (!B || !std_acts(B)))) return RRTMGPNN_ERR_UNSUPPORTED;
   Mlp32Args a{};
-  a.x = x; a.col_dry = col_dry; a.out0 = out0; a.out1 = out1;
+  a.x = x; a.col_dry = col_dry; a.out0 = out0; a.out1 = out1; a.out2 = out2;
   a.imgA = A->d_packed32; a.imgA_floats = A->packed32_floats;
-  a.imgB = mode == MLP_LW_PAIR ? B->d_packed32 : nullptr;
-  a.imgB_floats = mode == MLP_LW_PAIR ? B->packed32_floats : 0;
+  a.imgB = pair ? B->d_packed32 : nullptr;
+  a.imgB_floats = pair ? B->packed32_floats : 0;
   a.nx = A->dims[0]; a.ngpt = ngpt;
   if (in) {
     a.play = in->play; a.tlay = in->tlay; a.plev = in->plev; a.h2o = in->h2o; a.nlay = in->nlay;
@@ -493,7 +515,8 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
   // 16-byte stores, and every descriptor's range below kOOB
   auto al16 = [](const float *p) { return ((uintptr_t)p & 15) == 0; };
   if (ngpt % 32 != 0 || !al16(out0) || !out1 || !al16(out1)) return RRTMGPNN_ERR_UNSUPPORTED;
-  if (A->s32[5] * 32 != (mode == MLP_LW_PAIR ? ngpt : 2 * ngpt)) return RRTMGPNN_ERR_UNSUPPORTED;  // full g-tiles
+  if (A->s32[5] * 32 != (pair ? ngpt : 2 * ngpt) || (pair && B->s32[5] != A->s32[5]))
+    return RRTMGPNN_ERR_UNSUPPORTED;  // full g-tiles
   if ((unsigned long long)nbatch * 4ull * (unsigned long long)std::max(1, A->dims[0]) >= kMaxRecords ||
       32ull * 4ull * (unsigned long long)ngpt >= kMaxRecords)
     return RRTMGPNN_ERR_UNSUPPORTED;
@@ -518,6 +541,11 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
     // the shipped g256 pair: absorption 18-58-58-256, Planck fraction 18-16-16-256
     if (xin) return launch32<9, 2, 29, 2, 29, 1, 8, 1, 8, 8, MLP_LW_PAIR, true>(ctx, a);
     return launch32<9, 2, 29, 2, 29, 1, 8, 1, 8, 8, MLP_LW_PAIR, false>(ctx, a);
+  }
+  if (mode == MLP_SW_PAIR && shape32(A, 4, 1, 8, 1, 8, 7) && shape32(B, 4, 1, 8, 1, 8, 7)) {
+    // the shipped g224 pair: absorption and Rayleigh 7-16-16-224
+    if (xin) return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, true>(ctx, a);
+    return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, false>(ctx, a);
   }
   if (mode == MLP_LW_BOTH && !xin && shape32(A, 9, 2, 32, 2, 32, 8)) {
     // the shipped g128 single model: 18-64-64-256

@@ -64,7 +64,7 @@ class Context:
         check(_lib.lib().rrtmgpnn_context_set_sw_kernel(self.h, int(mode)), "context_set_sw_kernel")
 
     def set_mlp_kernel(self, mode):
-        """0: the LW networks on 32x32x2 MFMA tiles where instantiated (default); 1: 16x16x4 (bit-identical)."""
+        """0: the gas-optics networks on 32x32x2 MFMA tiles where instantiated (default); 1: 16x16x4 (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_mlp_kernel(self.h, int(mode)), "context_set_mlp_kernel")
 
     def __del__(self):
@@ -76,7 +76,7 @@ class Context:
 
 
 def set_mlp_kernel_default(mode):
-    """The LW networks' MFMA tiling of every context not set itself: 0 32x32x2 where instantiated (the default),
+    """The gas-optics networks' MFMA tiling of every context not set itself: 0 32x32x2 where instantiated (the default),
     1 16x16x4 (bit-identical outputs; tests force each)."""
     check(_lib.lib().rrtmgpnn_context_set_mlp_kernel(None, int(mode)), "context_set_mlp_kernel")
 

@@ -24,7 +24,7 @@ def sw_kernel(request):
 
 @pytest.fixture(params=[0, 1], ids=["mlp32", "mlp16"])
 def mlp_kernel(request):
-    """Force each MFMA tiling of the LW networks (32x32x2 where instantiated / 16x16x4) for the test, then restore
+    """Force each MFMA tiling of the gas-optics networks (32x32x2 where instantiated / 16x16x4) for the test, then restore
     the default."""
     from rrtmgpnn import api
     api.set_mlp_kernel_default(request.param)

@@ -113,7 +113,7 @@ def test_lw_gas_optics_user_col_dry(dev, orc, rfmip, models, mlp_kernel):
     np.testing.assert_array_equal(src.lay_source.cpu().numpy(), ref["lay_source"])
 
 
-def test_sw_gas_optics_user_col_dry(dev, orc, rfmip, models):
+def test_sw_gas_optics_user_col_dry(dev, orc, rfmip, models, mlp_kernel):
     from rrtmgpnn import api, data
     prob = subset(rfmip, np.arange(4, 1800, 13))
     ncol, nlay = prob["ncol"], prob["nlay"]

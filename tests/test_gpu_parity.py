@@ -87,7 +87,7 @@ def test_lw_gas_optics_matches_oracle(dev, orc, rfmip, models, mlp_kernel):
     np.testing.assert_array_equal(src.sfc_source_Jac.cpu().numpy(), ref["sfc_source_Jac"])
 
 
-def test_sw_gas_optics_matches_oracle(dev, orc, rfmip, models):
+def test_sw_gas_optics_matches_oracle(dev, orc, rfmip, models, mlp_kernel):
     from rrtmgpnn import api, data
     prob = subset(rfmip, np.arange(3, 1800, 11))
     ncol, nlay = prob["ncol"], prob["nlay"]

@@ -21,8 +21,9 @@ STAGES = [
     # mlp_pair_kernel<AK, AH1, AH2, BK, BH1, BH2, MODE, ACTS>: MODE 1 LW pair, 4 LW "both", 2 SW pair
     (re.compile(r"mlp_pair_kernel<(?:\s*\d+\s*,){6}\s*[14]\s*,"), "predict_nn_lw"),
     (re.compile(r"mlp_pair_kernel<(?:\s*\d+\s*,){6}\s*2\s*,"), "predict_nn_sw"),
-    # mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN>: the LW modes on 32x32x2 tiles
-    (re.compile(r"mlp32_kernel<"), "predict_nn_lw"),
+    # mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN>: MODE 1 LW pair, 4 LW "both", 2 SW pair
+    (re.compile(r"mlp32_kernel<(?:\s*\d+\s*,){10}\s*[14]\s*,"), "predict_nn_lw"),
+    (re.compile(r"mlp32_kernel<(?:\s*\d+\s*,){10}\s*2\s*,"), "predict_nn_sw"),
     (re.compile(r"cloud_optics_kernel"), "cloud_optics"),
     (re.compile(r"increment_bybnd_kernel"), "increment"),
     (re.compile(r"delta_scale_kernel"), "delta_scale_sw"),
