@@ -239,3 +239,37 @@ def test_captured_graph_pins_context_workspace(dev, rfmip):
     big.step()
     torch.cuda.synchronize()
     assert np.isfinite(big.fluxes()["sw_dn"]).all()
+
+def test_fused_gas_optics_special_pressures(dev, rfmip, mlp_kernel):
+    """log(play) in the fused kernels: the 32x32x2 kernel takes it through the branch-free ref_logf_nb, the separate
+    compute_nn_inputs kernel through ref_logf (glibc's branches).  With zero, negative, subnormal, one, huge, inf and
+    nan pressures in one column the two give the same tau / pfrac / ssa bits (nan where glibc's logf gives nan)."""
+    from rrtmgpnn import _lib
+    from rrtmgpnn.pipeline import ClearSkyStep
+    from rrtmgpnn._lib import check
+    prob = subset(rfmip, np.arange(37) * 11 % 1800)
+    st = ClearSkyStep(prob, device=0, fused=False, overlap=False)
+    special = np.array([0.0, -0.0, 1.0, 1e-40, 1.4e-45, 1.17549435e-38, -5.0, np.inf, -np.inf, np.nan, 3.4e38, 1e-30,
+                        0.5, 2.0, 100.0, 1.0000001], np.float32)
+    play = st.play.view(st.ncol, st.nlay)
+    play[3, :len(special)] = torch.as_tensor(special, device=dev)
+    L, c, p = _lib.lib(), st.ctx.h, (lambda t: t.data_ptr())
+    nl, nc = st.nlay, st.ncol
+    for name in ("get_col_dry", "nn_inputs_lw", "predict_nn_lw", "nn_inputs_sw", "predict_nn_sw"):
+        fn, args = next((f, a) for n, f, a in st.calls if n == name)
+        check(fn(*args), name)
+    torch.cuda.synchronize()
+    ref = [t.clone() for t in (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)]
+    got = [torch.full_like(t, 7.0) for t in ref]
+    check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, st.ng_lw, st.nx_lw, p(st.play), p(st.tlay), p(st.plev),
+                                      p(st.gases["h2o"]), st._g_lw, st._nd_lw, st._nets_lw, len(st.lw_nets),
+                                      p(got[0]), p(got[1])), "gas_optics_lw_nn")
+    check(L.rrtmgpnn_gas_optics_sw_nn(c, nc, nl, st.ng_sw, st.nx_sw, p(st.play), p(st.tlay), p(st.plev),
+                                      p(st.gases["h2o"]), st._g_sw, st._nd_sw, st._nets_sw, p(got[2]), p(got[3]), None),
+          "gas_optics_sw_nn")
+    torch.cuda.synchronize()
+    for k, (a, b) in enumerate(zip(ref, got)):
+        a, b = a.cpu().numpy(), b.cpu().numpy()
+        assert np.isnan(a).any() == np.isnan(b).any(), k
+        np.testing.assert_array_equal(a.view(np.uint32)[~np.isnan(a)], b.view(np.uint32)[~np.isnan(b)], err_msg=str(k))
+        np.testing.assert_array_equal(np.isnan(a), np.isnan(b), err_msg=str(k))
