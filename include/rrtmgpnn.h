@@ -240,6 +240,33 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
                                const float *tau, const float *ssa, const float *g, const float *mu0,
                                const float *sfc_alb_dir_gpt, const float *sfc_alb_dif_gpt,
                                float *flux_up, float *flux_dn, float *flux_dir);
+/* The solvers above with the outputs of ty_fluxes_flexible (rte/mo_fluxes.F90:57-67) and rte_lw's lw_Ds
+ * (rte/mo_rte_lw.F90:80-81, 239-246, 329-341).  gpt_flux_* (ngpt, nlay+1, ncol) device arrays, NULL for none.
+ * LW: both or neither of gpt_flux_up/dn; with one angle they receive the g-point RADIANCES and the broadband fluxes
+ * are reduced from them as lw_solver_noscat does (quirk B-5), with several angles the angle-summed fluxes.  lw_Ds
+ * (NULL: the Gauss angles): ngpt*ncol column-dependent secants read as D(igpt, icol) -- the kernel's layout; the
+ * reference's rte_lw checks the extents as (ncol, ngpt) but passes the array unchanged (quirk B-12) -- with one angle
+ * (nmus must be 1) of weight weights[0].  SW: all three of up, down (TOTAL: diffuse + direct, as the reference
+ * stores it) and direct, and the broadband down flux summed from the total (the reference's save_gpt_flux order,
+ * :660-684); even ngpt.  Bit-identical to the reference (tests/test_oracle.py, tests/test_gpu_gpt.py). */
+int rrtmgpnn_lw_solver_noscat_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                  const float *Ds, const float *weights, const float *lw_Ds, const float *inc_flux,
+                                  const float *tau, const float *lay_source, const float *lev_source,
+                                  const float *sfc_emis_gpt, const float *sfc_source, float *flux_up, float *flux_dn,
+                                  float *gpt_flux_up, float *gpt_flux_dn);
+int rrtmgpnn_lw_solver_noscat_planck_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                         const float *Ds, const float *weights, const float *lw_Ds,
+                                         const float *inc_flux, const float *tau, const float *pfrac, int nbnd,
+                                         int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
+                                         int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
+                                         float totplnk_delta, const float *totplnk, int emis_by_band,
+                                         const float *sfc_emis, float *flux_up, float *flux_dn, float *gpt_flux_up,
+                                         float *gpt_flux_dn);
+int rrtmgpnn_sw_solver_2stream_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                   const float *inc_flux, const float *inc_flux_dif, const float *tau,
+                                   const float *ssa, const float *g, const float *mu0, const float *sfc_alb_dir_gpt,
+                                   const float *sfc_alb_dif_gpt, float *flux_up, float *flux_dn, float *flux_dir,
+                                   float *gpt_flux_up, float *gpt_flux_dn, float *gpt_flux_dir);
 /* rte_sw on absorption-only (1scl) properties (rte/mo_rte_sw.F90:213-222): apply_BC_factor (top level =
  * inc_flux * mu0, rte/kernels/mo_rte_solver_kernels.F90:1685-1704) and sw_solver_noscat (:496-532), broadband direct
  * flux (nlay+1, ncol) = sum over g of each column's direct beam (sum_broadband_nocol, sequential).  The reference's

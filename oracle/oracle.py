@@ -56,6 +56,8 @@ class Oracle:
         L.orc_lw_solver_noscat_gaussquad.argtypes = [c_int, c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p,
                                                      _f32p, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_lw_solver_1rescl_gaussquad.argtypes = [c_int] * 5 + [_f32p] * 12
+        L.orc_lw_solver_noscat_ext.argtypes = [c_int] * 5 + [c_vp] * 15
+        L.orc_sw_solver_2stream_gpt.argtypes = [c_int] * 4 + [c_vp] * 14
         L.orc_lw_solver_2stream.argtypes = [c_int] * 4 + [_f32p] * 9
         L.orc_sw_solver_2stream.argtypes = [c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                             _f32p, _f32p, _f32p, _f32p, _f32p]
@@ -160,9 +162,24 @@ class Oracle:
                                     sfc, jac, lay, lev)
         return lay, lev, sfc, jac
 
-    def lw_solver(self, tau, lay, lev, emis_gpt, sfc_src, top_at_1=True, nmus=1, inc_flux=None, ssa=None, g=None):
-        """lw_solver_noscat_GaussQuad; with ssa/g the rescaled solution (do_rescaling, rte/mo_rte_lw.F90:372-387)."""
+    def lw_solver(self, tau, lay, lev, emis_gpt, sfc_src, top_at_1=True, nmus=1, inc_flux=None, ssa=None, g=None,
+                  lw_Ds=None, gpt=False):
+        """lw_solver_noscat_GaussQuad; with ssa/g the rescaled solution (do_rescaling, rte/mo_rte_lw.F90:372-387).
+        lw_Ds: rte_lw's column-dependent secants, read as D(igpt, icol) (rte/mo_rte_lw.F90:329-341; any array of
+        ngpt*ncol values, taken in memory order).  gpt: also return the g-point outputs (ncol, nlay+1, ngpt) -- with one
+        angle the radiances (quirk B-5), with several the fluxes."""
         ncol, nlay, ngpt = tau.shape
+        if lw_Ds is not None or gpt:
+            Ds, W = gauss(1 if lw_Ds is not None else nmus)
+            keep = [f32(Ds), f32(W), None if lw_Ds is None else f32(lw_Ds),
+                    f32(inc_flux) if inc_flux is not None else np.zeros((ncol, ngpt), np.float32), f32(tau),
+                    None if ssa is None else f32(ssa), None if g is None else f32(g), f32(lay), f32(lev),
+                    f32(emis_gpt), f32(sfc_src)]
+            out = [np.zeros((ncol, nlay + 1), np.float32) for _ in range(2)]
+            gp = [np.zeros((ncol, nlay + 1, ngpt), np.float32) for _ in range(2)] if gpt else [None, None]
+            self.L.orc_lw_solver_noscat_ext(ngpt, nlay, ncol, int(top_at_1), 1 if lw_Ds is not None else nmus,
+                                            *[_ptr(a) for a in keep + out + gp])
+            return (out[0], out[1], gp[0], gp[1]) if gpt else (out[0], out[1])
         Ds, W = gauss(nmus)
         up = np.zeros((ncol, nlay + 1), np.float32)
         dn = np.zeros((ncol, nlay + 1), np.float32)
@@ -186,8 +203,18 @@ class Oracle:
                                      f32(emis_gpt), f32(sfc_src), up, dn)
         return up, dn
 
-    def sw_solver(self, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True, inc_flux_dif=None):
+    def sw_solver(self, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True, inc_flux_dif=None,
+                  gpt=False):
+        """sw_solver_2stream; gpt: also the g-point up / total down / direct fluxes (ncol, nlay+1, ngpt), with the
+        broadband down flux summed as the reference does in that mode."""
         ncol, nlay, ngpt = tau.shape
+        if gpt:
+            keep = [f32(inc_flux), f32(inc_flux_dif) if inc_flux_dif is not None else np.zeros((ncol, ngpt), np.float32),
+                    f32(tau), f32(ssa), f32(g), f32(mu0), f32(alb_dir_gpt), f32(alb_dif_gpt)]
+            out = [np.zeros((ncol, nlay + 1), np.float32) for _ in range(3)]
+            gp = [np.zeros((ncol, nlay + 1, ngpt), np.float32) for _ in range(3)]
+            self.L.orc_sw_solver_2stream_gpt(ngpt, nlay, ncol, int(top_at_1), *[_ptr(a) for a in keep + out + gp])
+            return tuple(out) + tuple(gp)
         up = np.zeros((ncol, nlay + 1), np.float32)
         dn = np.zeros((ncol, nlay + 1), np.float32)
         dr = np.zeros((ncol, nlay + 1), np.float32)
@@ -370,6 +397,10 @@ class Reference:
         L.ref_delta_scale.restype = c_int
         L.ref_sw_noscat.argtypes = [c_int] * 4 + [_f32p] * 5
         L.ref_sw_noscat.restype = c_int
+        L.ref_rte_lw_gpt.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, c_int, c_int] + [_f32p] * 11
+        L.ref_rte_lw_gpt.restype = c_int
+        L.ref_rte_sw_gpt.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int] + [_f32p] * 13
+        L.ref_rte_sw_gpt.restype = c_int
 
     def sw_noscat(self, tau, mu0, inc_flux, top_at_1=True):
         """The reference's apply_BC (-> apply_BC_factor) + sw_solver_noscat kernels: broadband and spectral direct
@@ -405,6 +436,29 @@ class Reference:
                                       f32(kd["band_lims_wvn"]), int(top_at_1), nmus, f32(tau), f32(lay), f32(lev),
                                       f32(sfc_src), f32(sfc_jac), f32(sfc_emis_band), up, dn))
         return up, dn
+
+    def rte_lw_gpt(self, kd, tau, lay, lev, sfc_src, sfc_jac, sfc_emis_band, top_at_1=True, nmus=1, lw_Ds=None):
+        """rte_lw with ty_fluxes_flexible g-point outputs (ncol, nlay+1, ngpt) and optionally lw_Ds (ngpt*ncol values
+        in memory order; rte_lw sees them with the extents it checks, (ncol, ngpt))."""
+        ncol, nlay, ngpt = tau.shape
+        out = [np.zeros((ncol, nlay + 1), np.float32) for _ in range(2)]
+        gp = [np.zeros((ncol, nlay + 1, ngpt), np.float32) for _ in range(2)]
+        ds = f32(lw_Ds).ravel() if lw_Ds is not None else np.ones(ngpt * ncol, np.float32)
+        self._check(self.L.ref_rte_lw_gpt(ncol, nlay, kd["nband"], ngpt, np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                          f32(kd["band_lims_wvn"]), int(top_at_1), nmus, int(lw_Ds is not None), ds,
+                                          f32(tau), f32(lay), f32(lev), f32(sfc_src), f32(sfc_jac), f32(sfc_emis_band),
+                                          *out, *gp))
+        return out[0], out[1], gp[0], gp[1]
+
+    def rte_sw_gpt(self, kd, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True):
+        """rte_sw with ty_fluxes_flexible g-point up / down (total) / direct outputs (ncol, nlay+1, ngpt)."""
+        ncol, nlay, ngpt = tau.shape
+        out = [np.zeros((ncol, nlay + 1), np.float32) for _ in range(3)]
+        gp = [np.zeros((ncol, nlay + 1, ngpt), np.float32) for _ in range(3)]
+        self._check(self.L.ref_rte_sw_gpt(ncol, nlay, kd["nband"], ngpt, np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                          f32(kd["band_lims_wvn"]), int(top_at_1), f32(tau), f32(ssa), f32(g), f32(mu0),
+                                          f32(inc_flux), f32(alb_dir_gpt), f32(alb_dif_gpt), *out, *gp))
+        return tuple(out) + tuple(gp)
 
     def rte_sw(self, kd, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True):
         ncol, nlay, ngpt = tau.shape

@@ -143,6 +143,81 @@ contains
     ref_rte_sw = 0
   end function ref_rte_sw
 
+  ! rte_lw on 1scl properties with g-point outputs (ty_fluxes_flexible gpt_flux_up/dn associated) and, when use_ds /= 0,
+  ! the column-dependent secants lw_Ds (rte/mo_rte_lw.F90:239-246, 329-341): the extents rte_lw checks, (ncol, ngpt).
+  integer(c_int) function ref_rte_lw_gpt(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, top_at_1, nmus, &
+                                         use_ds, lw_ds, tau, lay_src, lev_src, sfc_src, sfc_src_jac, sfc_emis, &
+                                         flux_up, flux_dn, gpt_up, gpt_dn) bind(C, name="ref_rte_lw_gpt")
+    integer(c_int), value :: ncol, nlay, nband, ngpt, top_at_1, nmus, use_ds
+    integer(c_int), intent(in) :: band_lims_gpt(2, nband)
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband), lw_ds(ncol, ngpt)
+    real(c_float),  intent(in) :: tau(ngpt, nlay, ncol), lay_src(ngpt, nlay, ncol), lev_src(ngpt, nlay+1, ncol)
+    real(c_float),  intent(in) :: sfc_src(ngpt, ncol), sfc_src_jac(ngpt, ncol), sfc_emis(nband, ncol)
+    real(c_float),  intent(out), target :: flux_up(nlay+1, ncol), flux_dn(nlay+1, ncol)
+    real(c_float),  intent(out), target :: gpt_up(ngpt, nlay+1, ncol), gpt_dn(ngpt, nlay+1, ncol)
+
+    type(ty_optical_props_1scl) :: op
+    type(ty_source_func_lw)     :: src
+    type(ty_fluxes_flexible)    :: fl
+    character(len=128) :: err
+
+    ref_rte_lw_gpt = 1
+    err = op%alloc_1scl(ncol, nlay, band_lims_wvn, band_lims_gpt)
+    if (err /= '') then; last_msg = err; return; end if
+    err = src%alloc(ncol, nlay, op)
+    if (err /= '') then; last_msg = err; return; end if
+    op%tau = tau
+    src%lay_source = lay_src
+    src%lev_source = lev_src
+    src%sfc_source = sfc_src
+    src%sfc_source_Jac = sfc_src_jac
+    fl%flux_up => flux_up
+    fl%flux_dn => flux_dn
+    fl%gpt_flux_up => gpt_up
+    fl%gpt_flux_dn => gpt_dn
+    if (use_ds /= 0) then
+      err = rte_lw(op, top_at_1 /= 0, src, sfc_emis, fl, lw_Ds=lw_ds)
+    else
+      err = rte_lw(op, top_at_1 /= 0, src, sfc_emis, fl, n_gauss_angles=int(nmus), use_2stream=.false.)
+    end if
+    if (err /= '') then; last_msg = err; return; end if
+    ref_rte_lw_gpt = 0
+  end function ref_rte_lw_gpt
+
+  ! rte_sw on 2str properties with g-point outputs (save_gpt_flux, rte/mo_rte_sw.F90:155-173, 228-234)
+  integer(c_int) function ref_rte_sw_gpt(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, top_at_1, &
+                                         tau, ssa, g, mu0, inc_flux, sfc_alb_dir, sfc_alb_dif, &
+                                         flux_up, flux_dn, flux_dir, gpt_up, gpt_dn, gpt_dir) bind(C, name="ref_rte_sw_gpt")
+    integer(c_int), value :: ncol, nlay, nband, ngpt, top_at_1
+    integer(c_int), intent(in) :: band_lims_gpt(2, nband)
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband)
+    real(c_float),  intent(in) :: tau(ngpt, nlay, ncol), ssa(ngpt, nlay, ncol), g(ngpt, nlay, ncol)
+    real(c_float),  intent(in) :: mu0(ncol), inc_flux(ngpt, ncol), sfc_alb_dir(ngpt, ncol), sfc_alb_dif(ngpt, ncol)
+    real(c_float),  intent(out), target :: flux_up(nlay+1, ncol), flux_dn(nlay+1, ncol), flux_dir(nlay+1, ncol)
+    real(c_float),  intent(out), target :: gpt_up(ngpt, nlay+1, ncol), gpt_dn(ngpt, nlay+1, ncol), &
+                                           gpt_dir(ngpt, nlay+1, ncol)
+
+    type(ty_optical_props_2str) :: op
+    type(ty_fluxes_flexible)    :: fl
+    character(len=128) :: err
+
+    ref_rte_sw_gpt = 1
+    err = op%alloc_2str(ncol, nlay, band_lims_wvn, band_lims_gpt)
+    if (err /= '') then; last_msg = err; return; end if
+    op%tau = tau
+    op%ssa = ssa
+    op%g   = g
+    fl%flux_up         => flux_up
+    fl%flux_dn         => flux_dn
+    fl%flux_dn_dir     => flux_dir
+    fl%gpt_flux_up     => gpt_up
+    fl%gpt_flux_dn     => gpt_dn
+    fl%gpt_flux_dn_dir => gpt_dir
+    err = rte_sw(op, top_at_1 /= 0, mu0, inc_flux, sfc_alb_dir, sfc_alb_dif, fl)
+    if (err /= '') then; last_msg = err; return; end if
+    ref_rte_sw_gpt = 0
+  end function ref_rte_sw_gpt
+
   ! MLP chain of the reference: h = act(W^T x + b) via MKL sgemm (neural/mod_network.F90:273-354).
   ! w_all: concatenation of each layer's weights stored (n_in, n_out) C-order = w_transposed(n_out,n_in).
   integer(c_int) function ref_mlp(nlayers, dims, acts, w_all, b_all, nbatch, x, out) bind(C, name="ref_mlp")

@@ -253,7 +253,7 @@ void orc_planck_source_nn(int ncol, int nlay, int nbnd, int ngpt, int ntemp,
  * If gpt_up/gpt_dn are non-NULL the g-point radiances*fac are ACCUMULATED into them (nmus>1 path,
  * :383-412); otherwise broadband fluxes are written with the 4-way partial sums (:296-318).
  * ------------------------------------------------------------------------------------------- */
-static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weight,
+static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, const float *Dv, float weight,
                           const float *inc, const float *tau, const float *lay, const float *lev,
                           const float *emis, const float *sfc, float *radn_up, float *radn_dn,
                           float *tau_loc, float *trans, float *src_up, float *src_dn,
@@ -271,7 +271,7 @@ static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weigh
         float wb = ssal * (1.0f - gg[i]) * 0.5f;
         float scaleTau = (1.0f - ssal + wb);
         Cn[i] = 0.4f * wb / scaleTau;
-        tau_loc[i] = tau[i] * D * scaleTau;
+        tau_loc[i] = tau[i] * (Dv ? Dv[g] : D) * scaleTau;
         trans[i] = expf(-tau_loc[i]);
         An[i] = (1.0f - trans[i] * trans[i]);
       }
@@ -279,7 +279,7 @@ static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weigh
   for (int l = 0; l < nlay; l++)
     for (int g = 0; g < ngpt; g++) {
       size_t i = g + (size_t)ngpt * l;
-      tau_loc[i] = tau[i] * D;
+      tau_loc[i] = tau[i] * (Dv ? Dv[g] : D);  /* D(igpt, icol): the Gauss secant, or lw_Ds (rte/mo_rte_lw.F90:329-341) */
       trans[i] = expf(-tau_loc[i]);
     }
   for (int l = 0; l < nlay; l++)
@@ -352,13 +352,19 @@ static void lw_noscat_col(int ngpt, int nlay, int top_at_1, float D, float weigh
 
 /* lw_solver_noscat_GaussQuad :332-415 (+ lw_solver_noscat per angle); compute_Jac = false
  * (rte/mo_rte_rrtmgp_config.F90:28). Ds/weights have nmus entries.  ssa/g NULL: do_rescaling = false;
- * otherwise the rescaled solution rte_lw uses for 2str optical properties (rte/mo_rte_lw.F90:372-387). */
-void orc_lw_solver_1rescl_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
-                                    const float *Ds, const float *weights, const float *inc_flux,
-                                    const float *tau, const float *ssa, const float *g, const float *lay_source,
-                                    const float *lev_source, const float *sfc_emis, const float *sfc_source,
-                                    float *flux_up, float *flux_dn)
+ * otherwise the rescaled solution rte_lw uses for 2str optical properties (rte/mo_rte_lw.F90:372-387).
+ * lw_Ds (may be NULL): rte_lw's column-dependent secants (rte/mo_rte_lw.F90:329-341): lw_solver_noscat with one angle,
+ * D(igpt, icol) = lw_Ds[igpt + ngpt*icol] (the kernel's layout; rte_lw checks the extents as (ncol, ngpt), quirk B-12)
+ * and the weight of Ds[0]/weights[0].  gpt_up/gpt_dn (may be NULL, (ngpt, nlay+1, ncol)): save_gpt_flux -- with one
+ * angle the g-point RADIANCES (radn_up => flux_up_gpt, no fac: quirk B-5, :183-196, :262-267), with several the
+ * fluxes sum over angles of fac*radn (:383-407). */
+void orc_lw_solver_noscat_ext(int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
+                              const float *weights, const float *lw_Ds, const float *inc_flux, const float *tau,
+                              const float *ssa, const float *g, const float *lay_source, const float *lev_source,
+                              const float *sfc_emis, const float *sfc_source, float *flux_up, float *flux_dn,
+                              float *gpt_up, float *gpt_dn)
 {
+  if (lw_Ds) nmus = 1;
 #pragma omp parallel
   {
     size_t nl = (size_t)ngpt * nlay, nv = (size_t)ngpt * (nlay + 1);
@@ -371,12 +377,16 @@ void orc_lw_solver_1rescl_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, 
       const float *tc = tau + nl * icol, *lc = lay_source + nl * icol, *vc = lev_source + nv * icol;
       const float *ec = sfc_emis + (size_t)ngpt * icol, *sc = sfc_source + (size_t)ngpt * icol;
       const float *ic = inc_flux + (size_t)ngpt * icol;
+      const float *dv = lw_Ds ? lw_Ds + (size_t)ngpt * icol : NULL;
       float *fu = flux_up + (size_t)(nlay + 1) * icol, *fd = flux_dn + (size_t)(nlay + 1) * icol;
+      float *au = gpt_up ? gpt_up + nv * icol : acc_u, *ad = gpt_dn ? gpt_dn + nv * icol : acc_d;
       for (int imu = 0; imu < nmus; imu++) {
-        lw_noscat_col(ngpt, nlay, top_at_1, Ds[imu], weights[imu], ic, tc, lc, vc, ec, sc, ru, rd,
+        lw_noscat_col(ngpt, nlay, top_at_1, Ds[imu], dv, weights[imu], ic, tc, lc, vc, ec, sc, ru, rd,
                       tau_loc, trans, su, sd, ssa ? ssa + nl * icol : NULL, ssa ? g + nl * icol : NULL, An, Cn);
         float fac = 2.0f * PI_F * weights[imu];
         if (nmus == 1) {
+          if (gpt_up)
+            for (size_t i = 0; i < nv; i++) { au[i] = ru[i]; ad[i] = rd[i]; }
           for (int l = 0; l <= nlay; l++) {
             if (ngpt % 4 == 0) {
               float su4[4] = {0, 0, 0, 0}, sd4[4] = {0, 0, 0, 0};
@@ -395,20 +405,30 @@ void orc_lw_solver_1rescl_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, 
           }
         } else {
           for (size_t i = 0; i < nv; i++) {
-            if (imu == 0) { acc_u[i] = fac * ru[i]; acc_d[i] = fac * rd[i]; }
-            else { acc_u[i] = acc_u[i] + fac * ru[i]; acc_d[i] = acc_d[i] + fac * rd[i]; }
+            if (imu == 0) { au[i] = fac * ru[i]; ad[i] = fac * rd[i]; }
+            else { au[i] = au[i] + fac * ru[i]; ad[i] = ad[i] + fac * rd[i]; }
           }
         }
       }
       if (nmus > 1) /* sum_broadband rte/kernels/mo_fluxes_broadband_kernels.F90:31-39 */
         for (int l = 0; l <= nlay; l++) {
           float a = 0, b = 0;
-          for (int g = 0; g < ngpt; g++) { a += acc_u[g + (size_t)ngpt * l]; b += acc_d[g + (size_t)ngpt * l]; }
+          for (int g = 0; g < ngpt; g++) { a += au[g + (size_t)ngpt * l]; b += ad[g + (size_t)ngpt * l]; }
           fu[l] = a; fd[l] = b;
         }
     }
     free(buf);
   }
+}
+
+void orc_lw_solver_1rescl_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                    const float *Ds, const float *weights, const float *inc_flux,
+                                    const float *tau, const float *ssa, const float *g, const float *lay_source,
+                                    const float *lev_source, const float *sfc_emis, const float *sfc_source,
+                                    float *flux_up, float *flux_dn)
+{
+  orc_lw_solver_noscat_ext(ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, NULL, inc_flux, tau, ssa, g, lay_source,
+                           lev_source, sfc_emis, sfc_source, flux_up, flux_dn, NULL, NULL);
 }
 
 void orc_lw_solver_noscat_gaussquad(int ngpt, int nlay, int ncol, int top_at_1, int nmus,
@@ -587,10 +607,14 @@ void orc_sw_solver_noscat(int ngpt, int nlay, int ncol, int top_at_1, const floa
  * SW two-stream: rte/kernels/mo_rte_solver_kernels.F90:541-692 (sw_solver_2stream),
  * sw_two_stream_source :1366-1480, adding :1526-1637.  k_min = 1e-4 (sp, :76-82).
  * ------------------------------------------------------------------------------------------- */
-void orc_sw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
-                           const float *inc_flux_dif, const float *tau, const float *ssa, const float *gg,
-                           const float *mu0, const float *sfc_alb_dir, const float *sfc_alb_dif,
-                           float *flux_up, float *flux_dn, float *flux_dir)
+/* gpt_up/gpt_dn/gpt_dir (may be NULL, (ngpt, nlay+1, ncol)): save_gpt_flux (:572-588, :660-684) -- the g-point
+ * up, TOTAL down (diffuse + direct, rounded once: "adding computes only diffuse flux; flux_dn is total") and direct
+ * fluxes, and the broadband down flux summed as s + (dn + dir) instead of (s + dn) + dir. */
+void orc_sw_solver_2stream_gpt(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                               const float *inc_flux_dif, const float *tau, const float *ssa, const float *gg,
+                               const float *mu0, const float *sfc_alb_dir, const float *sfc_alb_dif,
+                               float *flux_up, float *flux_dn, float *flux_dir, float *gpt_up, float *gpt_dn,
+                               float *gpt_dir)
 {
   const float k_min = 1.e-4f, eps = FLT_EPSILON;
 #pragma omp parallel
@@ -688,6 +712,10 @@ void orc_sw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const flo
       }
       float *fu = flux_up + (size_t)(nlay + 1) * icol, *fd = flux_dn + (size_t)(nlay + 1) * icol;
       float *fr = flux_dir + (size_t)(nlay + 1) * icol;
+      if (gpt_up) {
+        float *gu = gpt_up + nv * icol, *gd = gpt_dn + nv * icol, *gr = gpt_dir + nv * icol;
+        for (size_t x = 0; x < nv; x++) { gu[x] = rup[x]; gd[x] = rdn[x] + rdir[x]; gr[x] = rdir[x]; }
+      }
       for (int l = 0; l <= nlay; l++) {
         if (ngpt % 4 == 0) {
           float su[4] = {0, 0, 0, 0}, sd[4] = {0, 0, 0, 0}, sr[4] = {0, 0, 0, 0};
@@ -696,7 +724,8 @@ void orc_sw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const flo
               size_t x = i + j + (size_t)ngpt * l;
               su[j] = su[j] + rup[x];
               sr[j] = sr[j] + rdir[x];
-              sd[j] = sd[j] + rdn[x] + rdir[x];
+              if (gpt_up) sd[j] = sd[j] + (rdn[x] + rdir[x]);
+              else sd[j] = sd[j] + rdn[x] + rdir[x];
             }
           fu[l] = su[0] + su[1] + su[2] + su[3];
           fd[l] = sd[0] + sd[1] + sd[2] + sd[3];
@@ -713,6 +742,15 @@ void orc_sw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const flo
     }
     free(buf);
   }
+}
+
+void orc_sw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
+                           const float *inc_flux_dif, const float *tau, const float *ssa, const float *gg,
+                           const float *mu0, const float *sfc_alb_dir, const float *sfc_alb_dif,
+                           float *flux_up, float *flux_dn, float *flux_dir)
+{
+  orc_sw_solver_2stream_gpt(ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, gg, mu0, sfc_alb_dir,
+                            sfc_alb_dif, flux_up, flux_dn, flux_dir, NULL, NULL, NULL);
 }
 
 /* rte/mo_rte_lw.F90:429-447 (expand): band values -> g-points. band_lims 1-based (2,nbnd). */

@@ -705,6 +705,70 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
                            sfc_alb_dif_gpt, nullptr, nullptr, nullptr, nullptr, flux_up, flux_dn, flux_dir);
 }
 
+// ---- the *_gpt entries: the call above with rte_lw's lw_Ds and ty_fluxes_flexible's g-point outputs, handed to the
+// launch through the context for this one call ----
+namespace {
+struct ExtrasScope {
+  rrtmgpnn_context *c;
+  ExtrasScope(rrtmgpnn_context *ctx, const float *ds, float *up, float *dn, float *dir) : c(ctx)
+  {
+    c->extras.lw_Ds = ds;
+    c->extras.gpt_up = up;
+    c->extras.gpt_dn = dn;
+    c->extras.gpt_dir = dir;
+  }
+  ~ExtrasScope() { c->extras = rrtmgpnn_context::SolverExtras{}; }
+};
+int lw_ds_check(int nmus, const float *lw_Ds)
+{
+  if (lw_Ds && nmus != 1)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "rte_lw: providing lw_Ds incompatible with specifying n_gauss_angles");
+  return RRTMGPNN_OK;
+}
+}  // namespace
+
+int rrtmgpnn_lw_solver_noscat_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                  const float *Ds, const float *weights, const float *lw_Ds, const float *inc_flux,
+                                  const float *tau, const float *lay_source, const float *lev_source,
+                                  const float *sfc_emis_gpt, const float *sfc_source, float *flux_up, float *flux_dn,
+                                  float *gpt_flux_up, float *gpt_flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (int rc = lw_ds_check(nmus, lw_Ds)) return rc;
+  ExtrasScope x(ctx, lw_Ds, gpt_flux_up, gpt_flux_dn, nullptr);
+  return rrtmgpnn_lw_solver_noscat(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, lay_source,
+                                   lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn);
+}
+
+int rrtmgpnn_lw_solver_noscat_planck_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                         const float *Ds, const float *weights, const float *lw_Ds,
+                                         const float *inc_flux, const float *tau, const float *pfrac, int nbnd,
+                                         int nPlanckTemp, const float *tlay, const float *tlev, const float *tsfc,
+                                         int sfc_lay, const int *band_lims_gpt, float temp_ref_min,
+                                         float totplnk_delta, const float *totplnk, int emis_by_band,
+                                         const float *sfc_emis, float *flux_up, float *flux_dn, float *gpt_flux_up,
+                                         float *gpt_flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (int rc = lw_ds_check(nmus, lw_Ds)) return rc;
+  ExtrasScope x(ctx, lw_Ds, gpt_flux_up, gpt_flux_dn, nullptr);
+  return rrtmgpnn_lw_solver_noscat_planck(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, pfrac,
+                                          nbnd, nPlanckTemp, tlay, tlev, tsfc, sfc_lay, band_lims_gpt, temp_ref_min,
+                                          totplnk_delta, totplnk, emis_by_band, sfc_emis, flux_up, flux_dn);
+}
+
+int rrtmgpnn_sw_solver_2stream_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                   const float *inc_flux, const float *inc_flux_dif, const float *tau,
+                                   const float *ssa, const float *g, const float *mu0, const float *sfc_alb_dir_gpt,
+                                   const float *sfc_alb_dif_gpt, float *flux_up, float *flux_dn, float *flux_dir,
+                                   float *gpt_flux_up, float *gpt_flux_dn, float *gpt_flux_dir)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  ExtrasScope x(ctx, nullptr, gpt_flux_up, gpt_flux_dn, gpt_flux_dir);
+  return rrtmgpnn_sw_solver_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
+                                    sfc_alb_dir_gpt, sfc_alb_dif_gpt, flux_up, flux_dn, flux_dir);
+}
+
 int rrtmgpnn_sw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                               const float *tau, const float *mu0, float *flux_dir)
 {

@@ -254,12 +254,21 @@ __device__ __forceinline__ void mlp32_hidden(const float *__restrict__ img, cons
 #define RRTMGPNN_MLP32_THREADS 512
 #endif
 constexpr int kMlp32Threads = RRTMGPNN_MLP32_THREADS;
+// the SW pair's block size and waves per SIMD (its 42 KB image leaves room for several blocks per CU)
+#ifndef RRTMGPNN_MLP32_SW_THREADS
+#define RRTMGPNN_MLP32_SW_THREADS 512
+#endif
+#ifndef RRTMGPNN_MLP32_SW_WPE
+#define RRTMGPNN_MLP32_SW_WPE 1
+#endif
+constexpr int kSwNT = RRTMGPNN_MLP32_SW_THREADS, kSwWPE = RRTMGPNN_MLP32_SW_WPE;
 
 // A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  The host guarantees that the
 // g-tiles are full: ngpt = 32 NGT (LW pair) or 2 ngpt = 32 NGT (LW both).  Dynamic LDS: the weight images, then 32
 // floats per wave (the tile's column amounts, handed from the sample lanes to the row registers).
-template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN>
-__global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
+template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN,
+          int NT = kMlp32Threads, int WPE = 1>
+__global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
 {
   constexpr bool kPair = MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR;
   extern __shared__ floatx4 lds4[];
@@ -451,21 +460,22 @@ __global__ __launch_bounds__(kMlp32Threads) void mlp32_kernel(Mlp32Args a)
   }
 }
 
-template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN>
+template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN,
+          int NT = kMlp32Threads, int WPE = 1>
 static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
 {
-  auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN>;
+  auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN, NT, WPE>;
   const size_t lds = sizeof(float) * ((size_t)(a.imgA_floats + (MODE != MLP_LW_BOTH ? a.imgB_floats : 0)) +
-                                      32 * (kMlp32Threads / 64));
+                                      32 * (NT / 64));
   if (lds > 160 * 1024) return RRTMGPNN_ERR_UNSUPPORTED;
   if (lds > 64 * 1024)
     if (int rc = raise_lds_limit((const void *)kern)) return rc;
   const long long ntiles = ((long long)a.nbatch + 31) / 32;
-  const int wpb = kMlp32Threads / 64;
-  const int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / kMlp32Threads);
+  const int wpb = NT / 64;
+  const int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / NT);
   const long long want = (ntiles + wpb - 1) / wpb;
   const long long grid = std::max<long long>(1, std::min<long long>(want, (long long)ctx->num_cus * per_cu));
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kMlp32Threads), lds, ctx->stream, a);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp32_kernel");
   return RRTMGPNN_OK;
 }
@@ -544,8 +554,8 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
   }
   if (mode == MLP_SW_PAIR && shape32(A, 4, 1, 8, 1, 8, 7) && shape32(B, 4, 1, 8, 1, 8, 7)) {
     // the shipped g224 pair: absorption and Rayleigh 7-16-16-224
-    if (xin) return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, true>(ctx, a);
-    return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, false>(ctx, a);
+    if (xin) return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, true, kSwNT, kSwWPE>(ctx, a);
+    return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, false, kSwNT, kSwWPE>(ctx, a);
   }
   if (mode == MLP_LW_BOTH && !xin && shape32(A, 9, 2, 32, 2, 32, 8)) {
     // the shipped g128 single model: 18-64-64-256

@@ -168,8 +168,8 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
                                            const float *__restrict__ lay, const float *__restrict__ lev,
                                            const float *__restrict__ emis, const float *__restrict__ sfc,
                                            LwPlanck pl, BandArgs bands, const float *__restrict__ tau_bnd,
-                                           float *__restrict__ ws, float *__restrict__ flux_up,
-                                           float *__restrict__ flux_dn)
+                                           float *__restrict__ gdn, float *__restrict__ gup, long long gcs,
+                                           float *__restrict__ flux_up, float *__restrict__ flux_dn)
 {
   static_assert(kRing % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -179,10 +179,13 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   const int nlev = nlay + 1;
   const uint32_t vg = 4u * (uint32_t)gc, row = 4u * (uint32_t)ngpt;
   // kMulti (nmus > 1, lw_solver_noscat_GaussQuad :383-412): g-point fluxes are summed over angles first, then
-  // reduced with sum_broadband's plain sequential sum; ws holds the per-g accumulators (2, nlev, ngpt).  A
-  // template parameter, so the nmus = 1 kernel's layer loop holds no global memory access besides its loads and
-  // the compiler's vmcnt waits keep the prefetch distance (a runtime branch merged both paths into vmcnt(0)).
-  float *wcol = kMulti ? ws + (size_t)2 * nlev * ngpt * icol : nullptr;
+  // reduced with sum_broadband's plain sequential sum; gdn / gup (column stride gcs) hold the per-g accumulators,
+  // (nlev, ngpt) per column: the context workspace, or the caller's g-point flux arrays (ty_fluxes_flexible).  With
+  // ang.rad (g-point outputs at one angle) they receive the radiances and the fluxes are reduced as lw_solver_noscat
+  // reduces them (quirk B-5).  A template parameter, so the nmus = 1 kernel's layer loop holds no global memory
+  // access besides its loads and the compiler's vmcnt waits keep the prefetch distance (a runtime branch merged both
+  // paths into vmcnt(0)).
+  float *wdn = kMulti ? gdn + gcs * icol : nullptr, *wup = kMulti ? gup + gcs * icol : nullptr;
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   float *btab = smem + kExpTabFloats;                        // fused: [nbnd][2*nlay+1] + [nbnd]
   const int brow = 2 * nlay + 1;
@@ -224,12 +227,14 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
                                                    : emis[g + (size_t)ngpt * icol]);
   const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
-  // stage one level's value: slot r of the ring, or (kMulti) the per-g accumulator of plane q
-  auto put = [&](float v, int r, int q, int level, bool acc) {
+  // stage one level's value v = fac * radiance: slot r of the ring, or (kMulti) the per-g accumulator of plane q
+  // (the radiance itself with ang.rad)
+  auto put = [&](float v, float rad, int r, int q, int level, bool acc) {
     if constexpr (kMulti) {
       if (on) {
-        float *w = wcol + ((size_t)q * nlev + level) * ngpt + g;
-        *w = acc ? *w + v : v;
+        float *w = (q == 0 ? wdn : wup) + (size_t)level * ngpt + g;
+        const float x = ang.rad ? rad : v;
+        *w = acc ? *w + x : x;
       }
     } else if (on) {
       ring[(size_t)r * ngpt + g] = v;
@@ -251,13 +256,14 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   const int dl_dn = top_at_1 ? 1 : -1;  // level index step going down
 
   for (int imu = 0; imu < ang.nmus; imu++) {
-    const float D = ang.D[imu];
+    // lw_Ds (rte/mo_rte_lw.F90:329-341): the kernel's D(igpt, icol), one angle
+    const float D = ang.Dg ? ang.Dg[gc + (size_t)ngpt * icol] : ang.D[imu];
     // radiance -> flux factor inside the broadband sum; with nmus == 1 and ngpt % 4 != 0 the reference
     // sums plain radiances (quirk B-5, mo_rte_solver_kernels.F90:287-320)
     const float fac = (kMulti || (ngpt & 3) == 0) ? 2.0f * kPi * ang.w[imu] : 1.0f;
     const bool acc = imu > 0;
     float I = inc / (2.0f * kPi * ang.w[imu]);
-    put(fac * I, 0, 0, top, acc);
+    put(fac * I, I, 0, 0, top, acc);
     flush(pdn, 1, top, 1);
     // downward: lw_transport_noscat_dn (:982-1009); j-th layer from the top is l = lay_dn(j)
     auto lay_dn = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
@@ -284,7 +290,7 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
           const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
           const float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
           I = T * I + S;
-          put(fac * I, r, 0, top_at_1 ? l + 1 : l, acc);
+          put(fac * I, I, r, 0, top_at_1 ? l + 1 : l, acc);
         }
       };
       for (int j0 = 0; j0 < nlay; j0 += kRing) {
@@ -295,7 +301,7 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     }
     // surface reflection and emission (:269)
     float U = I * (1.0f - e) + e * ss;
-    put(fac * U, 0, 1, sfcl, acc);
+    put(fac * U, U, 0, 1, sfcl, acc);
     flush(pup, 1, sfcl, 1);
     // upward: lw_transport_noscat_up (:950-980); j-th layer from the surface is l = lay_up(j)
     auto lay_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
@@ -322,7 +328,7 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
           const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
           const float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
           U = T * U + S;
-          put(fac * U, r, 1, top_at_1 ? l : l + 1, acc);
+          put(fac * U, U, r, 1, top_at_1 ? l : l + 1, acc);
         }
       };
       for (int j0 = 0; j0 < nlay; j0 += kRing) {
@@ -335,10 +341,19 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   if constexpr (kMulti) {
     __syncthreads();
     for (int t = g; t < 2 * nlev; t += blockDim.x) {
-      const float *w = wcol + (size_t)t * ngpt;
-      float s = 0.0f;
-      for (int i = 0; i < ngpt; i++) s = s + w[i];  // sum_broadband: sequential over g
       const int l = t % nlev;
+      const float *w = (t < nlev ? wdn : wup) + (size_t)l * ngpt;
+      float s = 0.0f;
+      if (ang.rad && (ngpt & 3) == 0) {
+        // one angle: lw_solver_noscat's inline reduction of fac * radiance in 4 partial sums (:296-318)
+        const float fac = 2.0f * kPi * ang.w[0];
+        float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int i = 0; i < ngpt; i += 4)
+          for (int k = 0; k < 4; k++) s4[k] = s4[k] + fac * w[i + k];
+        s = ((s4[0] + s4[1]) + s4[2]) + s4[3];
+      } else {
+        for (int i = 0; i < ngpt; i++) s = s + w[i];  // sum_broadband (or, one angle, ngpt % 4 != 0: quirk B-5)
+      }
       (t < nlev ? flux_dn : flux_up)[l + (size_t)nlev * icol] = s;
     }
     return;
@@ -359,27 +374,41 @@ static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, i
   if (ncol == 0) return RRTMGPNN_OK;
   if (nmus < 1 || nmus > 4) return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: nmus must be 1..4");
   if (ngpt > kLwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many g-points");
+  const auto &ex = ctx->extras;
+  if (ex.lw_Ds && nmus != 1) return fail(RRTMGPNN_ERR_ARGUMENT, "rte_lw: providing lw_Ds incompatible with specifying n_gauss_angles");
+  if ((ex.gpt_up == nullptr) != (ex.gpt_dn == nullptr))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: g-point outputs need both gpt_flux_up and gpt_flux_dn");
+  const bool gpt = ex.gpt_up != nullptr;
   LwAngles a{};
   a.nmus = nmus;
+  a.Dg = ex.lw_Ds;
+  a.rad = gpt && nmus == 1;
   for (int i = 0; i < nmus; i++) { a.D[i] = Ds[i]; a.w[i] = wts[i]; }
   int threads = (ngpt + 63) / 64 * 64;
   size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4);
   if (kFused) lds += sizeof(float) * lw_btab_floats(bands.nbnd, nlay);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many layers for LDS partials");
-  void *ws = nullptr;
-  if (nmus > 1) {
-    int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws);
+  // per-g accumulators: the caller's g-point arrays, or (several angles) the context workspace
+  float *gdn = ex.gpt_dn, *gup = ex.gpt_up;
+  const long long nv = (long long)ngpt * (nlay + 1);
+  long long gcs = nv;
+  if (!gpt && nmus > 1) {
+    void *ws = nullptr;
+    int rc = ctx->workspace(sizeof(float) * 2 * (size_t)nv * ncol, &ws);
     if (rc) return rc;
+    gdn = (float *)ws;
+    gup = gdn + nv;
+    gcs = 2 * nv;
   }
   constexpr int PF = kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF;
-  if (nmus > 1)
+  if (nmus > 1 || gpt)
     hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, PF, true>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
                        nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac, kFused ? lay_or_pfrac : lev_source,
-                       sfc_emis, sfc_source, pl, bands, tau_bnd, (float *)ws, flux_up, flux_dn);
+                       sfc_emis, sfc_source, pl, bands, tau_bnd, gdn, gup, gcs, flux_up, flux_dn);
   else
     hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, PF, false>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
                        nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac, kFused ? lay_or_pfrac : lev_source,
-                       sfc_emis, sfc_source, pl, bands, tau_bnd, (float *)ws, flux_up, flux_dn);
+                       sfc_emis, sfc_source, pl, bands, tau_bnd, gdn, gup, gcs, flux_up, flux_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_noscat_kernel");
   return RRTMGPNN_OK;
 }
@@ -720,7 +749,10 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   // per launch at C3, whole step C3 -3 %, C4 -1 % against kernels_sw_x2.hip, tools/gpu_ab.sh); mode 2 forces the
   // workspace-plane kernel, mode 1 one g-point per lane (also the odd-ngpt kernel).
   const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
-  const bool ck = (ngpt % 2) == 0 && (mode == 3 || mode == 0);
+  // g-point outputs (the *_gpt entries) are written by the checkpointed kernel, whatever the mode
+  const bool gpt = ctx->extras.gpt_up || ctx->extras.gpt_dn || ctx->extras.gpt_dir;
+  if (gpt && ngpt % 2) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: g-point outputs need an even ngpt");
+  const bool ck = (ngpt % 2) == 0 && (mode == 3 || mode == 0 || gpt);
   const bool x2 = !ck && kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc && kSwIncPark ? 3 : 0);

@@ -124,15 +124,18 @@ static_assert(kCkRing % kCkK == 0, "the flux ring must hold whole chunks");
 #define RRTMGPNN_SWCK_WAVES_NN 4
 #endif
 
-template <bool kHasG, bool kInc, int K>
-__global__ void __launch_bounds__(512, (!kHasG && !kInc) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES)
+// kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
+// broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
+template <bool kHasG, bool kInc, int K, bool kGpt = false>
+__global__ void __launch_bounds__(512, (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
                          const float *__restrict__ ssa, const float *__restrict__ gg, const float *__restrict__ mu0p,
                          const float *__restrict__ alb_dir, const float *__restrict__ alb_dif, BandArgs bands,
                          const float *__restrict__ tau_bnd, const float *__restrict__ ssa_bnd,
                          const float *__restrict__ g_bnd, float *__restrict__ ws, float *__restrict__ flux_up,
-                         float *__restrict__ flux_dn, float *__restrict__ flux_dir)
+                         float *__restrict__ flux_dn, float *__restrict__ flux_dir, float *__restrict__ gpt_up,
+                         float *__restrict__ gpt_dn, float *__restrict__ gpt_dir)
 {
   constexpr int R = kCkRing;
   constexpr bool kG0 = !kHasG && !kInc;  // g is the literal 0 (the NN path)
@@ -266,19 +269,28 @@ __global__ void __launch_bounds__(512, (!kHasG && !kInc) ? RRTMGPNN_SWCK_WAVES_N
     }
   }
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
-  auto put = [&](f2 up, f2 dif, f2 dir, int r) {
+  // level `lev` (array index) of the g-point outputs
+  auto put = [&](f2 up, f2 dif, f2 dir, int r, int lev) {
     if (on) {
+      const f2 dn = kGpt ? dif + dir : dif;  // kGpt: the total, rounded once ("flux_dn is total", :665-666)
       *(f2 *)&ring[(size_t)r * ngpt + g] = up;
-      *(f2 *)&ring[((size_t)R + r) * ngpt + g] = dif;
+      *(f2 *)&ring[((size_t)R + r) * ngpt + g] = dn;
       *(f2 *)&ring[((size_t)2 * R + r) * ngpt + g] = dir;
+      if constexpr (kGpt) {
+        const size_t o = (size_t)g + (size_t)ngpt * ((size_t)lev + (size_t)nlev * icol);
+        *(f2 *)&gpt_up[o] = up;
+        *(f2 *)&gpt_dn[o] = dn;
+        *(f2 *)&gpt_dir[o] = dir;
+      }
     }
   };
   auto flush = [&](int n, int lev0, int dl) {
-    ring_flush_sw<R>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn, flux_dir);
+    ring_flush_sw<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
+                           flux_dir);
   };
   const int dl_dn = top_at_1 ? 1 : -1;
   f2 Fdn = inc_dif ? ld_col(inc_dif) : splat(0.0f);
-  put(Fdn * alb_b + src_b, Fdn, Ftop, 0);
+  put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top);
   flush(1, top, 1);
   {
     Chunk cur, nxt;
@@ -335,7 +347,7 @@ __global__ void __launch_bounds__(512, (!kHasG && !kInc) ? RRTMGPNN_SWCK_WAVES_N
           const f2 denom = kCkKeepD ? D[p] : rcp2(1.0f - Rd[p] * A[p]);
           Fdn = (Td[p] * Fdn + Rd[p] * S[p] + Sd[p]) * denom;
           const f2 up = Fdn * A[p] + S[p];
-          put(up, Fdn, Fdir[p], rbase + p);
+          put(up, Fdn, Fdir[p], rbase + p, top + dl_dn * (ck * K + p + 1));
         }
       }
       if (rbase + K == R || ck == nck - 1) {
@@ -373,14 +385,23 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
   const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
+  const auto &ex = ctx->extras;
   auto go = [&](auto kern, const float *tb, const float *sb, const float *gb) -> int {
     if (lds > 64 * 1024)
       if (int rc = raise_lds_limit((const void *)kern)) return rc;
     hipLaunchKernelGGL(kern, grid, block, lds, ctx->stream, ngpt, nlay, ncol, top_at_1, ncb, inc_flux, inc_flux_dif,
-                       tau, ssa, g, mu0, alb_dir, alb_dif, b, tb, sb, gb, (float *)ws, flux_up, flux_dn, flux_dir);
+                       tau, ssa, g, mu0, alb_dir, alb_dif, b, tb, sb, gb, (float *)ws, flux_up, flux_dn, flux_dir,
+                       ex.gpt_up, ex.gpt_dn, ex.gpt_dir);
     RRTMGPNN_LAUNCH_CHECK("sw_2stream_ck_kernel");
     return RRTMGPNN_OK;
   };
+  if (ex.gpt_up || ex.gpt_dn || ex.gpt_dir) {  // ty_fluxes_flexible g-point outputs
+    if (!ex.gpt_up || !ex.gpt_dn || !ex.gpt_dir)
+      return fail(RRTMGPNN_ERR_ARGUMENT, "sw solver: g-point outputs need gpt_flux_up, gpt_flux_dn and gpt_flux_dn_dir");
+    if (bands) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: g-point outputs with a fused increment");
+    if (g) return go(sw_2stream_ck_kernel<true, false, kCkK, true>, nullptr, nullptr, nullptr);
+    return go(sw_2stream_ck_kernel<false, false, kCkK, true>, nullptr, nullptr, nullptr);
+  }
   if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
   if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);

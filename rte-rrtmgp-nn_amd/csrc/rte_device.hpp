@@ -101,6 +101,8 @@ __host__ __device__ constexpr size_t lw_btab_floats(int nbnd, int nlay) { return
 struct LwAngles {
   float D[4], w[4];
   int nmus;
+  const float *Dg;  // rte_lw's lw_Ds: per-(g-point, column) secants D(igpt, icol), one angle (nullptr: Gauss D)
+  int rad;          // kMulti with one angle (g-point outputs): store radiances, reduce with fac as lw_solver_noscat
 };
 
 // ------------------------------------------------------------------------------------------
@@ -164,7 +166,9 @@ __device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]
 // ring + c*3*R*ngpt).  Each (column, quantity, level) thread forms the level's complete ordered sum -- the same
 // partials and the same ((p0 + p1) + p2) + p3 as ring_flush + combine4 -- and stores it straight to the flux
 // array: up, dn (= dif + dir, dn_mode) and dir.  Columns at or past ncol (the grid's last block) store nothing.
-template <int R>
+// kTotal: the down slot already holds the total (diffuse + direct) g-point flux, as sw_solver_2stream forms it when it
+// saves g-point fluxes (:660-670): the down sum is s + total instead of (s + diffuse) + direct
+template <int R, bool kTotal = false>
 __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n, int lev0, int dl, int ngpt, int nlev,
                                               int icol0, int ncol, float *o_up, float *o_dn, float *o_dir)
 {
@@ -180,7 +184,7 @@ __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n,
     if ((ngpt & 3) == 0) {
       const float4 *r4 = (const float4 *)r, *q4 = (const float4 *)r2;
       const int n4 = ngpt >> 2;
-      if (dn) {
+      if (dn && !kTotal) {
 #pragma unroll 4
         for (int m = 0; m < n4; m++) {
           const float4 a = r4[m], b = q4[m];
@@ -194,7 +198,7 @@ __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n,
         }
       }
     } else {
-      if (dn) for (int i = 0; i < ngpt; i++) s0 = s0 + (r[i] + r2[i]);
+      if (dn && !kTotal) for (int i = 0; i < ngpt; i++) s0 = s0 + (r[i] + r2[i]);
       else    for (int i = 0; i < ngpt; i++) s0 = s0 + r[i];
     }
     const int icol = icol0 + c;

@@ -398,6 +398,25 @@ class FluxesBroadband:
     def are_desired(self):
         return any(x is not None for x in (self.flux_up, self.flux_dn, self.flux_dn_dir, self.flux_net))
 
+    def are_desired_gpt(self):
+        return False
+
+
+class FluxesFlexible(FluxesBroadband):
+    """ty_fluxes_flexible (rte/mo_fluxes.F90:57-67): the broadband outputs plus g-point fluxes, (ncol, nlay+1, ngpt)
+    tensors the caller allocates.  rte_lw fills gpt_flux_up/dn (1scl properties; with one angle the g-point radiances,
+    quirk B-5), rte_sw gpt_flux_up/dn (total)/dn_dir (2str properties); gpt_flux_net is not written (as in the
+    reference)."""
+
+    def __init__(self, flux_up=None, flux_dn=None, flux_dn_dir=None, flux_net=None, gpt_flux_up=None,
+                 gpt_flux_dn=None, gpt_flux_dn_dir=None, gpt_flux_net=None):
+        super().__init__(flux_up, flux_dn, flux_dn_dir, flux_net)
+        self.gpt_flux_up, self.gpt_flux_dn = gpt_flux_up, gpt_flux_dn
+        self.gpt_flux_dn_dir, self.gpt_flux_net = gpt_flux_dn_dir, gpt_flux_net
+
+    def are_desired_gpt(self):
+        return any(x is not None for x in (self.gpt_flux_up, self.gpt_flux_dn, self.gpt_flux_dn_dir, self.gpt_flux_net))
+
 
 # ---------------------------------------------------------------------------------------------
 class GasOpticsRRTMGP(OpticalProps):
@@ -730,11 +749,23 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
         return "rte_lw: lw_Ds not valid input for _2str class"
     if is2 and use_2stream and n_gauss_angles is not None and nmu != 1:
         return "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"
-    if lw_Ds is not None:
-        return "rte_lw: lw_Ds (column-dependent diffusivity) is not implemented"
     if flux_up_Jac is not None or flux_dn_Jac is not None:
         return "rte_lw: compute_Jac is .false. in this configuration (rte/mo_rte_rrtmgp_config.F90:28)"
     ncol, nlay, ngpt = optical_props.tau.shape
+    if lw_Ds is not None:  # (:239-246); Fortran extents (ncol, ngpt) = this tensor layout's (ngpt, ncol)
+        if tuple(lw_Ds.shape) != (ngpt, ncol):
+            return "rte_lw: lw_Ds inconsistently sized"
+        if bool((torch.as_tensor(lw_Ds) < 1.0).any()):
+            return "rte_lw: one or more values of lw_Ds < 1."
+        if nmu != 1:
+            return "rte_lw: providing lw_Ds incompatible with specifying n_gauss_angles"
+    gpt = fluxes.are_desired_gpt()
+    if gpt and is2:
+        return "rte_lw: g-point fluxes of two-stream optical properties are not produced by this build"
+    if gpt:
+        for a in (fluxes.gpt_flux_up, fluxes.gpt_flux_dn):
+            if a is not None and tuple(a.shape) != (ncol, nlay + 1, ngpt):
+                return "rte_lw: g-point flux arrays inconsistently sized"
     nband = optical_props.get_nband()
     if tuple(sfc_emis.shape) != (ncol, nband):
         return "rte_lw: sfc_emis inconsistently sized"
@@ -766,6 +797,17 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
                                           _p(op.tau), _p(op.ssa), _p(op.g), _p(sources.lay_source),
                                           _p(sources.lev_source), _p(emis_gpt), _p(sources.sfc_source), _p(up),
                                           _p(dn)), "lw_solver_1rescl")
+    elif gpt or lw_Ds is not None:  # ty_fluxes_flexible g-point outputs / column-dependent secants (:329-341)
+        gu = fluxes.gpt_flux_up if getattr(fluxes, "gpt_flux_up", None) is not None else \
+            (torch.empty((ncol, nlay + 1, ngpt), device=emis.device) if gpt else None)
+        gd = fluxes.gpt_flux_dn if getattr(fluxes, "gpt_flux_dn", None) is not None else \
+            (torch.empty((ncol, nlay + 1, ngpt), device=emis.device) if gpt else None)
+        ds = _f32dev(lw_Ds, emis.device) if lw_Ds is not None else None
+        check(L.rrtmgpnn_lw_solver_noscat_gpt(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu,
+                                              float_array(GAUSS_DS[nmu]), float_array(GAUSS_WTS[nmu]), _p(ds),
+                                              _p(inc_flux), _p(op.tau), _p(sources.lay_source),
+                                              _p(sources.lev_source), _p(emis_gpt), _p(sources.sfc_source), _p(up),
+                                              _p(dn), _p(gu), _p(gd)), "lw_solver_noscat_gpt")
     else:
         check(L.rrtmgpnn_lw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu,
                                           float_array(GAUSS_DS[nmu]), float_array(GAUSS_WTS[nmu]), _p(inc_flux),
@@ -807,10 +849,21 @@ def rte_sw(atmos, top_at_1, mu0, inc_flux, sfc_alb_dir_gpt, sfc_alb_dif_gpt, flu
     up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=dev)
     dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=dev)
     dr = fluxes.flux_dn_dir if fluxes.flux_dn_dir is not None else torch.empty((ncol, nlay + 1), device=dev)
-    check(_lib.lib().rrtmgpnn_sw_solver_2stream(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
-                                                _p(inc_flux_dif), _p(atmos.tau), _p(atmos.ssa), _p(atmos.g), _p(mu0),
-                                                _p(sfc_alb_dir_gpt), _p(sfc_alb_dif_gpt), _p(up), _p(dn), _p(dr)),
-          "sw_solver_2stream")
+    if fluxes.are_desired_gpt():  # save_gpt_flux (rte/mo_rte_sw.F90:155-173, 228-234): up, total down, direct
+        g3 = []
+        for a in (fluxes.gpt_flux_up, fluxes.gpt_flux_dn, fluxes.gpt_flux_dn_dir):
+            if a is not None and tuple(a.shape) != (ncol, nlay + 1, ngpt):
+                return "rte_sw: g-point flux arrays inconsistently sized"
+            g3.append(a if a is not None else torch.empty((ncol, nlay + 1, ngpt), device=dev))
+        check(_lib.lib().rrtmgpnn_sw_solver_2stream_gpt(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
+                                                        _p(inc_flux_dif), _p(atmos.tau), _p(atmos.ssa), _p(atmos.g),
+                                                        _p(mu0), _p(sfc_alb_dir_gpt), _p(sfc_alb_dif_gpt), _p(up),
+                                                        _p(dn), _p(dr), *[_p(a) for a in g3]), "sw_solver_2stream_gpt")
+    else:
+        check(_lib.lib().rrtmgpnn_sw_solver_2stream(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
+                                                    _p(inc_flux_dif), _p(atmos.tau), _p(atmos.ssa), _p(atmos.g),
+                                                    _p(mu0), _p(sfc_alb_dir_gpt), _p(sfc_alb_dif_gpt), _p(up),
+                                                    _p(dn), _p(dr)), "sw_solver_2stream")
     if fluxes.flux_net is not None:
         torch.sub(dn, up, out=fluxes.flux_net)
     return ""

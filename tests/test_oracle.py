@@ -147,3 +147,49 @@ def test_sw_noscat_bitwise_vs_reference_kernels(orc, rfmip, models, top_at_1):
     assert np.all(want == want[:1])  # quirk B-11: the reference sums column 1 for every column
     top = 0 if top_at_1 else -1
     assert np.all(got[:, top] > 0) and np.all(np.diff(got, axis=1) * (1 if top_at_1 else -1) <= 0)
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="reference oracle not built (needs /root/reference)")
+@pytest.mark.parametrize("top_at_1", [True, False])
+def test_gpt_fluxes_and_lw_ds_bitwise_vs_reference(orc, rfmip, models, top_at_1):
+    """ty_fluxes_flexible g-point outputs and rte_lw's lw_Ds: the restatement == the reference's rte_lw / rte_sw, bit
+    for bit.  LW with one angle returns g-point radiances (quirk B-5), with several the angle-summed fluxes; lw_Ds is
+    read in the kernel's (ngpt, ncol) order although rte_lw checks (ncol, ngpt) extents (quirk B-12).  SW g-point down
+    fluxes are total (diffuse + direct) and the broadband down flux is summed from them."""
+    import oracle as O
+    from rrtmgpnn import data
+    ref = O.Reference()
+    kd, kds = data.load_kdist("lw"), data.load_kdist("sw")
+    prob = subset(rfmip, np.arange(1, 1800, 97))
+    go = orc.lw_gas_optics(prob, [models["lw_abs"], models["lw_pfrac"]], kd)
+    tau, lay, lev = go["tau"], go["lay_source"], go["lev_source"]
+    if not top_at_1:
+        tau, lay, lev = (np.ascontiguousarray(a[:, ::-1]) for a in (tau, lay, lev))
+    ncol, nlay, ngpt = tau.shape
+    rng = np.random.default_rng(7)
+    emis_band = rng.uniform(0.8, 1.0, size=(ncol, kd["nband"])).astype(np.float32)
+    band = np.concatenate([np.full(hi - lo + 1, b) for b, (lo, hi) in enumerate(np.asarray(kd["band_lims_gpt"]).reshape(-1, 2))])
+    emis_gpt = np.ascontiguousarray(emis_band[:, band])
+    for nmus in (1, 2, 3):
+        want = ref.rte_lw_gpt(kd, tau, lay, lev, go["sfc_source"], go["sfc_source_Jac"], emis_band, top_at_1, nmus)
+        got = orc.lw_solver(tau, lay, lev, emis_gpt, go["sfc_source"], top_at_1, nmus, gpt=True)
+        for a, b, what in zip(got, want, ("up", "dn", "gpt_up", "gpt_dn")):
+            np.testing.assert_array_equal(a, b, err_msg="nmus %d %s" % (nmus, what))
+    ds = rng.uniform(1.0, 2.5, size=ngpt * ncol).astype(np.float32)
+    want = ref.rte_lw_gpt(kd, tau, lay, lev, go["sfc_source"], go["sfc_source_Jac"], emis_band, top_at_1, 1, lw_Ds=ds)
+    got = orc.lw_solver(tau, lay, lev, emis_gpt, go["sfc_source"], top_at_1, lw_Ds=ds, gpt=True)
+    for a, b, what in zip(got, want, ("up", "dn", "gpt_up", "gpt_dn")):
+        np.testing.assert_array_equal(a, b, err_msg="lw_Ds " + what)
+    plain = orc.lw_solver(tau, lay, lev, emis_gpt, go["sfc_source"], top_at_1)
+    assert not np.array_equal(plain[0], got[0])  # the secants took effect
+    gs = orc.sw_gas_optics(prob, [models["sw_abs"], models["sw_ray"]])
+    t2, w2, g2 = gs["tau"], gs["ssa"], np.zeros_like(gs["tau"])
+    if not top_at_1:
+        t2, w2 = (np.ascontiguousarray(a[:, ::-1]) for a in (t2, w2))
+    toa = data.toa_flux(prob, kds)
+    alb = rng.uniform(0.05, 0.5, size=toa.shape).astype(np.float32)
+    mu0 = rng.uniform(0.1, 1.0, size=ncol).astype(np.float32)
+    want = ref.rte_sw_gpt(kds, t2, w2, g2, mu0, toa, alb, alb, top_at_1)
+    got = orc.sw_solver(t2, w2, g2, mu0, toa, alb, alb, top_at_1, gpt=True)
+    for a, b, what in zip(got, want, ("up", "dn", "dir", "gpt_up", "gpt_dn", "gpt_dir")):
+        np.testing.assert_array_equal(a, b, err_msg="sw " + what)
