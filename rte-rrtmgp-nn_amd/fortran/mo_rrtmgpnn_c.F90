@@ -15,6 +15,7 @@ module mo_rrtmgpnn_c
   public :: c_rrtmgpnn_gas_optics_lw_nn, c_rrtmgpnn_gas_optics_sw_nn, c_rrtmgpnn_lw_solver_noscat_planck, &
             c_rrtmgpnn_sw_solver_noscat
   public :: c_rrtmgpnn_compute_heating_rate
+  public :: c_rrtmgpnn_lw_solver_noscat_gpt, c_rrtmgpnn_lw_solver_noscat_planck_gpt, c_rrtmgpnn_sw_solver_2stream_gpt
   public :: c_rrtmgpnn_network_load, c_rrtmgpnn_compute_nn_inputs, c_rrtmgpnn_get_col_dry, &
             c_rrtmgpnn_interpolate_tlev, c_rrtmgpnn_predict_nn_lw, c_rrtmgpnn_predict_nn_sw, &
             c_rrtmgpnn_compute_planck_source_nn, c_rrtmgpnn_lw_solver_noscat, c_rrtmgpnn_sw_solver_2stream, &
@@ -195,6 +196,36 @@ module mo_rrtmgpnn_c
       type(c_ptr), value :: ctx, inc_flux, tau, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn
       integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus
       real(c_float), dimension(*), intent(in) :: Ds, weights
+    end function
+    ! ty_fluxes_flexible g-point outputs and lw_Ds (include/rrtmgpnn.h)
+    integer(c_int) function c_rrtmgpnn_lw_solver_noscat_gpt(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, lw_Ds, &
+        inc_flux, tau, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn, gpt_flux_up, gpt_flux_dn) &
+        bind(C, name="rrtmgpnn_lw_solver_noscat_gpt")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx, lw_Ds, inc_flux, tau, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, &
+                            flux_dn, gpt_flux_up, gpt_flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus
+      real(c_float), dimension(*), intent(in) :: Ds, weights
+    end function
+    integer(c_int) function c_rrtmgpnn_lw_solver_noscat_planck_gpt(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, &
+        lw_Ds, inc_flux, tau, pfrac, nbnd, nPlanckTemp, tlay, tlev, tsfc, sfc_lay, band_lims_gpt, temp_ref_min, &
+        totplnk_delta, totplnk, emis_by_band, sfc_emis, flux_up, flux_dn, gpt_flux_up, gpt_flux_dn) &
+        bind(C, name="rrtmgpnn_lw_solver_noscat_planck_gpt")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx, lw_Ds, inc_flux, tau, pfrac, tlay, tlev, tsfc, totplnk, sfc_emis, flux_up, flux_dn, &
+                            gpt_flux_up, gpt_flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus, nbnd, nPlanckTemp, sfc_lay, emis_by_band
+      real(c_float), dimension(*), intent(in) :: Ds, weights
+      integer(c_int), dimension(*), intent(in) :: band_lims_gpt
+      real(c_float), value :: temp_ref_min, totplnk_delta
+    end function
+    integer(c_int) function c_rrtmgpnn_sw_solver_2stream_gpt(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, &
+        tau, ssa, g, mu0, sfc_alb_dir_gpt, sfc_alb_dif_gpt, flux_up, flux_dn, flux_dir, gpt_flux_up, gpt_flux_dn, &
+        gpt_flux_dir) bind(C, name="rrtmgpnn_sw_solver_2stream_gpt")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, inc_flux, inc_flux_dif, tau, ssa, g, mu0, sfc_alb_dir_gpt, sfc_alb_dif_gpt, &
+                            flux_up, flux_dn, flux_dir, gpt_flux_up, gpt_flux_dn, gpt_flux_dir
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1
     end function
     integer(c_int) function c_rrtmgpnn_lw_solver_1rescl(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, &
         inc_flux, tau, ssa, g, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn) &

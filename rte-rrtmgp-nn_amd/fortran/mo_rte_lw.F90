@@ -5,7 +5,8 @@
 ! (rrtmgpnn_lw_solver_noscat_planck, emissivity expanded by band in-kernel); the broadband reduction is fused into
 ! every solver, and the fluxes come back into the caller's flux_up / flux_dn / flux_net.
 ! 1scl: lw_solver_noscat_GaussQuad; 2str: the rescaled solution (default) or lw_solver_2stream
-! (use_2stream).  g-point fluxes, lw_Ds and the Jacobians return an error string.
+! (use_2stream).  ty_fluxes_flexible g-point fluxes and lw_Ds on 1scl properties (rrtmgpnn_lw_solver_noscat[_planck]_gpt:
+! with one angle the g-point radiances, quirk B-5); on 2str properties and for the Jacobians an error string.
 module mo_rte_lw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,         only: wp
@@ -42,14 +43,15 @@ contains
     real(wp), dimension(:,:), contiguous, target, optional, intent(in) :: inc_flux   ! (ngpt, ncol)
     integer,  optional, intent(in) :: n_gauss_angles
     logical,  optional, intent(in) :: use_2stream
-    real(wp), dimension(:,:), optional, intent(in) :: lw_Ds
+    real(wp), dimension(:,:), optional, target, intent(in) :: lw_Ds   ! (ncol, ngpt) extents, read as (ngpt, ncol): B-12
     real(wp), dimension(:,:), target, optional, intent(inout) :: flux_up_Jac, flux_dn_Jac
     character(len=128) :: error_msg
     integer :: ncol, nlay, ngpt, nband, nmus
-    integer(c_long_long) :: ng, nv, nsfc
+    integer(c_long_long) :: ng, nv, nsfc, ngv
     integer(c_int), allocatable :: lims(:,:)
     type(c_ptr) :: d_tau, d_ssa, d_g, d_lay, d_lev, d_sfc, d_jac, d_emis, d_emis_gpt, d_inc, d_up, d_dn
-    logical :: two_str, use_2s, src_tmp, g_tmp
+    type(c_ptr) :: d_ds, d_gup, d_gdn
+    logical :: two_str, use_2s, src_tmp, g_tmp, gpt
     real(wp), allocatable :: up(:,:), dn(:,:)
 
     ncol  = optical_props%get_ncol()
@@ -59,9 +61,6 @@ contains
     error_msg = ""
     if (.not. fluxes%are_desired()) then
       error_msg = "rte_lw: no space allocated for fluxes"; return
-    end if
-    if (fluxes%are_desired_gpt()) then
-      error_msg = "rte_lw: g-point fluxes are not produced by this build (broadband only)"; return
     end if
     if (any([sources%get_ncol(), sources%get_nlay(), sources%get_ngpt()] /= [ncol, nlay, ngpt])) then
       error_msg = "rte_lw: sources and optical properties inconsistently sized"; return
@@ -90,11 +89,18 @@ contains
       end if
       nmus = n_gauss_angles
     end if
-    if (present(lw_Ds)) then
-      error_msg = "rte_lw: lw_Ds (column-dependent diffusivity) is not implemented"; return
-    end if
     if (present(flux_up_Jac) .or. present(flux_dn_Jac)) then
       error_msg = "rte_lw: compute_Jac is .false. in this configuration (mo_rte_rrtmgp_config.F90:28)"; return
+    end if
+    if (associated(fluxes%gpt_flux_up)) then
+      if (any(shape(fluxes%gpt_flux_up) /= [ngpt, nlay + 1, ncol])) then
+        error_msg = "rte_lw: gpt_flux_up inconsistently sized"; return
+      end if
+    end if
+    if (associated(fluxes%gpt_flux_dn)) then
+      if (any(shape(fluxes%gpt_flux_dn) /= [ngpt, nlay + 1, ncol])) then
+        error_msg = "rte_lw: gpt_flux_dn inconsistently sized"; return
+      end if
     end if
     use_2s = .false.
     if (present(use_2stream)) use_2s = use_2stream
@@ -106,7 +112,24 @@ contains
       if (use_2s) then
         error_msg = "rte_lw: can't use two-stream methods with only absorption optical depth"; return
       end if
+      if (present(lw_Ds)) then  ! (:239-246)
+        if (any(shape(lw_Ds) /= [ncol, ngpt])) then
+          error_msg = "rte_lw: lw_Ds inconsistently sized"; return
+        end if
+        if (any(lw_Ds < 1._wp)) then
+          error_msg = "rte_lw: one or more values of lw_Ds < 1."; return
+        end if
+        if (nmus /= 1) then
+          error_msg = "rte_lw: providing lw_Ds incompatible with specifying n_gauss_angles"; return
+        end if
+      end if
     type is (ty_optical_props_2str)
+      if (present(lw_Ds)) then
+        error_msg = "rte_lw: lw_Ds not valid input for _2str class"; return
+      end if
+      if (fluxes%are_desired_gpt()) then
+        error_msg = "rte_lw: g-point fluxes of two-stream optical properties are not produced by this build"; return
+      end if
       if (use_2s .and. nmus /= 1) then
         error_msg = "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"; return
       end if
@@ -127,18 +150,29 @@ contains
     if (present(inc_flux)) d_inc = dev_stage(inc_flux, nsfc)
     d_up = dev_scratch(nv)
     d_dn = dev_scratch(nv)
+    ! ty_fluxes_flexible g-point outputs and lw_Ds (1scl): the *_gpt entries
+    gpt = fluxes%are_desired_gpt()
+    ngv = int(ngpt, c_long_long) * (nlay + 1) * ncol
+    d_ds = c_null_ptr
+    d_gup = c_null_ptr
+    d_gdn = c_null_ptr
+    if (present(lw_Ds)) d_ds = dev_stage(lw_Ds, nsfc)
+    if (gpt) then
+      d_gup = dev_scratch(ngv)
+      d_gdn = dev_scratch(ngv)
+    end if
     d_emis_gpt = c_null_ptr
     if (.not. two_str .and. sources%planck_deferred) then
       ! lw_solver_noscat_GaussQuad (:326-353) with compute_Planck_source_nn (gas_optics, :398-404) and expand(sfc_emis)
       ! (:429-447) inside the solver
-      error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat_planck(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                    merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), gauss_wts(1:nmus, nmus), d_inc, &
-                    d_tau, dev_present(sources%lay_source, ng, PRESENT_READ), nband, sources%pk_ntemp, &
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat_planck_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                    merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), gauss_wts(1:nmus, nmus), d_ds, &
+                    d_inc, d_tau, dev_present(sources%lay_source, ng, PRESENT_READ), nband, sources%pk_ntemp, &
                     dev_present(sources%pk_tlay, size(sources%pk_tlay, kind=c_long_long), PRESENT_READ), &
                     dev_present(sources%pk_tlev, size(sources%pk_tlev, kind=c_long_long), PRESENT_READ), &
                     dev_present(sources%pk_tsfc, size(sources%pk_tsfc, kind=c_long_long), PRESENT_READ), &
                     sources%pk_sfc_lay, lims, sources%pk_tmin, sources%pk_tdelta, sources%pk_totplnk, 1_c_int, d_emis, &
-                    d_up, d_dn), "rte_lw: lw_solver_noscat")
+                    d_up, d_dn, d_gup, d_gdn), "rte_lw: lw_solver_noscat")
     else
       src_tmp = .false.
       g_tmp = .false.
@@ -165,10 +199,10 @@ contains
                                      gauss_wts(1:nmus, nmus), d_inc, d_tau, d_ssa, d_g, d_lay, d_lev, d_emis_gpt, &
                                      d_sfc, d_up, d_dn), "rte_lw: lw_solver_noscat (rescaled)")
         else
-          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
                                      merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
-                                     gauss_wts(1:nmus, nmus), d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, d_up, &
-                                     d_dn), "rte_lw: lw_solver_noscat")
+                                     gauss_wts(1:nmus, nmus), d_ds, d_inc, d_tau, d_lay, d_lev, d_emis_gpt, d_sfc, &
+                                     d_up, d_dn, d_gup, d_gdn), "rte_lw: lw_solver_noscat")
         end if
       end if
       if (src_tmp) then
@@ -180,6 +214,10 @@ contains
     if (error_msg == '') then
       call dev_copy_out(up, d_up, nv)
       call dev_copy_out(dn, d_dn, nv)
+      if (gpt) then
+        if (associated(fluxes%gpt_flux_up)) call dev_copy_out(fluxes%gpt_flux_up, d_gup, ngv)
+        if (associated(fluxes%gpt_flux_dn)) call dev_copy_out(fluxes%gpt_flux_dn, d_gdn, ngv)
+      end if
     end if
     call rrtmgpnn_sync(error_msg, "rte_lw")
     if (error_msg == '') then
@@ -189,5 +227,6 @@ contains
     end if
     call dev_release(d_emis); call dev_release(d_emis_gpt); call dev_release(d_inc)
     call dev_release(d_up); call dev_release(d_dn)
+    call dev_release(d_ds); call dev_release(d_gup); call dev_release(d_gdn)
   end function rte_lw
 end module mo_rte_lw

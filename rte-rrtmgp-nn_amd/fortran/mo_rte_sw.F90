@@ -2,7 +2,8 @@
 ! g-point).  The optical properties are read from their device copies (mo_optical_props).  2str: the two-stream
 ! solver (sw_solver_2stream, rte/kernels/mo_rte_solver_kernels.F90:541-692) as one HIP kernel with the broadband
 ! reduction fused in; 1scl: apply_BC + sw_solver_noscat (:213-222), the direct beam only (flux_dn_dir; flux_up /
-! flux_dn are left as they are, as in the reference).  g-point fluxes return an error string.
+! flux_dn are left as they are, as in the reference).  ty_fluxes_flexible g-point fluxes on 2str properties
+! (rrtmgpnn_sw_solver_2stream_gpt: up, total down, direct, :155-173, 228-234); on 1scl an error string.
 module mo_rte_sw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,      only: wp
@@ -26,10 +27,10 @@ contains
     real(wp), dimension(:,:), optional, contiguous, target, intent(in) :: inc_flux_dif      ! (ngpt, ncol)
     character(len=128) :: error_msg
     integer :: ncol, nlay, ngpt
-    integer(c_long_long) :: ng, nv, nsfc
-    type(c_ptr) :: d_tau, d_ssa, d_g, d_mu0, d_inc, d_dif, d_adir, d_adif, d_up, d_dn, d_dir
+    integer(c_long_long) :: ng, nv, nsfc, ngv
+    type(c_ptr) :: d_tau, d_ssa, d_g, d_mu0, d_inc, d_dif, d_adir, d_adif, d_up, d_dn, d_dir, d_gup, d_gdn, d_gdir
     real(wp), allocatable :: up(:,:), dn(:,:), dir(:,:)
-    logical :: two_str
+    logical :: two_str, gpt
 
     ncol = atmos%get_ncol()
     nlay = atmos%get_nlay()
@@ -38,8 +39,20 @@ contains
     if (.not. fluxes%are_desired()) then
       error_msg = "rte_sw: no space allocated for fluxes"; return
     end if
-    if (fluxes%are_desired_gpt()) then
-      error_msg = "rte_sw: g-point fluxes are not produced by this build (broadband only)"; return
+    if (associated(fluxes%gpt_flux_up)) then
+      if (any(shape(fluxes%gpt_flux_up) /= [ngpt, nlay + 1, ncol])) then
+        error_msg = "rte_sw: gpt_flux_up inconsistently sized"; return
+      end if
+    end if
+    if (associated(fluxes%gpt_flux_dn)) then
+      if (any(shape(fluxes%gpt_flux_dn) /= [ngpt, nlay + 1, ncol])) then
+        error_msg = "rte_sw: gpt_flux_dn inconsistently sized"; return
+      end if
+    end if
+    if (associated(fluxes%gpt_flux_dn_dir)) then
+      if (any(shape(fluxes%gpt_flux_dn_dir) /= [ngpt, nlay + 1, ncol])) then
+        error_msg = "rte_sw: gpt_flux_dn_dir inconsistently sized"; return
+      end if
     end if
     if (size(mu0) /= ncol) then
       error_msg = "rte_sw: mu0 inconsistently sized"; return
@@ -91,6 +104,11 @@ contains
     d_up = dev_scratch(nv)
     d_dn = dev_scratch(nv)
     d_dir = dev_scratch(nv)
+    gpt = fluxes%are_desired_gpt()
+    ngv = int(ngpt, c_long_long) * (nlay + 1) * ncol
+    d_gup = c_null_ptr
+    d_gdn = c_null_ptr
+    d_gdir = c_null_ptr
     two_str = .false.
     select type (atmos)
     class is (ty_optical_props_2str)
@@ -98,10 +116,26 @@ contains
       d_ssa = dev_present(atmos%ssa, ng, PRESENT_READ)
       d_g = c_null_ptr  ! NULL: g is identically zero (the solver takes it as a literal 0, same fluxes)
       if (.not. atmos%g_zero) d_g = dev_present(atmos%g, ng, PRESENT_READ)
-      error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                                 merge(1_c_int, 0_c_int, top_at_1), d_inc, d_dif, d_tau, d_ssa, d_g, d_mu0, &
-                                 d_adir, d_adif, d_up, d_dn, d_dir), "rte_sw: sw_solver_2stream")
+      if (gpt) then
+        d_gup = dev_scratch(ngv)
+        d_gdn = dev_scratch(ngv)
+        d_gdir = dev_scratch(ngv)
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_2stream_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                   merge(1_c_int, 0_c_int, top_at_1), d_inc, d_dif, d_tau, d_ssa, d_g, d_mu0, &
+                                   d_adir, d_adif, d_up, d_dn, d_dir, d_gup, d_gdn, d_gdir), "rte_sw: sw_solver_2stream")
+      else
+        error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                   merge(1_c_int, 0_c_int, top_at_1), d_inc, d_dif, d_tau, d_ssa, d_g, d_mu0, &
+                                   d_adir, d_adif, d_up, d_dn, d_dir), "rte_sw: sw_solver_2stream")
+      end if
     class default
+      if (gpt) then
+        error_msg = "rte_sw: g-point fluxes of absorption-only optical properties are not produced by this build"
+        call dev_release(d_mu0); call dev_release(d_inc); call dev_release(d_dif); call dev_release(d_adir)
+        if (.not. same_array(sfc_alb_dir_gpt, sfc_alb_dif_gpt)) call dev_release(d_adif)
+        call dev_release(d_up); call dev_release(d_dn); call dev_release(d_dir)
+        return
+      end if
       ! 1scl: apply_BC(inc_flux, mu0) + sw_solver_noscat (:213-222): the direct beam only, no diffuse flux
       error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
                                  merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_mu0, d_dir), &
@@ -112,6 +146,11 @@ contains
       if (two_str) call dev_copy_out(up, d_up, nv)
       if (two_str) call dev_copy_out(dn, d_dn, nv)
       call dev_copy_out(dir, d_dir, nv)
+      if (gpt) then
+        if (associated(fluxes%gpt_flux_up)) call dev_copy_out(fluxes%gpt_flux_up, d_gup, ngv)
+        if (associated(fluxes%gpt_flux_dn)) call dev_copy_out(fluxes%gpt_flux_dn, d_gdn, ngv)
+        if (associated(fluxes%gpt_flux_dn_dir)) call dev_copy_out(fluxes%gpt_flux_dn_dir, d_gdir, ngv)
+      end if
     end if
     call rrtmgpnn_sync(error_msg, "rte_sw")
     if (error_msg == '') then
@@ -125,6 +164,7 @@ contains
     call dev_release(d_mu0); call dev_release(d_inc); call dev_release(d_dif); call dev_release(d_adir)
     if (.not. same_array(sfc_alb_dir_gpt, sfc_alb_dif_gpt)) call dev_release(d_adif)
     call dev_release(d_up); call dev_release(d_dn); call dev_release(d_dir)
+    call dev_release(d_gup); call dev_release(d_gdn); call dev_release(d_gdir)
   end function rte_sw
 
   ! whether two dummy arrays are the same actual array (same first element, same shape)

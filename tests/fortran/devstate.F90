@@ -3,22 +3,33 @@
 ! followed by update_device() is what the next rte_lw reads.
 ! usage: devstate <problem.rbin> <output.rbin> <data_dir>
 !   output: tau, lay_source, lev_source, sfc_source (as gas_optics produced them), and the LW fluxes of rte_lw run
-!   twice: on the gas-optics tau (flux_up/dn_a) and on 0.5 * tau written on the host (flux_up/dn_b).
+!   twice: on the gas-optics tau (flux_up/dn_a) and on 0.5 * tau written on the host (flux_up/dn_b); then, on that
+!   tau, ty_fluxes_flexible g-point fluxes with rte_lw's lw_Ds (c: lw_Ds(icol, igpt) = 1 + 0.01 mod(7 icol + igpt, 100))
+!   and with three Gauss angles (d), and rte_sw on two-stream properties tau = 0.1 tau_a, ssa = 0.5, g = 0.3 over the
+!   same spectral discretisation with g-point fluxes (e: mu0 = 0.6, inc_flux = 1, albedos 0.2).
 program devstate
   use mo_rte_kind,           only: wp
-  use mo_optical_props,      only: ty_optical_props_1scl
+  use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
   use mo_source_functions,   only: ty_source_func_lw
   use mo_fluxes,             only: ty_fluxes_flexible
   use mo_gas_concentrations, only: ty_gas_concs
   use mo_gas_optics_rrtmgp,  only: ty_gas_optics_rrtmgp
   use mod_network_rrtmgp,    only: rrtmgp_network_type
   use mo_rte_lw,             only: rte_lw
+  use mo_rte_sw,             only: rte_sw
   use mo_rrtmgpnn_rbin
   implicit none
   character(len=512) :: pfile, ofile, ddir
   real(wp), allocatable :: play(:,:), plev(:,:), tlay(:,:), tlev(:,:), tsfc(:), sfc_emis(:), scal(:), vmr(:,:)
   real(wp), allocatable :: emis(:,:), tau0(:,:,:), lay0(:,:,:), lev0(:,:,:), sfc0(:,:)
   real(wp), allocatable, target :: up_a(:,:), dn_a(:,:), up_b(:,:), dn_b(:,:)
+  real(wp), allocatable, target :: up_c(:,:), dn_c(:,:), gup_c(:,:,:), gdn_c(:,:,:), up_d(:,:), dn_d(:,:)
+  real(wp), allocatable, target :: gup_d(:,:,:), gdn_d(:,:,:), up_e(:,:), dn_e(:,:), dir_e(:,:)
+  real(wp), allocatable, target :: gup_e(:,:,:), gdn_e(:,:,:), gdir_e(:,:,:)
+  real(wp), allocatable :: lw_ds(:,:), inc(:,:), alb(:,:), mu0(:)
+  type(ty_optical_props_2str) :: op2
+  type(ty_fluxes_flexible) :: fl2
+  integer :: ngpt
   character(len=32), allocatable :: gas_names(:)
   type(ty_gas_concs) :: gas_concs
   type(ty_gas_optics_rrtmgp) :: kdist
@@ -76,7 +87,45 @@ program devstate
   fl%flux_up => up_b
   fl%flux_dn => dn_b
   call chk(rte_lw(op, top_at_1, src, emis, fl))
-  u = rbin_write_begin(ofile, 8)
+  ! (c) lw_Ds and g-point fluxes, (d) three angles and g-point fluxes -- on the tau of (b)
+  ngpt = kdist%get_ngpt()
+  allocate(lw_ds(ncol, ngpt))
+  do ig = 1, ngpt
+    do icol = 1, ncol
+      lw_ds(icol, ig) = 1._wp + 0.01_wp * real(mod(7 * icol + ig, 100), wp)
+    end do
+  end do
+  allocate(up_c(nlay + 1, ncol), dn_c(nlay + 1, ncol), gup_c(ngpt, nlay + 1, ncol), gdn_c(ngpt, nlay + 1, ncol))
+  fl%flux_up => up_c
+  fl%flux_dn => dn_c
+  fl%gpt_flux_up => gup_c
+  fl%gpt_flux_dn => gdn_c
+  call chk(rte_lw(op, top_at_1, src, emis, fl, lw_Ds=lw_ds))
+  allocate(up_d(nlay + 1, ncol), dn_d(nlay + 1, ncol), gup_d(ngpt, nlay + 1, ncol), gdn_d(ngpt, nlay + 1, ncol))
+  fl%flux_up => up_d
+  fl%flux_dn => dn_d
+  fl%gpt_flux_up => gup_d
+  fl%gpt_flux_dn => gdn_d
+  call chk(rte_lw(op, top_at_1, src, emis, fl, n_gauss_angles=3))
+  ! (e) rte_sw with g-point fluxes
+  call chk(op2%alloc_2str(ncol, nlay, kdist))
+  op2%tau = 0.1_wp * tau0
+  op2%ssa = 0.5_wp
+  op2%g = 0.3_wp
+  allocate(inc(ngpt, ncol), alb(ngpt, ncol), mu0(ncol))
+  inc = 1._wp
+  alb = 0.2_wp
+  mu0 = 0.6_wp
+  allocate(up_e(nlay + 1, ncol), dn_e(nlay + 1, ncol), dir_e(nlay + 1, ncol))
+  allocate(gup_e(ngpt, nlay + 1, ncol), gdn_e(ngpt, nlay + 1, ncol), gdir_e(ngpt, nlay + 1, ncol))
+  fl2%flux_up => up_e
+  fl2%flux_dn => dn_e
+  fl2%flux_dn_dir => dir_e
+  fl2%gpt_flux_up => gup_e
+  fl2%gpt_flux_dn => gdn_e
+  fl2%gpt_flux_dn_dir => gdir_e
+  call chk(rte_sw(op2, top_at_1, mu0, inc, alb, alb, fl2))
+  u = rbin_write_begin(ofile, 23)
   call rbin_write_real(u, "tau", tau0, shape(tau0))
   call rbin_write_real(u, "lay_source", lay0, shape(lay0))
   call rbin_write_real(u, "lev_source", lev0, shape(lev0))
@@ -85,6 +134,21 @@ program devstate
   call rbin_write_real(u, "flux_dn_a", dn_a, shape(dn_a))
   call rbin_write_real(u, "flux_up_b", up_b, shape(up_b))
   call rbin_write_real(u, "flux_dn_b", dn_b, shape(dn_b))
+  call rbin_write_real(u, "flux_up_c", up_c, shape(up_c))
+  call rbin_write_real(u, "flux_dn_c", dn_c, shape(dn_c))
+  call rbin_write_real(u, "gpt_up_c", gup_c, shape(gup_c))
+  call rbin_write_real(u, "gpt_dn_c", gdn_c, shape(gdn_c))
+  call rbin_write_real(u, "flux_up_d", up_d, shape(up_d))
+  call rbin_write_real(u, "flux_dn_d", dn_d, shape(dn_d))
+  call rbin_write_real(u, "gpt_up_d", gup_d, shape(gup_d))
+  call rbin_write_real(u, "gpt_dn_d", gdn_d, shape(gdn_d))
+  call rbin_write_real(u, "flux_up_e", up_e, shape(up_e))
+  call rbin_write_real(u, "flux_dn_e", dn_e, shape(dn_e))
+  call rbin_write_real(u, "flux_dir_e", dir_e, shape(dir_e))
+  call rbin_write_real(u, "gpt_up_e", gup_e, shape(gup_e))
+  call rbin_write_real(u, "gpt_dn_e", gdn_e, shape(gdn_e))
+  call rbin_write_real(u, "gpt_dir_e", gdir_e, shape(gdir_e))
+  call rbin_write_real(u, "lw_ds", lw_ds, shape(lw_ds))
   call rbin_write_end(u)
 contains
   subroutine chk(msg)

@@ -183,3 +183,21 @@ def test_fortran_device_state_update_host_and_device(tmp_path, orc, rfmip):
         up, dn = orc.lw_solver(tau, go["lay_source"], go["lev_source"], emis, go["sfc_source"], prob["top_at_1"])
         np.testing.assert_array_equal(got["flux_up_" + tag], up, err_msg=tag)
         np.testing.assert_array_equal(got["flux_dn_" + tag], dn, err_msg=tag)
+    # ty_fluxes_flexible g-point outputs: (c) with lw_Ds, (d) with three angles, on the tau of (b); (e) rte_sw
+    tau_b = (np.float32(0.5) * go["tau"]).astype(np.float32)
+    ncol = tau_b.shape[0]
+    i, g = np.meshgrid(np.arange(1, ncol + 1), np.arange(1, ngpt + 1), indexing="ij")
+    ds = (np.float32(1) + np.float32(0.01) * ((7 * i + g) % 100).astype(np.float32)).astype(np.float32)  # (ncol, ngpt)
+    np.testing.assert_array_equal(got["lw_ds"], ds.T)  # written with its Fortran extents (ncol, ngpt)
+    # the kernel reads the array's memory (Fortran order: icol fastest) as D(igpt, icol) -- quirk B-12
+    for tag, kw in (("c", dict(lw_Ds=np.ascontiguousarray(ds.T))), ("d", dict(nmus=3))):
+        want = orc.lw_solver(tau_b, go["lay_source"], go["lev_source"], emis, go["sfc_source"], prob["top_at_1"],
+                             gpt=True, **kw)
+        for k, w in zip(("flux_up_", "flux_dn_", "gpt_up_", "gpt_dn_"), want):
+            np.testing.assert_array_equal(got[k + tag], w, err_msg=k + tag)
+    t2 = (np.float32(0.1) * go["tau"]).astype(np.float32)
+    want = orc.sw_solver(t2, np.full_like(t2, 0.5), np.full_like(t2, 0.3), np.full(ncol, 0.6, np.float32),
+                         np.ones((ncol, ngpt), np.float32), np.full((ncol, ngpt), 0.2, np.float32),
+                         np.full((ncol, ngpt), 0.2, np.float32), prob["top_at_1"], gpt=True)
+    for k, w in zip(("flux_up_e", "flux_dn_e", "flux_dir_e", "gpt_up_e", "gpt_dn_e", "gpt_dir_e"), want):
+        np.testing.assert_array_equal(got[k], w, err_msg=k)
