@@ -128,7 +128,12 @@ def lib():
             raise RrtmgpnnError("librrtmgpnn.so not found at %s: build it with `make -C rte-rrtmgp-nn_amd` "
                                 "(no CPU fallback exists by design)" % LIB_PATH)
         h = ctypes.CDLL(LIB_PATH)
+        # an RRTMGPNN_LIB override (A/B runs against builds of older trees) may lack newer entry points; the
+        # shipped library must export every one (tests/test_host.py checks include/rrtmgpnn.h against it)
+        lenient = bool(os.environ.get("RRTMGPNN_LIB"))
         for name, (res, args) in SIGNATURES.items():
+            if lenient and not hasattr(h, name):
+                continue
             f = getattr(h, name)
             f.restype = res
             f.argtypes = args
