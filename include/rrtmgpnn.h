@@ -275,6 +275,28 @@ int rrtmgpnn_sw_solver_2stream_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, in
  * bit (tests/test_oracle.py).  inc_flux (ngpt, ncol), tau (ngpt, nlay, ncol), mu0 (ncol). */
 int rrtmgpnn_sw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                               const float *tau, const float *mu0, float *flux_dir);
+/* The scattering LW solvers and the SW direct beam with ty_fluxes_flexible's g-point outputs (ngpt, nlay+1, ncol),
+ * both or neither of gpt_flux_up/dn for LW.
+ * 1rescl: what lw_solver_noscat_GaussQuad leaves in flux_up_gpt/flux_dn_gpt with do_rescaling (rte/mo_rte_lw.F90:
+ *   377-387; kernels :179-281, 383-411): with one angle the radiances of the final up and down passes (quirk B-5),
+ *   with several the angle-summed fluxes.
+ * 2stream: the adding fluxes lw_solver_2stream forms per g-point (:454-485).
+ * noscat (SW, 1scl): the spectral direct beam, top level = inc_flux * mu0 (apply_BC_factor + sw_solver_noscat; the
+ *   reference's rte_sw passes a local array to apply_BC_factor when g-point fluxes are desired, :155-163, 218: this
+ *   entry applies the boundary condition to the caller's array, the evident meaning, as for B-10/B-11).
+ * Broadband outputs as the entries above, bit for bit (tests/test_gpu_gpt.py). */
+int rrtmgpnn_lw_solver_1rescl_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                  const float *Ds, const float *weights, const float *inc_flux, const float *tau,
+                                  const float *ssa, const float *g, const float *lay_source, const float *lev_source,
+                                  const float *sfc_emis_gpt, const float *sfc_source, float *flux_up, float *flux_dn,
+                                  float *gpt_flux_up, float *gpt_flux_dn);
+int rrtmgpnn_lw_solver_2stream_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                   const float *inc_flux, const float *tau, const float *ssa, const float *g,
+                                   const float *lev_source, const float *sfc_emis_gpt, const float *sfc_source,
+                                   float *flux_up, float *flux_dn, float *gpt_flux_up, float *gpt_flux_dn);
+int rrtmgpnn_sw_solver_noscat_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                  const float *inc_flux, const float *tau, const float *mu0, float *flux_dir,
+                                  float *gpt_flux_dir);
 /* rrtmgpnn_sw_solver_2stream of the atmosphere incremented by band-resolved two-stream properties
  * (tau, ssa, g)_bnd (nbnd, nlay, ncol) -- clouds%increment(atmos) (inc_2stream_by_2stream_bybnd,
  * rte/kernels/mo_optical_props_kernels.F90:430-463) fused into the solver: same fluxes, bit for bit, as

@@ -59,6 +59,7 @@ class Oracle:
         L.orc_lw_solver_noscat_ext.argtypes = [c_int] * 5 + [c_vp] * 15
         L.orc_sw_solver_2stream_gpt.argtypes = [c_int] * 4 + [c_vp] * 14
         L.orc_lw_solver_2stream.argtypes = [c_int] * 4 + [_f32p] * 9
+        L.orc_lw_solver_2stream_gpt.argtypes = [c_int] * 4 + [_f32p] * 9 + [c_vp] * 2
         L.orc_sw_solver_2stream.argtypes = [c_int, c_int, c_int, c_int, _f32p, _f32p, _f32p, _f32p, _f32p, _f32p,
                                             _f32p, _f32p, _f32p, _f32p, _f32p]
         L.orc_expand.argtypes = [c_int, c_int, c_int, _i32p, _f32p, _f32p]
@@ -193,15 +194,17 @@ class Oracle:
                                                   f32(sfc_src), up, dn)
         return up, dn
 
-    def lw_solver_2stream(self, tau, ssa, g, lev, emis_gpt, sfc_src, top_at_1=True, inc_flux=None):
-        """lw_solver_2stream (rte/kernels/mo_rte_solver_kernels.F90:426-486)."""
+    def lw_solver_2stream(self, tau, ssa, g, lev, emis_gpt, sfc_src, top_at_1=True, inc_flux=None, gpt=False):
+        """lw_solver_2stream (rte/kernels/mo_rte_solver_kernels.F90:426-486); gpt: also the g-point fluxes
+        flux_up_gpt / flux_dn_gpt (ncol, nlay+1, ngpt)."""
         ncol, nlay, ngpt = tau.shape
         up = np.zeros((ncol, nlay + 1), np.float32)
         dn = np.zeros((ncol, nlay + 1), np.float32)
         inc = f32(inc_flux) if inc_flux is not None else np.zeros((ncol, ngpt), np.float32)
-        self.L.orc_lw_solver_2stream(ngpt, nlay, ncol, int(top_at_1), inc, f32(tau), f32(ssa), f32(g), f32(lev),
-                                     f32(emis_gpt), f32(sfc_src), up, dn)
-        return up, dn
+        gp = [np.zeros((ncol, nlay + 1, ngpt), np.float32) for _ in range(2)] if gpt else [None, None]
+        self.L.orc_lw_solver_2stream_gpt(ngpt, nlay, ncol, int(top_at_1), inc, f32(tau), f32(ssa), f32(g), f32(lev),
+                                         f32(emis_gpt), f32(sfc_src), up, dn, _ptr(gp[0]), _ptr(gp[1]))
+        return (up, dn, gp[0], gp[1]) if gpt else (up, dn)
 
     def sw_solver(self, tau, ssa, g, mu0, inc_flux, alb_dir_gpt, alb_dif_gpt, top_at_1=True, inc_flux_dif=None,
                   gpt=False):
@@ -401,6 +404,8 @@ class Reference:
         L.ref_rte_lw_gpt.restype = c_int
         L.ref_rte_sw_gpt.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int] + [_f32p] * 13
         L.ref_rte_sw_gpt.restype = c_int
+        L.ref_rte_lw_2str_gpt.argtypes = [c_int, c_int, c_int, c_int, _i32p, _f32p, c_int, c_int, c_int] + [_f32p] * 12
+        L.ref_rte_lw_2str_gpt.restype = c_int
 
     def sw_noscat(self, tau, mu0, inc_flux, top_at_1=True):
         """The reference's apply_BC (-> apply_BC_factor) + sw_solver_noscat kernels: broadband and spectral direct
@@ -427,6 +432,19 @@ class Reference:
                                            int(top_at_1), nmus, int(use_2stream), f32(tau), f32(ssa), f32(g), f32(lay),
                                            f32(lev), f32(sfc_src), f32(sfc_jac), f32(sfc_emis_band), up, dn))
         return up, dn
+
+    def rte_lw_2str_gpt(self, kd, tau, ssa, g, lay, lev, sfc_src, sfc_jac, sfc_emis_band, top_at_1=True, nmus=1,
+                        use_2stream=False):
+        """rte_lw_2str with ty_fluxes_flexible g-point outputs (ncol, nlay+1, ngpt)."""
+        ncol, nlay, ngpt = tau.shape
+        out = [np.zeros((ncol, nlay + 1), np.float32) for _ in range(2)]
+        gp = [np.zeros((ncol, nlay + 1, ngpt), np.float32) for _ in range(2)]
+        self._check(self.L.ref_rte_lw_2str_gpt(ncol, nlay, kd["nband"], ngpt,
+                                               np.ascontiguousarray(kd["band_lims_gpt"], np.int32),
+                                               f32(kd["band_lims_wvn"]), int(top_at_1), nmus, int(use_2stream),
+                                               f32(tau), f32(ssa), f32(g), f32(lay), f32(lev), f32(sfc_src),
+                                               f32(sfc_jac), f32(sfc_emis_band), *out, *gp))
+        return out[0], out[1], gp[0], gp[1]
 
     def rte_lw(self, kd, tau, lay, lev, sfc_src, sfc_jac, sfc_emis_band, top_at_1=True, nmus=1):
         ncol, nlay, ngpt = tau.shape

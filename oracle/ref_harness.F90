@@ -115,6 +115,46 @@ contains
     ref_rte_lw_2str = 0
   end function ref_rte_lw_2str
 
+  ! ref_rte_lw_2str with the caller's g-point outputs associated (ty_fluxes_flexible gpt_flux_up/dn): the rescaled
+  ! solution's radiances (one angle) or angle-summed fluxes, or lw_solver_2stream's adding fluxes.
+  integer(c_int) function ref_rte_lw_2str_gpt(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, top_at_1, nmus, &
+                                              use_2stream, tau, ssa, g, lay_src, lev_src, sfc_src, sfc_src_jac, &
+                                              sfc_emis, flux_up, flux_dn, gpt_up, gpt_dn) bind(C, name="ref_rte_lw_2str_gpt")
+    integer(c_int), value :: ncol, nlay, nband, ngpt, top_at_1, nmus, use_2stream
+    integer(c_int), intent(in) :: band_lims_gpt(2, nband)
+    real(c_float),  intent(in) :: band_lims_wvn(2, nband)
+    real(c_float),  intent(in) :: tau(ngpt, nlay, ncol), ssa(ngpt, nlay, ncol), g(ngpt, nlay, ncol)
+    real(c_float),  intent(in) :: lay_src(ngpt, nlay, ncol), lev_src(ngpt, nlay+1, ncol)
+    real(c_float),  intent(in) :: sfc_src(ngpt, ncol), sfc_src_jac(ngpt, ncol), sfc_emis(nband, ncol)
+    real(c_float),  intent(out), target :: flux_up(nlay+1, ncol), flux_dn(nlay+1, ncol)
+    real(c_float),  intent(out), target :: gpt_up(ngpt, nlay+1, ncol), gpt_dn(ngpt, nlay+1, ncol)
+
+    type(ty_optical_props_2str) :: op
+    type(ty_source_func_lw)     :: src
+    type(ty_fluxes_flexible)    :: fl
+    character(len=128) :: err
+
+    ref_rte_lw_2str_gpt = 1
+    err = op%alloc_2str(ncol, nlay, band_lims_wvn, band_lims_gpt)
+    if (err /= '') then; last_msg = err; return; end if
+    err = src%alloc(ncol, nlay, op)
+    if (err /= '') then; last_msg = err; return; end if
+    op%tau = tau
+    op%ssa = ssa
+    op%g = g
+    src%lay_source = lay_src
+    src%lev_source = lev_src
+    src%sfc_source = sfc_src
+    src%sfc_source_Jac = sfc_src_jac
+    fl%flux_up => flux_up
+    fl%flux_dn => flux_dn
+    fl%gpt_flux_up => gpt_up
+    fl%gpt_flux_dn => gpt_dn
+    err = rte_lw(op, top_at_1 /= 0, src, sfc_emis, fl, n_gauss_angles=int(nmus), use_2stream=use_2stream /= 0)
+    if (err /= '') then; last_msg = err; return; end if
+    ref_rte_lw_2str_gpt = 0
+  end function ref_rte_lw_2str_gpt
+
   integer(c_int) function ref_rte_sw(ncol, nlay, nband, ngpt, band_lims_gpt, band_lims_wvn, top_at_1, &
                                      tau, ssa, g, mu0, inc_flux, sfc_alb_dir, sfc_alb_dif, &
                                      flux_up, flux_dn, flux_dir) bind(C, name="ref_rte_sw")

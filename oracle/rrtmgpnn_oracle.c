@@ -493,9 +493,11 @@ static void adding_col(int ngpt, int nlay, int top_at_1, const float *albedo_sfc
  * (:1018-1069, Fu et al. 1997 coefficients, LW_diff_sec = 1.66), lw_source_2str (:1112-1162, Toon et al.
  * linear-in-tau sources), adding (:1526-1637) and sum_broadband_nocol (plain sequential sums).
  * ------------------------------------------------------------------------------------------- */
-void orc_lw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux, const float *tau,
-                           const float *ssa, const float *gg, const float *lev_source, const float *sfc_emis,
-                           const float *sfc_source, float *flux_up, float *flux_dn)
+/* gpt_up/gpt_dn (may be NULL, (ngpt, nlay+1, ncol)): flux_up_gpt / flux_dn_gpt, the adding fluxes per g-point
+ * (:443, 481), which the reference always forms (in the caller's arrays when ty_fluxes_flexible asks for them) */
+void orc_lw_solver_2stream_gpt(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux, const float *tau,
+                               const float *ssa, const float *gg, const float *lev_source, const float *sfc_emis,
+                               const float *sfc_source, float *flux_up, float *flux_dn, float *gpt_up, float *gpt_dn)
 {
   const float k_min = 1.e-4f, LW_diff_sec = 1.66f;
 #pragma omp parallel
@@ -552,9 +554,19 @@ void orc_lw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const flo
         for (int i = 0; i < ngpt; i++) { a += rup[i + (size_t)ngpt * l]; b += rdn[i + (size_t)ngpt * l]; }
         fu[l] = a; fd[l] = b;
       }
+      if (gpt_up)
+        for (size_t i = 0; i < nv; i++) { gpt_up[nv * icol + i] = rup[i]; gpt_dn[nv * icol + i] = rdn[i]; }
     }
     free(buf);
   }
+}
+
+void orc_lw_solver_2stream(int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux, const float *tau,
+                           const float *ssa, const float *gg, const float *lev_source, const float *sfc_emis,
+                           const float *sfc_source, float *flux_up, float *flux_dn)
+{
+  orc_lw_solver_2stream_gpt(ngpt, nlay, ncol, top_at_1, inc_flux, tau, ssa, gg, lev_source, sfc_emis, sfc_source,
+                            flux_up, flux_dn, NULL, NULL);
 }
 
 /* ---------------------------------------------------------------------------------------------

@@ -778,6 +778,38 @@ int rrtmgpnn_sw_solver_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int nco
   return launch_sw_noscat(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, mu0, flux_dir);
 }
 
+int rrtmgpnn_lw_solver_1rescl_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus,
+                                  const float *Ds, const float *weights, const float *inc_flux, const float *tau,
+                                  const float *ssa, const float *g, const float *lay_source, const float *lev_source,
+                                  const float *sfc_emis_gpt, const float *sfc_source, float *flux_up, float *flux_dn,
+                                  float *gpt_flux_up, float *gpt_flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  ExtrasScope x(ctx, nullptr, gpt_flux_up, gpt_flux_dn, nullptr);
+  return rrtmgpnn_lw_solver_1rescl(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, inc_flux, tau, ssa, g,
+                                   lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn);
+}
+
+int rrtmgpnn_lw_solver_2stream_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                   const float *inc_flux, const float *tau, const float *ssa, const float *g,
+                                   const float *lev_source, const float *sfc_emis_gpt, const float *sfc_source,
+                                   float *flux_up, float *flux_dn, float *gpt_flux_up, float *gpt_flux_dn)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  ExtrasScope x(ctx, nullptr, gpt_flux_up, gpt_flux_dn, nullptr);
+  return rrtmgpnn_lw_solver_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, ssa, g, lev_source, sfc_emis_gpt,
+                                    sfc_source, flux_up, flux_dn);
+}
+
+int rrtmgpnn_sw_solver_noscat_gpt(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                  const float *inc_flux, const float *tau, const float *mu0, float *flux_dir,
+                                  float *gpt_flux_dir)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  ExtrasScope x(ctx, nullptr, nullptr, nullptr, gpt_flux_dir);
+  return rrtmgpnn_sw_solver_noscat(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, mu0, flux_dir);
+}
+
 int rrtmgpnn_sw_solver_2stream_inc(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
                                    const float *inc_flux, const float *inc_flux_dif, const float *tau,
                                    const float *ssa, const float *g, int nbnd, const int *band_lims_gpt,

@@ -48,13 +48,18 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
                                                        const float *__restrict__ gg, const float *__restrict__ lay,
                                                        const float *__restrict__ lev, const float *__restrict__ emis,
                                                        const float *__restrict__ sfc, float *__restrict__ ws,
-                                                       float *__restrict__ flux_up, float *__restrict__ flux_dn)
+                                                       float *__restrict__ flux_up, float *__restrict__ flux_dn,
+                                                       float *__restrict__ gpt_up, float *__restrict__ gpt_dn)
 {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
   const int gc = on ? g : ngpt - 1;
   const int nlev = nlay + 1;
+  // ty_fluxes_flexible g-point outputs (ngpt, nlev, ncol): with one angle the radiances (quirk B-5), with several they
+  // are the angle accumulators
+  const bool gpt = gpt_up != nullptr;
+  float *gdn = gpt ? gpt_dn + (size_t)ngpt * nlev * icol : nullptr, *gup = gpt ? gpt_up + (size_t)ngpt * nlev * icol : nullptr;
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   float *ring = smem + kExpTabFloats;                 // [kScatRing][ngpt]
   float *part = ring + (size_t)kScatRing * ngpt;      // [2][nlev][4]: 0 = dn, 1 = up
@@ -80,13 +85,15 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
     const float D = ang.D[imu];
     const float fac = (multi || (ngpt & 3) == 0) ? 2.0f * kPi * ang.w[imu] : 1.0f;  // quirk B-5 as noscat
     const bool acc = imu > 0;
-    auto put = [&](float v, int r, int q, int level) {
+    // v = fac * radiance; rad = the radiance
+    auto put = [&](float v, float rad, int r, int q, int level) {
       if (!on) return;
       if (multi) {
-        float *w = acc_base + ((size_t)q * nlev + level) * ngpt + g;
+        float *w = (gpt ? (q == 0 ? gdn : gup) + (size_t)level * ngpt : acc_base + ((size_t)q * nlev + level) * ngpt) + g;
         *w = acc ? *w + v : v;
       } else {
         ring[(size_t)r * ngpt + g] = v;
+        if (gpt) (q == 0 ? gdn : gup)[(size_t)level * ngpt + g] = rad;
       }
     };
     auto flush = [&](float *pq, int n, int lev0, int dl) {
@@ -105,7 +112,7 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
     // surface reflection and emission
     float U = I * (1.0f - e) + e * ss;
     if (on) WU[X(sfcl)] = U;
-    put(fac * U, 0, 1, sfcl);
+    put(fac * U, U, 0, 1, sfcl);
     flush(pup, 1, sfcl, 1);
     // 2: up with the adjustment from the first-pass radiance at the layer top (lw_transport_1rescl)
     for (int j0 = 0; j0 < nlay; j0 += kScatRing) {
@@ -118,7 +125,7 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
           const float adj = r.Cn * (r.An * WD[X(ltop)] - r.trans * r.sdn - r.sup);
           U = r.trans * U + r.sup + adj;
           if (on) WU[X(ltop)] = U;
-          put(fac * U, s, 1, ltop);
+          put(fac * U, U, s, 1, ltop);
         }
       }
       flush(pup, min(kScatRing, nlay - j0), sfcl - dl_dn * (j0 + 1), -dl_dn);
@@ -126,7 +133,7 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
     // 3: down again with the adjustment from radn_up(l) in array order: the layer top when top_at_1, the
     //    layer bottom otherwise (:1761-1767 vs :1783-1789, reproduced)
     I = I0;
-    put(fac * I, 0, 0, top);
+    put(fac * I, I, 0, 0, top);
     flush(pdn, 1, top, 1);
     for (int j0 = 0; j0 < nlay; j0 += kScatRing) {
       for (int s = 0; s < kScatRing; s++) {
@@ -136,7 +143,7 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
           const RsLayer r = layer(l, D);
           const float adj = r.Cn * (r.An * WU[X(l)] - r.trans * r.sup - r.sdn);
           I = r.trans * I + r.sdn + adj;
-          put(fac * I, s, 0, top_at_1 ? l + 1 : l);
+          put(fac * I, I, s, 0, top_at_1 ? l + 1 : l);
         }
       }
       flush(pdn, min(kScatRing, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
@@ -145,7 +152,7 @@ __global__ void __launch_bounds__(256) lw_rescl_kernel(int ngpt, int nlay, int n
   if (multi) {
     __syncthreads();
     for (int t = g; t < 2 * nlev; t += blockDim.x) {
-      const float *w = acc_base + (size_t)t * ngpt;
+      const float *w = gpt ? (t < nlev ? gdn : gup) + (size_t)(t % nlev) * ngpt : acc_base + (size_t)t * ngpt;
       float s = 0.0f;
       for (int i = 0; i < ngpt; i++) s = s + w[i];  // sum_broadband: sequential over g
       const int l = t % nlev;
@@ -196,7 +203,8 @@ __global__ void __launch_bounds__(256) lw_2stream_kernel(int ngpt, int nlay, int
                                                          const float *__restrict__ gg, const float *__restrict__ lev,
                                                          const float *__restrict__ emis,
                                                          const float *__restrict__ sfc, float *__restrict__ ws,
-                                                         float *__restrict__ flux_up, float *__restrict__ flux_dn)
+                                                         float *__restrict__ flux_up, float *__restrict__ flux_dn,
+                                                         float *__restrict__ gpt_up, float *__restrict__ gpt_dn)
 {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int icol = blockIdx.x, g = threadIdx.x;
@@ -239,17 +247,23 @@ __global__ void __launch_bounds__(256) lw_2stream_kernel(int ngpt, int nlay, int
     src_b = src;
   }
   // top to bottom: fluxes (Eqs 12-13), sum_broadband_nocol = sum(flux, 1): sequential over g
-  auto put = [&](float up, float dn, int s) {
+  // level `lev` of the g-point outputs (flux_up_gpt / flux_dn_gpt, :481-483), when asked for
+  float *gu = gpt_up ? gpt_up + (size_t)ngpt * nlev * icol : nullptr, *gd = gpt_dn ? gpt_dn + (size_t)ngpt * nlev * icol : nullptr;
+  auto put = [&](float up, float dn, int s, int lev) {
     if (on) {
       ring[(size_t)s * ngpt + g] = up;
       ring[((size_t)kScatRing + s) * ngpt + g] = dn;
+      if (gu) {
+        gu[(size_t)lev * ngpt + g] = up;
+        gd[(size_t)lev * ngpt + g] = dn;
+      }
     }
   };
   auto flush = [&](int n, int lev0, int dl) {
     ring_flush<kScatRing>(ring, part, 2, n, lev0, dl, ngpt, nlev, false, true);
   };
   float Fdn = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
-  put(Fdn * alb_b + src_b, Fdn, 0);
+  put(Fdn * alb_b + src_b, Fdn, 0, top);
   flush(1, top, 1);
   for (int j0 = 0; j0 < nlay; j0 += kScatRing) {
     for (int s = 0; s < kScatRing; s++) {
@@ -260,7 +274,7 @@ __global__ void __launch_bounds__(256) lw_2stream_kernel(int ngpt, int nlay, int
         const float alb = WA[X(lbelow)], src = WS[X(lbelow)];
         const float denom = 1.0f / (1.0f - r.Rdif * alb);
         Fdn = (r.Tdif * Fdn + r.Rdif * src + r.sdn) * denom;
-        put(Fdn * alb + src, Fdn, s);
+        put(Fdn * alb + src, Fdn, s, lbelow);
       }
     }
     flush(min(kScatRing, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
@@ -287,9 +301,12 @@ int launch_lw_rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw rescaled solver: too many layers for LDS partials");
   void *ws = nullptr;
   if (int rc = ctx->workspace(sizeof(float) * (nmus > 1 ? 4 : 2) * (size_t)ngpt * (nlay + 1) * ncol, &ws)) return rc;
+  const auto &ex = ctx->extras;
+  if ((ex.gpt_up == nullptr) != (ex.gpt_dn == nullptr))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: g-point outputs need both gpt_flux_up and gpt_flux_dn");
   hipLaunchKernelGGL(lw_rescl_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1, a,
                      inc_flux, tau, ssa, g, lay_source, lev_source, sfc_emis, sfc_source, (float *)ws, flux_up,
-                     flux_dn);
+                     flux_dn, ex.gpt_up, ex.gpt_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_rescl_kernel");
   return RRTMGPNN_OK;
 }
@@ -305,8 +322,12 @@ int launch_lw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw two-stream solver: too many layers for LDS partials");
   void *ws = nullptr;
   if (int rc = ctx->workspace(sizeof(float) * 2 * (size_t)ngpt * (nlay + 1) * ncol, &ws)) return rc;
+  const auto &ex = ctx->extras;
+  if ((ex.gpt_up == nullptr) != (ex.gpt_dn == nullptr))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "lw solver: g-point outputs need both gpt_flux_up and gpt_flux_dn");
   hipLaunchKernelGGL(lw_2stream_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, ncol, top_at_1,
-                     inc_flux, tau, ssa, g, lev_source, sfc_emis, sfc_source, (float *)ws, flux_up, flux_dn);
+                     inc_flux, tau, ssa, g, lev_source, sfc_emis, sfc_source, (float *)ws, flux_up, flux_dn, ex.gpt_up,
+                     ex.gpt_dn);
   RRTMGPNN_LAUNCH_CHECK("lw_2stream_kernel");
   return RRTMGPNN_OK;
 }

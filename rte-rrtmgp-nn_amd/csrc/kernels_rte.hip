@@ -800,7 +800,7 @@ constexpr int kNsRing = 8;
 __global__ void __launch_bounds__(1024) sw_noscat_kernel(int ngpt, int nlay, int top_at_1,
                                                          const float *__restrict__ inc_flux,
                                                          const float *__restrict__ tau, const float *__restrict__ mu0p,
-                                                         float *__restrict__ flux_dir)
+                                                         float *__restrict__ flux_dir, float *__restrict__ gpt_dir)
 {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
@@ -824,8 +824,11 @@ __global__ void __launch_bounds__(1024) sw_noscat_kernel(int ngpt, int nlay, int
     }
     __syncthreads();
   };
+  // g-point direct flux (ty_fluxes_flexible gpt_flux_dn_dir, (ngpt, nlev, ncol)) when asked for
+  float *gcol = gpt_dir ? gpt_dir + (size_t)ngpt * nlev * icol : nullptr;
   float F = inc_flux[gc + (size_t)ngpt * icol] * mu0;
   if (on) ring[g] = F;
+  if (on && gcol) gcol[(size_t)ngpt * top + g] = F;
   flush(1, top);
   for (int j0 = 0; j0 < nlay; j0 += kNsRing) {
     const int n = min(kNsRing, nlay - j0);
@@ -840,6 +843,7 @@ __global__ void __launch_bounds__(1024) sw_noscat_kernel(int ngpt, int nlay, int
       if (r < n) {
         F = F * solver_exp_beam(-tv[r] * mu0_inv, etab);
         if (on) ring[(size_t)r * ngpt + g] = F;
+        if (on && gcol) gcol[(size_t)ngpt * (top + dl * (j0 + r + 1)) + g] = F;
       }
     }
     flush(n, top + dl * (j0 + 1));
@@ -854,7 +858,7 @@ int launch_sw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
   const int threads = (ngpt + 63) / 64 * 64;
   const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kNsRing * ngpt);
   hipLaunchKernelGGL(sw_noscat_kernel, dim3(ncol), dim3(threads), lds, ctx->stream, ngpt, nlay, top_at_1, inc_flux,
-                     tau, mu0, flux_dir);
+                     tau, mu0, flux_dir, ctx->extras.gpt_dir);
   RRTMGPNN_LAUNCH_CHECK("sw_noscat_kernel");
   return RRTMGPNN_OK;
 }

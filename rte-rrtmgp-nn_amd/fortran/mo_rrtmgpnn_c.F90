@@ -16,6 +16,7 @@ module mo_rrtmgpnn_c
             c_rrtmgpnn_sw_solver_noscat
   public :: c_rrtmgpnn_compute_heating_rate
   public :: c_rrtmgpnn_lw_solver_noscat_gpt, c_rrtmgpnn_lw_solver_noscat_planck_gpt, c_rrtmgpnn_sw_solver_2stream_gpt
+  public :: c_rrtmgpnn_lw_solver_1rescl_gpt, c_rrtmgpnn_lw_solver_2stream_gpt, c_rrtmgpnn_sw_solver_noscat_gpt
   public :: c_rrtmgpnn_network_load, c_rrtmgpnn_compute_nn_inputs, c_rrtmgpnn_get_col_dry, &
             c_rrtmgpnn_interpolate_tlev, c_rrtmgpnn_predict_nn_lw, c_rrtmgpnn_predict_nn_sw, &
             c_rrtmgpnn_compute_planck_source_nn, c_rrtmgpnn_lw_solver_noscat, c_rrtmgpnn_sw_solver_2stream, &
@@ -235,6 +236,29 @@ module mo_rrtmgpnn_c
                             flux_dn
       integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus
       real(c_float), dimension(*), intent(in) :: Ds, weights
+    end function
+    integer(c_int) function c_rrtmgpnn_lw_solver_1rescl_gpt(ctx, ngpt, nlay, ncol, top_at_1, nmus, Ds, weights, &
+        inc_flux, tau, ssa, g, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn, gpt_flux_up, &
+        gpt_flux_dn) bind(C, name="rrtmgpnn_lw_solver_1rescl_gpt")
+      import :: c_int, c_ptr, c_float
+      type(c_ptr), value :: ctx, inc_flux, tau, ssa, g, lay_source, lev_source, sfc_emis_gpt, sfc_source, flux_up, &
+                            flux_dn, gpt_flux_up, gpt_flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1, nmus
+      real(c_float), dimension(*), intent(in) :: Ds, weights
+    end function
+    integer(c_int) function c_rrtmgpnn_lw_solver_2stream_gpt(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, ssa, g, &
+        lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn, gpt_flux_up, gpt_flux_dn) &
+        bind(C, name="rrtmgpnn_lw_solver_2stream_gpt")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, inc_flux, tau, ssa, g, lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn, &
+                            gpt_flux_up, gpt_flux_dn
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1
+    end function
+    integer(c_int) function c_rrtmgpnn_sw_solver_noscat_gpt(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, mu0, &
+        flux_dir, gpt_flux_dir) bind(C, name="rrtmgpnn_sw_solver_noscat_gpt")
+      import :: c_int, c_ptr
+      type(c_ptr), value :: ctx, inc_flux, tau, mu0, flux_dir, gpt_flux_dir
+      integer(c_int), value :: ngpt, nlay, ncol, top_at_1
     end function
     integer(c_int) function c_rrtmgpnn_lw_solver_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, tau, ssa, g, &
         lev_source, sfc_emis_gpt, sfc_source, flux_up, flux_dn) bind(C, name="rrtmgpnn_lw_solver_2stream")

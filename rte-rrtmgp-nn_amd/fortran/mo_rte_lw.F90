@@ -5,8 +5,9 @@
 ! (rrtmgpnn_lw_solver_noscat_planck, emissivity expanded by band in-kernel); the broadband reduction is fused into
 ! every solver, and the fluxes come back into the caller's flux_up / flux_dn / flux_net.
 ! 1scl: lw_solver_noscat_GaussQuad; 2str: the rescaled solution (default) or lw_solver_2stream
-! (use_2stream).  ty_fluxes_flexible g-point fluxes and lw_Ds on 1scl properties (rrtmgpnn_lw_solver_noscat[_planck]_gpt:
-! with one angle the g-point radiances, quirk B-5); on 2str properties and for the Jacobians an error string.
+! (use_2stream).  ty_fluxes_flexible g-point fluxes through the *_gpt entries: no-scattering and rescaled solutions
+! with one angle the g-point radiances (quirk B-5), with several the angle-summed fluxes; lw_solver_2stream the adding
+! fluxes.  lw_Ds on 1scl properties; the Jacobians an error string (compute_Jac = .false.).
 module mo_rte_lw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,         only: wp
@@ -127,9 +128,6 @@ contains
       if (present(lw_Ds)) then
         error_msg = "rte_lw: lw_Ds not valid input for _2str class"; return
       end if
-      if (fluxes%are_desired_gpt()) then
-        error_msg = "rte_lw: g-point fluxes of two-stream optical properties are not produced by this build"; return
-      end if
       if (use_2s .and. nmus /= 1) then
         error_msg = "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"; return
       end if
@@ -150,7 +148,7 @@ contains
     if (present(inc_flux)) d_inc = dev_stage(inc_flux, nsfc)
     d_up = dev_scratch(nv)
     d_dn = dev_scratch(nv)
-    ! ty_fluxes_flexible g-point outputs and lw_Ds (1scl): the *_gpt entries
+    ! ty_fluxes_flexible g-point outputs and lw_Ds: the *_gpt entries (NULL outputs: the plain solvers)
     gpt = fluxes%are_desired_gpt()
     ngv = int(ngpt, c_long_long) * (nlay + 1) * ncol
     d_ds = c_null_ptr
@@ -190,14 +188,14 @@ contains
           d_g = dev_g_read(optical_props, g_tmp)
         end select
         if (two_str .and. use_2s) then
-          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_2stream(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_2stream_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
                                      merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_ssa, d_g, d_lev, d_emis_gpt, &
-                                     d_sfc, d_up, d_dn), "rte_lw: lw_solver_2stream")
+                                     d_sfc, d_up, d_dn, d_gup, d_gdn), "rte_lw: lw_solver_2stream")
         else if (two_str) then
-          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_1rescl(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+          error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_1rescl_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
                                      merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &
                                      gauss_wts(1:nmus, nmus), d_inc, d_tau, d_ssa, d_g, d_lay, d_lev, d_emis_gpt, &
-                                     d_sfc, d_up, d_dn), "rte_lw: lw_solver_noscat (rescaled)")
+                                     d_sfc, d_up, d_dn, d_gup, d_gdn), "rte_lw: lw_solver_noscat (rescaled)")
         else
           error_msg = rrtmgpnn_check(c_rrtmgpnn_lw_solver_noscat_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
                                      merge(1_c_int, 0_c_int, top_at_1), nmus, gauss_Ds(1:nmus, nmus), &

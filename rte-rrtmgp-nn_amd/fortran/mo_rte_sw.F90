@@ -3,7 +3,8 @@
 ! solver (sw_solver_2stream, rte/kernels/mo_rte_solver_kernels.F90:541-692) as one HIP kernel with the broadband
 ! reduction fused in; 1scl: apply_BC + sw_solver_noscat (:213-222), the direct beam only (flux_dn_dir; flux_up /
 ! flux_dn are left as they are, as in the reference).  ty_fluxes_flexible g-point fluxes on 2str properties
-! (rrtmgpnn_sw_solver_2stream_gpt: up, total down, direct, :155-173, 228-234); on 1scl an error string.
+! (rrtmgpnn_sw_solver_2stream_gpt: up, total down, direct, :155-173, 228-234) and on 1scl properties the spectral
+! direct beam into gpt_flux_dn_dir (rrtmgpnn_sw_solver_noscat_gpt, :155-163, 218-222).
 module mo_rte_sw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,      only: wp
@@ -129,16 +130,11 @@ contains
                                    d_adir, d_adif, d_up, d_dn, d_dir), "rte_sw: sw_solver_2stream")
       end if
     class default
-      if (gpt) then
-        error_msg = "rte_sw: g-point fluxes of absorption-only optical properties are not produced by this build"
-        call dev_release(d_mu0); call dev_release(d_inc); call dev_release(d_dif); call dev_release(d_adir)
-        if (.not. same_array(sfc_alb_dir_gpt, sfc_alb_dif_gpt)) call dev_release(d_adif)
-        call dev_release(d_up); call dev_release(d_dn); call dev_release(d_dir)
-        return
-      end if
-      ! 1scl: apply_BC(inc_flux, mu0) + sw_solver_noscat (:213-222): the direct beam only, no diffuse flux
-      error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_noscat(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
-                                 merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_mu0, d_dir), &
+      ! 1scl: apply_BC(inc_flux, mu0) + sw_solver_noscat (:213-222): the direct beam only, no diffuse flux; with
+      ! g-point outputs the spectral beam (the reference does not write gpt_flux_up / gpt_flux_dn here)
+      if (gpt .and. associated(fluxes%gpt_flux_dn_dir)) d_gdir = dev_scratch(ngv)
+      error_msg = rrtmgpnn_check(c_rrtmgpnn_sw_solver_noscat_gpt(rrtmgpnn_ctx(), ngpt, nlay, ncol, &
+                                 merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_mu0, d_dir, d_gdir), &
                                  "rte_sw: sw_solver_noscat")
     end select
     allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol), dir(nlay + 1, ncol))
@@ -146,11 +142,11 @@ contains
       if (two_str) call dev_copy_out(up, d_up, nv)
       if (two_str) call dev_copy_out(dn, d_dn, nv)
       call dev_copy_out(dir, d_dir, nv)
-      if (gpt) then
+      if (gpt .and. two_str) then
         if (associated(fluxes%gpt_flux_up)) call dev_copy_out(fluxes%gpt_flux_up, d_gup, ngv)
         if (associated(fluxes%gpt_flux_dn)) call dev_copy_out(fluxes%gpt_flux_dn, d_gdn, ngv)
-        if (associated(fluxes%gpt_flux_dn_dir)) call dev_copy_out(fluxes%gpt_flux_dn_dir, d_gdir, ngv)
       end if
+      if (gpt .and. associated(fluxes%gpt_flux_dn_dir)) call dev_copy_out(fluxes%gpt_flux_dn_dir, d_gdir, ngv)
     end if
     call rrtmgpnn_sync(error_msg, "rte_sw")
     if (error_msg == '') then

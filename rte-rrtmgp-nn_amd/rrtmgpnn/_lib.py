@@ -86,6 +86,10 @@ SIGNATURES = {
                                                      c_vp, c_int, P(c_int), c_float, c_float, c_vp, c_int, c_vp,
                                                      c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_sw_solver_2stream_gpt": (c_int, [c_vp, c_int, c_int, c_int, c_int] + [c_vp] * 14),
+    "rrtmgpnn_lw_solver_1rescl_gpt": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, P(c_float), P(c_float)]
+                                      + [c_vp] * 12),
+    "rrtmgpnn_lw_solver_2stream_gpt": (c_int, [c_vp, c_int, c_int, c_int, c_int] + [c_vp] * 11),
+    "rrtmgpnn_sw_solver_noscat_gpt": (c_int, [c_vp, c_int, c_int, c_int, c_int] + [c_vp] * 5),
     "rrtmgpnn_expand_band_to_gpt": (c_int, [c_vp, c_int, c_int, c_int, P(c_int), c_vp, c_vp]),
     "rrtmgpnn_compute_heating_rate": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_calc_heating_rate_k_day": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),

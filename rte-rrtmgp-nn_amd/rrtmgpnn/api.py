@@ -404,9 +404,10 @@ class FluxesBroadband:
 
 class FluxesFlexible(FluxesBroadband):
     """ty_fluxes_flexible (rte/mo_fluxes.F90:57-67): the broadband outputs plus g-point fluxes, (ncol, nlay+1, ngpt)
-    tensors the caller allocates.  rte_lw fills gpt_flux_up/dn (1scl properties; with one angle the g-point radiances,
-    quirk B-5), rte_sw gpt_flux_up/dn (total)/dn_dir (2str properties); gpt_flux_net is not written (as in the
-    reference)."""
+    tensors the caller allocates.  rte_lw fills gpt_flux_up/dn (no-scattering and rescaled solutions: with one angle
+    the g-point radiances, quirk B-5, with several the angle-summed fluxes; use_2stream: the adding fluxes), rte_sw
+    gpt_flux_up/dn (total)/dn_dir on 2str properties and gpt_flux_dn_dir (the spectral direct beam) on 1scl ones;
+    gpt_flux_net is not written (as in the reference)."""
 
     def __init__(self, flux_up=None, flux_dn=None, flux_dn_dir=None, flux_net=None, gpt_flux_up=None,
                  gpt_flux_dn=None, gpt_flux_dn_dir=None, gpt_flux_net=None):
@@ -760,8 +761,6 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
         if nmu != 1:
             return "rte_lw: providing lw_Ds incompatible with specifying n_gauss_angles"
     gpt = fluxes.are_desired_gpt()
-    if gpt and is2:
-        return "rte_lw: g-point fluxes of two-stream optical properties are not produced by this build"
     if gpt:
         for a in (fluxes.gpt_flux_up, fluxes.gpt_flux_dn):
             if a is not None and tuple(a.shape) != (ncol, nlay + 1, ngpt):
@@ -780,28 +779,36 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
     up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=emis.device)
     dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=emis.device)
     op = optical_props
+    # ty_fluxes_flexible g-point outputs (:275-288): the caller's arrays, scratch for the one not asked for
+    gu = gd = None
+    if gpt:
+        gu = fluxes.gpt_flux_up if fluxes.gpt_flux_up is not None else \
+            torch.empty((ncol, nlay + 1, ngpt), device=emis.device)
+        gd = fluxes.gpt_flux_dn if fluxes.gpt_flux_dn is not None else \
+            torch.empty((ncol, nlay + 1, ngpt), device=emis.device)
     if is2 and use_2stream:  # lw_solver_2stream (rte/mo_rte_lw.F90:357-371); validate() runs unconditionally
         e = op.validate()
         if e:
             return e
-        check(L.rrtmgpnn_lw_solver_2stream(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux), _p(op.tau),
-                                           _p(op.ssa), _p(op.g), _p(sources.lev_source), _p(emis_gpt),
-                                           _p(sources.sfc_source), _p(up), _p(dn)), "lw_solver_2stream")
+        common = (ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux), _p(op.tau), _p(op.ssa), _p(op.g),
+                  _p(sources.lev_source), _p(emis_gpt), _p(sources.sfc_source), _p(up), _p(dn))
+        if gpt:
+            check(L.rrtmgpnn_lw_solver_2stream_gpt(*common, _p(gu), _p(gd)), "lw_solver_2stream_gpt")
+        else:
+            check(L.rrtmgpnn_lw_solver_2stream(*common), "lw_solver_2stream")
     elif is2:  # rescaled no-scattering solution (:372-387)
         if check_values:
             e = op.validate()
             if e:
                 return e
-        check(L.rrtmgpnn_lw_solver_1rescl(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu,
-                                          float_array(GAUSS_DS[nmu]), float_array(GAUSS_WTS[nmu]), _p(inc_flux),
-                                          _p(op.tau), _p(op.ssa), _p(op.g), _p(sources.lay_source),
-                                          _p(sources.lev_source), _p(emis_gpt), _p(sources.sfc_source), _p(up),
-                                          _p(dn)), "lw_solver_1rescl")
+        common = (ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu, float_array(GAUSS_DS[nmu]),
+                  float_array(GAUSS_WTS[nmu]), _p(inc_flux), _p(op.tau), _p(op.ssa), _p(op.g), _p(sources.lay_source),
+                  _p(sources.lev_source), _p(emis_gpt), _p(sources.sfc_source), _p(up), _p(dn))
+        if gpt:
+            check(L.rrtmgpnn_lw_solver_1rescl_gpt(*common, _p(gu), _p(gd)), "lw_solver_1rescl_gpt")
+        else:
+            check(L.rrtmgpnn_lw_solver_1rescl(*common), "lw_solver_1rescl")
     elif gpt or lw_Ds is not None:  # ty_fluxes_flexible g-point outputs / column-dependent secants (:329-341)
-        gu = fluxes.gpt_flux_up if getattr(fluxes, "gpt_flux_up", None) is not None else \
-            (torch.empty((ncol, nlay + 1, ngpt), device=emis.device) if gpt else None)
-        gd = fluxes.gpt_flux_dn if getattr(fluxes, "gpt_flux_dn", None) is not None else \
-            (torch.empty((ncol, nlay + 1, ngpt), device=emis.device) if gpt else None)
         ds = _f32dev(lw_Ds, emis.device) if lw_Ds is not None else None
         check(L.rrtmgpnn_lw_solver_noscat_gpt(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), nmu,
                                               float_array(GAUSS_DS[nmu]), float_array(GAUSS_WTS[nmu]), _p(ds),
@@ -843,8 +850,17 @@ def rte_sw(atmos, top_at_1, mu0, inc_flux, sfc_alb_dir_gpt, sfc_alb_dif_gpt, flu
         # is written (flux_up / flux_dn / flux_net are left as they are)
         if fluxes.flux_dn_dir is None:
             return "rte_sw: the no-scattering solution needs flux_dn_dir"
-        check(_lib.lib().rrtmgpnn_sw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
-                                                   _p(atmos.tau), _p(mu0), _p(fluxes.flux_dn_dir)), "sw_solver_noscat")
+        gdir = getattr(fluxes, "gpt_flux_dn_dir", None)
+        if gdir is not None:  # the spectral beam into the caller's gpt_flux_dn_dir (:155-163, 218-222)
+            if tuple(gdir.shape) != (ncol, nlay + 1, ngpt):
+                return "rte_sw: g-point flux arrays inconsistently sized"
+            check(_lib.lib().rrtmgpnn_sw_solver_noscat_gpt(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
+                                                           _p(atmos.tau), _p(mu0), _p(fluxes.flux_dn_dir), _p(gdir)),
+                  "sw_solver_noscat_gpt")
+        else:
+            check(_lib.lib().rrtmgpnn_sw_solver_noscat(ctx.h, ngpt, nlay, ncol, int(bool(top_at_1)), _p(inc_flux),
+                                                       _p(atmos.tau), _p(mu0), _p(fluxes.flux_dn_dir)),
+                  "sw_solver_noscat")
         return ""
     up = fluxes.flux_up if fluxes.flux_up is not None else torch.empty((ncol, nlay + 1), device=dev)
     dn = fluxes.flux_dn if fluxes.flux_dn is not None else torch.empty((ncol, nlay + 1), device=dev)

@@ -6,7 +6,9 @@
 !   twice: on the gas-optics tau (flux_up/dn_a) and on 0.5 * tau written on the host (flux_up/dn_b); then, on that
 !   tau, ty_fluxes_flexible g-point fluxes with rte_lw's lw_Ds (c: lw_Ds(icol, igpt) = 1 + 0.01 mod(7 icol + igpt, 100))
 !   and with three Gauss angles (d), and rte_sw on two-stream properties tau = 0.1 tau_a, ssa = 0.5, g = 0.3 over the
-!   same spectral discretisation with g-point fluxes (e: mu0 = 0.6, inc_flux = 1, albedos 0.2).
+!   same spectral discretisation with g-point fluxes (e: mu0 = 0.6, inc_flux = 1, albedos 0.2); rte_lw on those
+!   two-stream properties with g-point fluxes, rescaled (f) and use_2stream (g); rte_sw on the 1scl tau of (b) with
+!   gpt_flux_dn_dir (h: the spectral direct beam).
 program devstate
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -26,6 +28,9 @@ program devstate
   real(wp), allocatable, target :: up_c(:,:), dn_c(:,:), gup_c(:,:,:), gdn_c(:,:,:), up_d(:,:), dn_d(:,:)
   real(wp), allocatable, target :: gup_d(:,:,:), gdn_d(:,:,:), up_e(:,:), dn_e(:,:), dir_e(:,:)
   real(wp), allocatable, target :: gup_e(:,:,:), gdn_e(:,:,:), gdir_e(:,:,:)
+  real(wp), allocatable, target :: up_f(:,:), dn_f(:,:), gup_f(:,:,:), gdn_f(:,:,:)
+  real(wp), allocatable, target :: up_g(:,:), dn_g(:,:), gup_g(:,:,:), gdn_g(:,:,:), dir_h(:,:), gdir_h(:,:,:)
+  type(ty_fluxes_flexible) :: fl3, fl4
   real(wp), allocatable :: lw_ds(:,:), inc(:,:), alb(:,:), mu0(:)
   type(ty_optical_props_2str) :: op2
   type(ty_fluxes_flexible) :: fl2
@@ -125,7 +130,25 @@ program devstate
   fl2%gpt_flux_dn => gdn_e
   fl2%gpt_flux_dn_dir => gdir_e
   call chk(rte_sw(op2, top_at_1, mu0, inc, alb, alb, fl2))
-  u = rbin_write_begin(ofile, 23)
+  ! (f), (g) rte_lw on the two-stream properties with g-point fluxes
+  allocate(up_f(nlay + 1, ncol), dn_f(nlay + 1, ncol), gup_f(ngpt, nlay + 1, ncol), gdn_f(ngpt, nlay + 1, ncol))
+  fl3%flux_up => up_f
+  fl3%flux_dn => dn_f
+  fl3%gpt_flux_up => gup_f
+  fl3%gpt_flux_dn => gdn_f
+  call chk(rte_lw(op2, top_at_1, src, emis, fl3))
+  allocate(up_g(nlay + 1, ncol), dn_g(nlay + 1, ncol), gup_g(ngpt, nlay + 1, ncol), gdn_g(ngpt, nlay + 1, ncol))
+  fl3%flux_up => up_g
+  fl3%flux_dn => dn_g
+  fl3%gpt_flux_up => gup_g
+  fl3%gpt_flux_dn => gdn_g
+  call chk(rte_lw(op2, top_at_1, src, emis, fl3, use_2stream=.true.))
+  ! (h) rte_sw on the 1scl properties with the spectral direct beam
+  allocate(dir_h(nlay + 1, ncol), gdir_h(ngpt, nlay + 1, ncol))
+  fl4%flux_dn_dir => dir_h
+  fl4%gpt_flux_dn_dir => gdir_h
+  call chk(rte_sw(op, top_at_1, mu0, inc, alb, alb, fl4))
+  u = rbin_write_begin(ofile, 33)
   call rbin_write_real(u, "tau", tau0, shape(tau0))
   call rbin_write_real(u, "lay_source", lay0, shape(lay0))
   call rbin_write_real(u, "lev_source", lev0, shape(lev0))
@@ -149,6 +172,16 @@ program devstate
   call rbin_write_real(u, "gpt_dn_e", gdn_e, shape(gdn_e))
   call rbin_write_real(u, "gpt_dir_e", gdir_e, shape(gdir_e))
   call rbin_write_real(u, "lw_ds", lw_ds, shape(lw_ds))
+  call rbin_write_real(u, "flux_up_f", up_f, shape(up_f))
+  call rbin_write_real(u, "flux_dn_f", dn_f, shape(dn_f))
+  call rbin_write_real(u, "gpt_up_f", gup_f, shape(gup_f))
+  call rbin_write_real(u, "gpt_dn_f", gdn_f, shape(gdn_f))
+  call rbin_write_real(u, "flux_up_g", up_g, shape(up_g))
+  call rbin_write_real(u, "flux_dn_g", dn_g, shape(dn_g))
+  call rbin_write_real(u, "gpt_up_g", gup_g, shape(gup_g))
+  call rbin_write_real(u, "gpt_dn_g", gdn_g, shape(gdn_g))
+  call rbin_write_real(u, "flux_dir_h", dir_h, shape(dir_h))
+  call rbin_write_real(u, "gpt_dir_h", gdir_h, shape(gdir_h))
   call rbin_write_end(u)
 contains
   subroutine chk(msg)

@@ -201,3 +201,16 @@ def test_fortran_device_state_update_host_and_device(tmp_path, orc, rfmip):
                          np.full((ncol, ngpt), 0.2, np.float32), prob["top_at_1"], gpt=True)
     for k, w in zip(("flux_up_e", "flux_dn_e", "flux_dir_e", "gpt_up_e", "gpt_dn_e", "gpt_dir_e"), want):
         np.testing.assert_array_equal(got[k], w, err_msg=k)
+    # (f) rescaled and (g) use_2stream rte_lw on those two-stream properties, with g-point fluxes
+    w2, g2 = np.full_like(t2, 0.5), np.full_like(t2, 0.3)
+    want_f = orc.lw_solver(t2, go["lay_source"], go["lev_source"], emis, go["sfc_source"], prob["top_at_1"], ssa=w2,
+                           g=g2, gpt=True)
+    want_g = orc.lw_solver_2stream(t2, w2, g2, go["lev_source"], emis, go["sfc_source"], prob["top_at_1"], gpt=True)
+    for tag, want in (("f", want_f), ("g", want_g)):
+        for k, w in zip(("flux_up_", "flux_dn_", "gpt_up_", "gpt_dn_"), want):
+            np.testing.assert_array_equal(got[k + tag], w, err_msg=k + tag)
+    # (h) rte_sw on the 1scl tau of (b): broadband and spectral direct beam
+    dr, gdr = orc.sw_solver_noscat(tau_b, np.full(ncol, 0.6, np.float32), np.ones((ncol, ngpt), np.float32),
+                                   prob["top_at_1"], gpt=True)
+    np.testing.assert_array_equal(got["flux_dir_h"], dr)
+    np.testing.assert_array_equal(got["gpt_dir_h"], gdr)

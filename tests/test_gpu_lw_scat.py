@@ -70,6 +70,49 @@ def test_lw_2stream_bitwise_vs_oracle(dev, orc, prob, top_at_1, with_inc):
         np.testing.assert_array_equal(x, y, err_msg=k)
 
 
+@pytest.mark.parametrize("top_at_1", [True, False])
+@pytest.mark.parametrize("mode", ["rescl1", "rescl2", "rescl4", "2stream", "2stream_inc"])
+def test_lw_scattering_gpt_bitwise_vs_oracle(dev, orc, prob, top_at_1, mode):
+    """FluxesFlexible on two-stream properties (rrtmgpnn_lw_solver_1rescl_gpt / _2stream_gpt through rte_lw): the
+    g-point outputs and the broadband fluxes equal the oracle's (pinned to the reference's rte_lw by
+    tests/test_lw_scattering_oracle.py), bit for bit."""
+    from rrtmgpnn import api
+    p = prob if top_at_1 else _flip(prob)
+    kd = p["kd"]
+    ncol, nlay, ngpt = p["tau"].shape
+    two = mode.startswith("2stream")
+    nmus = None if two else int(mode[-1])
+    inc = np.random.default_rng(6).uniform(0, 2, (ncol, ngpt)).astype(np.float32) if mode.endswith("inc") else None
+    op = api.OpticalProps2str()
+    assert op.init(kd["band_lims_wvn"], kd["band_lims_gpt"]) == ""
+    assert op.alloc_2str(ncol, nlay, device=dev) == ""
+    op.tau.copy_(T(p["tau"], dev)), op.ssa.copy_(T(p["ssa"], dev)), op.g.copy_(T(p["g"], dev))
+    src = api.SourceFuncLW()
+    assert src.alloc(ncol, nlay, op, device=dev) == ""
+    src.lay_source.copy_(T(p["lay"], dev)), src.lev_source.copy_(T(p["lev"], dev))
+    src.sfc_source.copy_(T(p["sfc"], dev))
+    nan = lambda *s: torch.full(s, float("nan"), device=dev)  # noqa: E731
+    fl = api.FluxesFlexible(flux_up=nan(ncol, nlay + 1), flux_dn=nan(ncol, nlay + 1),
+                            gpt_flux_up=nan(ncol, nlay + 1, ngpt), gpt_flux_dn=nan(ncol, nlay + 1, ngpt))
+    e = api.rte_lw(op, top_at_1, src, T(p["emis_band"], dev), fl, inc_flux=None if inc is None else T(inc, dev),
+                   n_gauss_angles=nmus, use_2stream=two)
+    assert e == "", e
+    torch.cuda.synchronize()
+    if two:
+        want = orc.lw_solver_2stream(p["tau"], p["ssa"], p["g"], p["lev"], p["emis_gpt"], p["sfc"], top_at_1, inc,
+                                     gpt=True)
+    else:
+        want = orc.lw_solver(p["tau"], p["lay"], p["lev"], p["emis_gpt"], p["sfc"], top_at_1, nmus, ssa=p["ssa"],
+                             g=p["g"], gpt=True)
+    got = (fl.flux_up, fl.flux_dn, fl.gpt_flux_up, fl.gpt_flux_dn)
+    for x, y, k in zip(got, want, ("up", "dn", "gpt_up", "gpt_dn")):
+        np.testing.assert_array_equal(x.cpu().numpy(), y, err_msg=k)
+    # the broadband fluxes are those of the plain entries
+    plain = _gpu_lw(p, dev, top_at_1, nmus, use_2stream=two, inc=inc)
+    np.testing.assert_array_equal(plain[0], want[0])
+    np.testing.assert_array_equal(plain[1], want[1])
+
+
 def test_lw_scattering_argument_checks(dev, prob):
     from rrtmgpnn import api
     kd = prob["kd"]

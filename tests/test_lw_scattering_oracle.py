@@ -70,6 +70,30 @@ def test_lw_2stream_bitwise_vs_reference(orc, rfmip, top_at_1):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("top_at_1", [True, False])
+@pytest.mark.parametrize("mode", ["rescl1", "rescl3", "2stream"])
+def test_lw_scattering_gpt_bitwise_vs_reference(orc, rfmip, top_at_1, mode):
+    """ty_fluxes_flexible g-point outputs on two-stream properties (rte/mo_rte_lw.F90:357-387): the rescaled
+    solution's radiances with one angle (quirk B-5) and angle-summed fluxes with several, lw_solver_2stream's adding
+    fluxes -- the restatement == the reference's rte_lw, bit for bit."""
+    ref = _ref()
+    p = lw_2str_problem(orc, rfmip, seed=3)
+    if not top_at_1:
+        p = _flip(p)
+    if mode == "2stream":
+        a = orc.lw_solver_2stream(p["tau"], p["ssa"], p["g"], p["lev"], p["emis_gpt"], p["sfc"], top_at_1, gpt=True)
+        nmus = 1
+    else:
+        nmus = 1 if mode == "rescl1" else 3
+        a = orc.lw_solver(p["tau"], p["lay"], p["lev"], p["emis_gpt"], p["sfc"], top_at_1, nmus, ssa=p["ssa"],
+                          g=p["g"], gpt=True)
+    b = ref.rte_lw_2str_gpt(p["kd"], p["tau"], p["ssa"], p["g"], p["lay"], p["lev"], p["sfc"], p["jac"],
+                            p["emis_band"], top_at_1, nmus, use_2stream=mode == "2stream")
+    for x, y, what in zip(a, b, ("up", "dn", "gpt_up", "gpt_dn")):
+        np.testing.assert_array_equal(x, y, err_msg=what)
+    assert np.abs(a[2]).max() > 0
+
+
 def test_lw_scattering_physics(orc, rfmip):
     """The rescaled solution equals the no-scattering solver where ssa = 0, and the two scattering solvers agree
     on the outgoing LW to ~10 W/m2 (different approximations of the same scattering)."""
