@@ -96,15 +96,15 @@ __device__ __forceinline__ float sqrt_rn_normal(float x)
 }
 
 // Correctly rounded 1/b for b in [2^-60, 2^60] (the solvers' denominators: k(1+e^-2k tau)+... and
-// 1 - R_dif*albedo): the compiler's IEEE division sequence minus v_div_scale / v_div_fixup, which
-// leave the operands and the result untouched in that range, so the bits are those of 1.0f / b.
+// 1 - R_dif*albedo): v_rcp_f32, one Newton step and one residual correction -- the compiler's IEEE division
+// sequence minus v_div_scale / v_div_fixup (which leave the operands and the result untouched in that range) and
+// minus its second correction.  Equal to 1.0f / b on every float of [2^-60, 2^60], checked on the GPU
+// (tools/exhaustive_ops.hip; the sequence with both corrections too).
 __device__ __forceinline__ float rcp_rn_normal(float b)
 {
   float r = __builtin_amdgcn_rcpf(b);
   r = fmaf(fmaf(-b, r, 1.0f), r, r);
-  float q = r;                       // 1 * r
-  q = fmaf(fmaf(-b, q, 1.0f), r, q);
-  return fmaf(fmaf(-b, q, 1.0f), r, q);
+  return fmaf(fmaf(-b, r, 1.0f), r, r);
 }
 
 // Correctly rounded a / b for operands and quotient in the normal range (|a| >= 2^-100, |b| and |a/b| in
@@ -118,6 +118,17 @@ __device__ __forceinline__ float div_rn_normal(float a, float b)
   float q = a * r;
   q = fmaf(fmaf(-b, q, a), r, q);
   return fmaf(fmaf(-b, q, a), r, q);
+}
+
+// softsign's quotient x / (|x| + 1) (b = |x| + 1): v_rcp_f32 and two residual corrections, without the Newton step
+// on the reciprocal, the residual taken as b*q - x so that a -0 quotient keeps its sign.  Equal to x / b on every
+// float |x| < 2^126, -0 included, checked on the GPU (tools/exhaustive_ops.hip; div_rn_normal returned +0 for -0).
+__device__ __forceinline__ float div_softsign(float x, float b)
+{
+  const float r = __builtin_amdgcn_rcpf(b);
+  float q = x * r;
+  q = fmaf(-fmaf(b, q, -x), r, q);
+  return fmaf(-fmaf(b, q, -x), r, q);
 }
 
 // ref_expf_nb for x <= 0 (the solvers' exp(-tau*D), exp(-tau/mu0), exp(-k*tau) with tau >= 0): only glibc's

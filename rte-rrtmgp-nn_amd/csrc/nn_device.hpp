@@ -34,13 +34,12 @@ __device__ __forceinline__ float pow8(float t)
 #define RRTMGPNN_MLP_FASTDIV 1
 #endif
 
-// softsign (neural/mod_activation.F90:107-128).  FASTDIV: the division sequence minus v_div_scale/v_div_fixup
-// (libm_ref.hpp div_rn_normal), exact for |x| < 2^126 -- below 2^-24, |x| + 1 rounds to 1 and the quotient is x
-// itself; above, both operands and the quotient are normal
+// softsign (neural/mod_activation.F90:107-128).  FASTDIV: libm_ref.hpp div_softsign (reciprocal and two residual
+// corrections), equal to the IEEE quotient for every |x| < 2^126, checked exhaustively on the GPU
 __device__ __forceinline__ float softsign(float x)
 {
 #if RRTMGPNN_MLP_FASTDIV
-  return div_rn_normal(x, fabsf(x) + 1.0f);
+  return div_softsign(x, fabsf(x) + 1.0f);
 #else
   return x / (fabsf(x) + 1.0f);
 #endif

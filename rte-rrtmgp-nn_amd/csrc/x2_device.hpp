@@ -45,9 +45,7 @@ __device__ __forceinline__ f2 rcp2(f2 b)
   f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
   const f2 one = splat(1.0f);
   r = vfma(vfma(-b, r, one), r, r);
-  f2 q = r;
-  q = vfma(vfma(-b, q, one), r, q);
-  return vfma(vfma(-b, q, one), r, q);
+  return vfma(vfma(-b, r, one), r, r);
 }
 
 // solver_div (rte_device.hpp) with the Newton fmas paired
