@@ -47,6 +47,20 @@ __device__ __forceinline__ float sqrt_cur(float x)
   float r = (em <= 0.0f) ? sm : s;
   return (ep > 0.0f) ? sp : r;
 }
+// the hardware estimate alone, and with only one of the two one-ulp corrections
+__device__ __forceinline__ float sqrt_raw(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float sqrt_up(float x)
+{
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  return (fmaf(-sp, s, x) > 0.0f) ? sp : s;
+}
+__device__ __forceinline__ float sqrt_dn(float x)
+{
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  return (fmaf(-sm, s, x) <= 0.0f) ? sm : s;
+}
 __device__ __forceinline__ float sqrt_d(float x) { return (float)__builtin_amdgcn_sqrt((double)x); }
 __device__ __forceinline__ float div_cur(float a, float b)
 {
@@ -95,7 +109,7 @@ __global__ void check(int op, uint32_t lo, uint64_t n, uint32_t per, unsigned lo
     } else if (op == 1) {
       ref = sqrtf(x);
       ref2 = (float)sqrt((double)x);
-      v[0] = sqrt_cur(x); v[1] = sqrt_d(x); nv = 2;
+      v[0] = sqrt_cur(x); v[1] = sqrt_d(x); v[2] = sqrt_raw(x); v[3] = sqrt_up(x); v[4] = sqrt_dn(x); nv = 5;
     } else {
       if (!(fabsf(x) < 3.0e38f)) continue;  // finite x; |x| + 1 below inf
       const float b = fabsf(x) + 1.0f;
@@ -153,8 +167,9 @@ int main()
   const char *rv[kVar] = {"current(newton+2corr)", "newton+1corr", "2corr", nullptr, nullptr, nullptr, nullptr,
                           "ref-vs-double"};
   run(0, "rcp", 0x21800000u /* 2^-60 */, 0x5d800000u /* 2^60 */, rv);
-  const char *sv[kVar] = {"current", "f64-sqrt", nullptr, nullptr, nullptr, nullptr, nullptr, "ref-vs-double"};
+  const char *sv[kVar] = {"current", "f64-sqrt", "raw", "up-only", "down-only", nullptr, nullptr, "ref-vs-double"};
   run(1, "sqrt", 0x35800000u /* 2^-20 */, 0x49800000u /* 2^20 */, sv);
+  run(1, "sqrt<", 0x38d1b717u /* 1e-4 */, 0x40800000u /* 4 */, sv);
   const char *dv[kVar] = {"current(newton+2corr)", "2corr", "2corr-negres", nullptr, nullptr, nullptr, nullptr,
                           "ref-vs-double"};
   run(2, "soft+", 0x00000000u, 0x7f7fffffu, dv);
