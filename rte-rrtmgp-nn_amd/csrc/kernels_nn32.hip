@@ -262,6 +262,10 @@ constexpr int kMlp32Threads = RRTMGPNN_MLP32_THREADS;
 #define RRTMGPNN_MLP32_SW_WPE 1
 #endif
 constexpr int kSwNT = RRTMGPNN_MLP32_SW_THREADS, kSwWPE = RRTMGPNN_MLP32_SW_WPE;
+// grid sized by the occupancy the runtime reports (1) or by the LDS footprint alone (0)
+#ifndef RRTMGPNN_MLP32_OCC
+#define RRTMGPNN_MLP32_OCC 1
+#endif
 
 // A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  The host guarantees that the
 // g-tiles are full: ngpt = 32 NGT (LW pair) or 2 ngpt = 32 NGT (LW both).  Dynamic LDS: the weight images, then 32
@@ -472,8 +476,21 @@ static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
     if (int rc = raise_lds_limit((const void *)kern)) return rc;
   const long long ntiles = ((long long)a.nbatch + 31) / 32;
   const int wpb = NT / 64;
-  const int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / NT);
+  int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / NT);
   const long long want = (ntiles + wpb - 1) / wpb;
+#if RRTMGPNN_MLP32_OCC
+  // Blocks a CU actually holds (registers included).  When the tiles fill less than two rounds of resident blocks, a
+  // grid of one round strides them and loads each weight image once per CU, instead of a partial second round that
+  // loads it again for little work (the SW pair at C3: 184 VGPRs, one 8-wave block per CU, 422 blocks: step -1 %).
+  // With many rounds the blocks' turnover lets the overlapped LW chain share the CUs (C4: one round was 1 % slower).
+  static int occ = 0;
+  if (!occ) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)kern, NT, lds) == hipSuccess && nb > 0) occ = nb;
+    else occ = -1;
+  }
+  if (occ > 0 && want <= 2LL * occ * ctx->num_cus) per_cu = std::min(per_cu, occ);
+#endif
   const long long grid = std::max<long long>(1, std::min<long long>(want, (long long)ctx->num_cus * per_cu));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp32_kernel");
