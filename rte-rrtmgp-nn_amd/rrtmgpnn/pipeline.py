@@ -250,6 +250,30 @@ class ClearSkyStep:
         # and joined at the end of the step -- the VALU-bound SW solver shares the CUs with the MFMA-bound LW
         # network and the LW solver instead of running after them
         self.overlap = overlap
+        # The LW chain may start once a call of the SW chain has finished (issued first, the SW network then has the
+        # chip to itself).  Default: after the SW network when the SW solver's grid fits in one round of resident
+        # waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane, against 16 per CU): the solver is then
+        # latency-bound and its start is the step's critical path (C3: step -3 %); with more columns it is VALU-bound
+        # and the chains are better started together (C4: gating was 2.3 % slower).  RRTMGPNN_LW_AFTER=<SW-chain call>
+        # or "none" overrides.
+        names = [n for n, _, _ in self.calls]
+        gate = ""
+        if overlap and self.fused and "predict_nn_sw" in names:
+            cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+            if self.ncol * self.ng_sw <= 2048 * cus:
+                gate = "predict_nn_sw"
+        env = os.environ.get("RRTMGPNN_LW_AFTER", "")
+        self.lw_after = (env if env != "none" else "") if env else gate
+        if not overlap:
+            self.lw_after = ""
+        if self.lw_after:
+            names = [n for n, _, _ in self.calls]
+            if self.lw_after not in names or self.lw_after not in SW_CHAIN or "get_col_dry" in names:
+                raise ValueError("RRTMGPNN_LW_AFTER: %r is not a call of this fused step's SW chain" % self.lw_after)
+            cut = names.index(self.lw_after)
+            head = [c for i, c in enumerate(self.calls) if c[0] in SW_CHAIN and i <= cut]
+            self.calls = head + [c for c in self.calls if c not in head]
+            self._gate = torch.cuda.Event()
         self.ctx2 = None
         if overlap:
             self.ctx2 = Context(self.dev.index, self._sw_stream())
@@ -303,6 +327,9 @@ class ClearSkyStep:
             if self.overlap and name == fork_after:
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
+            if self.overlap and name == self.lw_after:
+                self._gate.record(self.ctx2.stream)
+                self.ctx.stream.wait_event(self._gate)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)

@@ -28,4 +28,4 @@ def test_shortened_division_sequences_are_exact_on_their_domains():
     shipped = [("rcp", "newton+1corr"), ("sqrt", "current"), ("soft+<", "2corr-negres"), ("soft-<", "2corr-negres")]
     for key in shipped + [k for k in res if k[1] == "ref-vs-double"]:
         n, bad = res[key]
-        assert n > 300_000_000 and bad == 0, (key, n, bad)
+        assert n > 100_000_000 and bad == 0, (key, n, bad)
