@@ -21,6 +21,8 @@
 // ceil(nlay / K); index c holds level c*K counted from the top, index nck the surface.
 #include "x2_device.hpp"
 
+#include <algorithm>
+
 namespace rrtmgpnn {
 using namespace x2;
 
@@ -115,7 +117,6 @@ __device__ __forceinline__ void ck_inc(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, f2 
 #endif
 constexpr bool kCkKeepD = RRTMGPNN_SWCK_KEEPD != 0;
 constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
-static_assert(kCkRing % kCkK == 0, "the flux ring must hold whole chunks");
 
 // Waves per SIMD of the clear-sky NN instance (g = NULL, no increment), which needs fewer registers: at 4 (128 VGPRs,
 // 2 spilled) the C3 grid (900 blocks of 4 waves) is resident at once instead of 768 + a second round of 132; SW solver
@@ -126,8 +127,18 @@ static_assert(kCkRing % kCkK == 0, "the flux ring must hold whole chunks");
 
 // kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
 // broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
-template <bool kHasG, bool kInc, int K, bool kGpt = false>
-__global__ void __launch_bounds__(512, (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES)
+// Small grids (the clear-sky instance when the grid fits in one round of resident waves, e.g. C3): K = 4 layers per
+// chunk at 2 waves per SIMD (more independent layers per wave where there are too few waves to hide the exps'
+// latency), ring of 8 levels.  Whole-step A/B at C3 (one box, alternating): +1.3 %, SW solver -2.4 %; a ring of 4 was
+// 3 % slower, K = 2 at 4 waves +0.5 %.  With many columns (C4, C5) K = 3 at 3-4 waves stays (K = 4 was 13 % slower).
+#ifndef RRTMGPNN_SWCK_SMALL
+#define RRTMGPNN_SWCK_SMALL 1
+#endif
+constexpr int kCkKSmall = 4, kCkRingSmall = 8, kCkWavesSmall = 2;
+
+template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
+          int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES>
+__global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
                          const float *__restrict__ ssa, const float *__restrict__ gg, const float *__restrict__ mu0p,
@@ -137,7 +148,7 @@ __global__ void __launch_bounds__(512, (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWC
                          float *__restrict__ flux_dn, float *__restrict__ flux_dir, float *__restrict__ gpt_up,
                          float *__restrict__ gpt_dn, float *__restrict__ gpt_dir)
 {
-  constexpr int R = kCkRing;
+  static_assert(R % K == 0, "the flux ring must hold whole chunks");
   constexpr bool kG0 = !kHasG && !kInc;  // g is the literal 0 (the NN path)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // `ncb` columns per block: lane t works on column c = t / (ngpt/2), g-points g, g + 1
@@ -361,10 +372,11 @@ __global__ void __launch_bounds__(512, (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWC
   }
 }
 
-// workspace floats of the checkpointed kernel
+// workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either instance)
 size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol)
 {
-  const size_t nck = (size_t)(nlay + kCkK - 1) / kCkK;
+  const int k = std::min(kCkK, kCkKSmall);
+  const size_t nck = (size_t)(nlay + k - 1) / k;
   return (size_t)ngpt * ncol * (nck + 2 * (nck + 1));
 }
 
@@ -380,13 +392,15 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
 #endif
   const int ncb = RRTMGPNN_SWCK_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SWCK_NCB : 1;
   const int threads = (ncb * (ngpt / 2) + 63) / 64 * 64;
-  const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * kCkRing * ngpt);
-  if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: LDS ring exceeds 160 KiB");
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
   const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
   const auto &ex = ctx->extras;
-  auto go = [&](auto kern, const float *tb, const float *sb, const float *gb) -> int {
+  size_t lds = 0;
+  auto lds_for = [&](int ring) { return sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * ring * ngpt); };
+  auto go = [&](auto kern, const float *tb, const float *sb, const float *gb, int ring = kCkRing) -> int {
+    lds = lds_for(ring);
+    if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: LDS ring exceeds 160 KiB");
     if (lds > 64 * 1024)
       if (int rc = raise_lds_limit((const void *)kern)) return rc;
     hipLaunchKernelGGL(kern, grid, block, lds, ctx->stream, ngpt, nlay, ncol, top_at_1, ncb, inc_flux, inc_flux_dif,
@@ -405,6 +419,12 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
   if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
+  // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
+  // waves per CU)
+  const long long lanes = (long long)ncol * (ngpt / 2);
+  if (RRTMGPNN_SWCK_SMALL && lanes <= 64LL * 16 * ctx->num_cus)
+    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall>, nullptr, nullptr,
+              nullptr, kCkRingSmall);
   return go(sw_2stream_ck_kernel<false, false, kCkK>, nullptr, nullptr, nullptr);
 }
 
