@@ -49,6 +49,7 @@ def parse():
                          "without a value the config's global size: C5 1e6 columns); default: N x the config's block")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
+    ap.add_argument("--sw-after", default="", help="start the SW chain after this LW-chain call (e.g. predict_nn_lw)")
     ap.add_argument("--lw-after", default="", help="start the LW chain after this SW-chain call (e.g. predict_nn_sw; none: chains start together; default: the library pipeline's choice)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
@@ -226,6 +227,8 @@ def main():
     prob, clouds = problem(*chunks[0])
     if args.lw_after:
         os.environ["RRTMGPNN_LW_AFTER"] = args.lw_after
+    if args.sw_after:
+        os.environ["RRTMGPNN_SW_AFTER"] = args.sw_after
     step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap,
                         sw=args.config not in ("c1", "c2"))
     ncol, nlay = step.ncol, step.nlay
@@ -440,7 +443,8 @@ def main():
                        "parallelism": "column-sharded (shard.column_range), 1 process per GPU",
                        "launch": ("hipGraph replay" if use_graph else "eager") +
                                  (", LW and SW chains on two streams" if step.overlap else "") +
-                                 (", the LW chain after %s" % step.lw_after if step.lw_after else ""),
+                                 (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
+                                 (", the SW chain after %s" % step.sw_after if step.sw_after else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
                                    "fused Planck-in-LW-solver, g=0 elided" +
                                    (", cloud increments fused into both solvers" if step.allsky else ""))},

@@ -266,6 +266,14 @@ class ClearSkyStep:
         self.lw_after = (env if env != "none" else "") if env else gate
         if not overlap:
             self.lw_after = ""
+        # RRTMGPNN_SW_AFTER=<LW-chain call>: the SW chain starts once that call of the LW chain has finished (the LW
+        # calls are issued first in the fused order); exclusive with the LW gate
+        self.sw_after = os.environ.get("RRTMGPNN_SW_AFTER", "") if overlap else ""
+        if self.sw_after:
+            if self.sw_after not in names or self.sw_after in SW_CHAIN or "get_col_dry" in names:
+                raise ValueError("RRTMGPNN_SW_AFTER: %r is not a call of this fused step's LW chain" % self.sw_after)
+            self.lw_after = ""
+            self._gate_sw = torch.cuda.Event()
         if self.lw_after:
             names = [n for n, _, _ in self.calls]
             if self.lw_after not in names or self.lw_after not in SW_CHAIN or "get_col_dry" in names:
@@ -330,6 +338,9 @@ class ClearSkyStep:
             if self.overlap and name == self.lw_after:
                 self._gate.record(self.ctx2.stream)
                 self.ctx.stream.wait_event(self._gate)
+            if self.overlap and name == self.sw_after:
+                self._gate_sw.record(self.ctx.stream)
+                self.ctx2.stream.wait_event(self._gate_sw)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)
