@@ -266,13 +266,12 @@ class ClearSkyStep:
         self.lw_after = (env if env != "none" else "") if env else gate
         if not overlap:
             self.lw_after = ""
-        # RRTMGPNN_SW_AFTER=<LW-chain call>: the SW chain starts once that call of the LW chain has finished (the LW
-        # calls are issued first in the fused order); exclusive with the LW gate
+        # RRTMGPNN_SW_AFTER=<LW-chain call>: the SW chain's calls issued after that LW call (all of them, or with the
+        # LW gate above only those after the SW network) wait for it to finish
         self.sw_after = os.environ.get("RRTMGPNN_SW_AFTER", "") if overlap else ""
         if self.sw_after:
             if self.sw_after not in names or self.sw_after in SW_CHAIN or "get_col_dry" in names:
                 raise ValueError("RRTMGPNN_SW_AFTER: %r is not a call of this fused step's LW chain" % self.sw_after)
-            self.lw_after = ""
             self._gate_sw = torch.cuda.Event()
         if self.lw_after:
             names = [n for n, _, _ in self.calls]
