@@ -134,7 +134,17 @@ constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
 #ifndef RRTMGPNN_SWCK_SMALL
 #define RRTMGPNN_SWCK_SMALL 1
 #endif
-constexpr int kCkKSmall = 4, kCkRingSmall = 8, kCkWavesSmall = 2;
+#ifndef RRTMGPNN_SWCK_K_SMALL
+#define RRTMGPNN_SWCK_K_SMALL 4
+#endif
+#ifndef RRTMGPNN_SWCK_RING_SMALL
+#define RRTMGPNN_SWCK_RING_SMALL 8
+#endif
+#ifndef RRTMGPNN_SWCK_WAVES_SMALL
+#define RRTMGPNN_SWCK_WAVES_SMALL 2
+#endif
+constexpr int kCkKSmall = RRTMGPNN_SWCK_K_SMALL, kCkRingSmall = RRTMGPNN_SWCK_RING_SMALL,
+              kCkWavesSmall = RRTMGPNN_SWCK_WAVES_SMALL;
 
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES>
