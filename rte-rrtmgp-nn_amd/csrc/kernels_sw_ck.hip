@@ -145,9 +145,15 @@ constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
 #endif
 constexpr int kCkKSmall = RRTMGPNN_SWCK_K_SMALL, kCkRingSmall = RRTMGPNN_SWCK_RING_SMALL,
               kCkWavesSmall = RRTMGPNN_SWCK_WAVES_SMALL;
+// the small-grid instance keeps pass 1's beam transmittances exp(-tau/mu0) in a workspace plane and passes 2 and 3 read
+// them (one more plane written and two read) instead of evaluating the exp again
+#ifndef RRTMGPNN_SWCK_TN_SMALL
+#define RRTMGPNN_SWCK_TN_SMALL 1
+#endif
+constexpr bool kCkTnSmall = RRTMGPNN_SWCK_TN_SMALL != 0;
 
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
-          int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES>
+          int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES, bool kTn = false>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -185,6 +191,8 @@ __global__ void __launch_bounds__(512, WAVES)
   const ColArr2 CB(ws, (size_t)ngpt * nck * icol0, (uint32_t)nc * row * nck);
   const ColArr2 CA(ws + pB, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
   const ColArr2 CS(ws + pB + pA, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
+  // kTn: the beam transmittances (ngpt, nlay, ncol), addressed as tau
+  const ColArr2 CT(kTn ? ws + pB + 2 * pA : ws, kTn ? cl : 0, kTn ? bL : 0u);
   const uint32_t vBs = on ? vB : kBufOOB, vAs = on ? vA : kBufOOB;
   // band-resolved increments: one band offset per g-point of the pair
   const size_t cb = (size_t)bands.nbnd * nlay * icol0;
@@ -206,7 +214,7 @@ __global__ void __launch_bounds__(512, WAVES)
 
   // one chunk's optical properties (the band increment is formed as they are used, as inc_2str2 does)
   struct Chunk {
-    f2 t[K], w[K], g[K], qt[K], qw[K], qg[K];
+    f2 t[K], w[K], g[K], qt[K], qw[K], qg[K], tn[K];
   };
   auto load_chunk = [&](Chunk &ch, int ck, bool with_ssa) {
 #pragma unroll
@@ -214,6 +222,7 @@ __global__ void __launch_bounds__(512, WAVES)
       const int l = lay(ck * K + p);
       const uint32_t s = row * (uint32_t)l;
       ch.t[p] = Ttau.ld(vL, s);
+      ch.tn[p] = kTn && with_ssa ? CT.ld(vL, s) : splat(0.0f);
       ch.w[p] = with_ssa ? Tssa.ld(vL, s) : splat(0.0f);
       ch.g[p] = kHasG && with_ssa ? Tg.ld(vL, s) : splat(0.0f);
       if constexpr (kInc) {
@@ -245,6 +254,10 @@ __global__ void __launch_bounds__(512, WAVES)
       f2 Tn[K];
 #pragma unroll
       for (int p = 0; p < K; p++) Tn[p] = exp2v_beam(-(kInc ? cur.t[p] + cur.qt[p] : cur.t[p]) * mu0_inv, etab);
+      if constexpr (kTn) {
+#pragma unroll
+        for (int p = 0; p < K; p++) CT.st(Tn[p], (on && p < n) ? vL : kBufOOB, row * (uint32_t)lay(ck * K + p));
+      }
 #pragma unroll
       for (int p = 0; p < K; p++)
         if (p < n) Fd = Tn[p] * Fd;
@@ -268,7 +281,7 @@ __global__ void __launch_bounds__(512, WAVES)
 #pragma unroll
       for (int p = 0; p < K; p++) {
         props(cur, p, t[p], w[p], g0[p]);
-        Tn[p] = exp2v_beam(-t[p] * mu0_inv, etab);  // pass 1's transmittance, same bits
+        Tn[p] = kTn ? cur.tn[p] : exp2v_beam(-t[p] * mu0_inv, etab);  // pass 1's transmittance, same bits
         Fin[p] = Fb;                           // the beam at the layer's top
         Fb = Tn[p] * Fb;
       }
@@ -329,7 +342,7 @@ __global__ void __launch_bounds__(512, WAVES)
       for (int p = 0; p < K; p++) {
         f2 t, w, g0;
         props(cur, p, t, w, g0);
-        const f2 Tn = exp2v_beam(-t * mu0_inv, etab);
+        const f2 Tn = kTn ? cur.tn[p] : exp2v_beam(-t * mu0_inv, etab);
         const Coef2 cf = ck_two_stream<kG0>(t, w, g0, mu0, Tn, Fd3, etab);
         Rd[p] = cf.Rdif;
         Td[p] = cf.Tdif;
@@ -382,12 +395,20 @@ __global__ void __launch_bounds__(512, WAVES)
   }
 }
 
-// workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either instance)
-size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol)
+bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bool inc, bool gpt)
 {
+  // 2 g-points per lane; one round of 16 waves of 64 lanes per CU
+  return RRTMGPNN_SWCK_SMALL && !has_g && !inc && !gpt && (long long)ncol * (ngpt / 2) <= 64LL * 16 * ctx->num_cus;
+}
+
+// workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either
+// instance; small: plus the small-grid instance's plane of beam transmittances)
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small)
+{
+  const size_t tn = small && kCkTnSmall ? (size_t)ngpt * nlay * ncol : 0;
   const int k = std::min(kCkK, kCkKSmall);
   const size_t nck = (size_t)(nlay + k - 1) / k;
-  return (size_t)ngpt * ncol * (nck + 2 * (nck + 1));
+  return (size_t)ngpt * ncol * (nck + 2 * (nck + 1)) + tn;
 }
 
 // ngpt even and <= 256
@@ -431,10 +452,9 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
-  const long long lanes = (long long)ncol * (ngpt / 2);
-  if (RRTMGPNN_SWCK_SMALL && lanes <= 64LL * 16 * ctx->num_cus)
-    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall>, nullptr, nullptr,
-              nullptr, kCkRingSmall);
+  if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
+    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall>, nullptr,
+              nullptr, nullptr, kCkRingSmall);
   return go(sw_2stream_ck_kernel<false, false, kCkK>, nullptr, nullptr, nullptr);
 }
 
