@@ -756,7 +756,7 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   const bool x2 = !ck && kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc && kSwIncPark ? 3 : 0);
-  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt))
+  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), inc)
                         : 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
   int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;

@@ -151,6 +151,11 @@ constexpr int kCkKSmall = RRTMGPNN_SWCK_K_SMALL, kCkRingSmall = RRTMGPNN_SWCK_RI
 #define RRTMGPNN_SWCK_TN_SMALL 1
 #endif
 constexpr bool kCkTnSmall = RRTMGPNN_SWCK_TN_SMALL != 0;
+// the same for the all-sky instances (fused cloud increment), whatever the grid
+#ifndef RRTMGPNN_SWCK_TN_INC
+#define RRTMGPNN_SWCK_TN_INC 0
+#endif
+constexpr bool kCkTnInc = RRTMGPNN_SWCK_TN_INC != 0;
 
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES, bool kTn = false>
@@ -403,9 +408,9 @@ bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bo
 
 // workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either
 // instance; small: plus the small-grid instance's plane of beam transmittances)
-size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small)
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc)
 {
-  const size_t tn = small && kCkTnSmall ? (size_t)ngpt * nlay * ncol : 0;
+  const size_t tn = (small && kCkTnSmall) || (inc && kCkTnInc) ? (size_t)ngpt * nlay * ncol : 0;
   const int k = std::min(kCkK, kCkKSmall);
   const size_t nck = (size_t)(nlay + k - 1) / k;
   return (size_t)ngpt * ncol * (nck + 2 * (nck + 1)) + tn;
@@ -447,8 +452,9 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     if (g) return go(sw_2stream_ck_kernel<true, false, kCkK, true>, nullptr, nullptr, nullptr);
     return go(sw_2stream_ck_kernel<false, false, kCkK, true>, nullptr, nullptr, nullptr);
   }
-  if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
-  if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
+  constexpr int kW = RRTMGPNN_SWCK_WAVES;
+  if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, kW, kCkTnInc>, tau_bnd, ssa_bnd, g_bnd);
+  if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, kW, kCkTnInc>, tau_bnd, ssa_bnd, g_bnd);
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
