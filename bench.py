@@ -176,7 +176,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from rrtmgpnn import data, shard
-    from rrtmgpnn.pipeline import ClearSkyStep
+    from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
 
     # ---- the global problem and this rank's part of it (shard.column_range) ----
     metric = METRIC
@@ -190,7 +190,6 @@ def main():
         global_cols = block * world
         scaling = "weak"
     lo, hi = shard.column_range(global_cols, rank, world)
-    chunks = [(c, min(c + block, hi)) for c in range(lo, hi, block)] or [(lo, lo)]
 
     def problem(c0, c1):
         """Columns [c0, c1) of the global problem (and their clouds at C4)."""
@@ -224,44 +223,23 @@ def main():
     if args.sw_kernel:
         from rrtmgpnn import api
         api.set_sw_kernel_default(args.sw_kernel)
-    prob, clouds = problem(*chunks[0])
     if args.lw_after:
         os.environ["RRTMGPNN_LW_AFTER"] = args.lw_after
     if args.sw_after:
         os.environ["RRTMGPNN_SW_AFTER"] = args.sw_after
-    step = ClearSkyStep(prob, device=local, fused=not args.unfused, clouds=clouds, overlap=not args.no_overlap,
-                        sw=args.config not in ("c1", "c2"))
-    ncol, nlay = step.ncol, step.nlay
-    ins, outs = step.io_tensors()
-    # more than one chunk: every chunk's inputs resident in HBM, copied into the step's buffers before its replay and
-    # its fluxes copied out after it (device-to-device, inside the timed region)
-    chunk_ins = [None] * len(chunks)
-    rank_flux = None
-    if len(chunks) > 1:
-        chunk_ins[0] = [t.clone() for t in ins]
-        for k, (c0, c1) in enumerate(chunks[1:], 1):
-            if c1 - c0 != ncol:  # a short last chunk would need a step of its own shape
-                raise SystemExit("bench: rank range %d..%d does not split into %d-column chunks" % (lo, hi, ncol))
-            pk, ck = problem(c0, c1)
-            chunk_ins[k] = step.inputs_for(pk, ck)
-        rank_flux = [torch.empty((hi - lo,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev) for o in outs]
-
     use_graph = not args.no_graph
-    run_one = step.step
-    if use_graph:
-        step.capture()
-        run_one = step.replay
-
-    def run():
-        if len(chunks) == 1:
-            run_one()
-            return
-        for k, (c0, c1) in enumerate(chunks):
-            for d, src in zip(ins, chunk_ins[k]):
-                d.copy_(src, non_blocking=True)
-            run_one()
-            for r, o in zip(rank_flux, outs):
-                r[c0 - lo:c1 - lo].copy_(o, non_blocking=True)
+    # the rank's columns in chunks of at most one block (pipeline.ChunkedRank): with more than one chunk every chunk's
+    # inputs are resident in HBM and copied into the step's buffers before its replay, its fluxes copied into the
+    # rank's slab after it (device to device, inside the timed region); tests/test_gpu_chunked.py checks the slab
+    rank_run = ChunkedRank(lo, hi, block, problem,
+                           lambda p, c: ClearSkyStep(p, device=local, fused=not args.unfused, clouds=c,
+                                                     overlap=not args.no_overlap, sw=args.config not in ("c1", "c2")),
+                           use_graph=use_graph)
+    step = rank_run.step
+    prob, clouds = rank_run.first
+    ncol, nlay = step.ncol, step.nlay
+    run_one = step.replay if use_graph else step.step
+    run = rank_run.run
 
     for _ in range(args.warmup):
         run()
@@ -411,8 +389,7 @@ def main():
     gather_ms = None
     end_to_end = None
     if world > 1:
-        fl = rank_flux if rank_flux is not None else outs
-        local_slab = torch.stack(list(fl), dim=1)
+        local_slab = torch.stack(list(rank_run.flux), dim=1)
         torch.cuda.synchronize(dev)
         dist.barrier()
         g0 = time.perf_counter()
@@ -487,6 +464,11 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
     get_col_dry, output scaling, compute_Planck_source_nn) is the C restatement's (its reference modules need
     netcdf-fortran).  Blocks cycle through up to 3 600 columns of the workload; `reps` timed runs, the median
     reported (tests/test_cpu_bench.py checks the program's fluxes against the oracle bit for bit).
+
+    Threads: `value` is measured on the box's CPU share for one GPU (OMP_NUM_THREADS, 16 on the GPU box; this
+    process may not use more).  `thread_sweep` adds measured 1- and 8-thread points, and `extrapolated` scales the
+    16-thread value linearly to the per-GPU share of the whole node (nproc / 8 logical CPUs) and to all nproc: the
+    blocks are independent, so linear scaling is an upper bound on the CPU path there, not a measurement.
     kind "port": the C restatement alone, OpenMP over columns (when oracle/_ref is absent)."""
     import statistics
     import subprocess
@@ -502,32 +484,50 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
         sub = prob if nsamp == ncol else _subset(prob, np.arange(nsamp))
         cl = None if clouds is None else tuple(np.asarray(c)[:nsamp] for c in clouds)
         block = _cpu_block(nsamp)
-        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_STACKSIZE="256M", MKL_THREADING_LAYER="SEQUENTIAL")
         with tempfile.TemporaryDirectory() as td:
             path = os.path.join(td, "problem.rbin")
             data.write_problem(sub, path, clouds=cl)
 
-            def run(ncols, nreps):
-                r = subprocess.run([exe, path, data.DATA_DIR, str(threads), str(block), str(ncols), str(int(sw)),
+            def run(nthr, ncols, nreps):
+                env = dict(os.environ, OMP_NUM_THREADS=str(nthr), OMP_STACKSIZE="256M",
+                           MKL_THREADING_LAYER="SEQUENTIAL")
+                r = subprocess.run([exe, path, data.DATA_DIR, str(nthr), str(block), str(ncols), str(int(sw)),
                                     str(nreps)], capture_output=True, text=True, env=env, timeout=600)
                 if r.returncode != 0:
                     raise RuntimeError("rrtmgp_cpu_bench failed: " + (r.stdout + r.stderr)[-400:])
                 return json.loads(r.stdout.strip().splitlines()[-1])
 
-            try:
-                n0 = max(nsamp, 8 * threads * block)  # every thread busy for the calibration run too
-                cal = run(n0, 1)  # after the program's own untimed warm-up pass
-                per_rep = target_s / (reps + 1)
+            def measure(nthr, seconds, nreps):
+                n0 = max(nsamp, 8 * nthr * block)  # every thread busy for the calibration run too
+                cal = run(nthr, n0, 1)  # after the program's own untimed warm-up pass
+                per_rep = seconds / (nreps + 1)
                 n = max(nsamp, int(round(n0 * per_rep / max(cal["seconds"][0], 1e-4) / block)) * block)
-                res = run(n, reps)
+                return run(nthr, n, nreps)
+
+            try:
+                res = measure(threads, target_s, reps)
+                sweep = {}
+                for t in sorted({1, min(8, threads)} - {threads}):
+                    r = measure(t, max(2.0, target_s / 5), 3)
+                    sweep[str(t)] = round(r["columns"] / statistics.median(r["seconds"]), 1)
             except (RuntimeError, ValueError, subprocess.TimeoutExpired) as e:
                 return {"value": None, "unit": "columns/s", "cores": threads, "kind": "reference",
                         "sample": "failed: %s" % e}
         secs = res["seconds"]
         med = statistics.median(secs)
-        return {"value": round(res["columns"] / med, 1), "unit": "columns/s", "cores": threads, "kind": "reference",
-                "nproc": res["nproc"], "runs_s": [round(t, 4) for t in secs],
+        value = res["columns"] / med
+        sweep[str(threads)] = round(value, 1)
+        nproc = int(res["nproc"])
+        per_thread = value / threads
+        return {"value": round(value, 1), "unit": "columns/s", "cores": threads, "kind": "reference",
+                "nproc": nproc, "runs_s": [round(t, 4) for t in secs],
                 "spread": round((max(secs) - min(secs)) / med, 4),
+                "thread_sweep": sweep,
+                "extrapolated": {
+                    "per_gpu_share": {"threads": max(1, nproc // 8), "value": round(per_thread * max(1, nproc // 8), 1)},
+                    "node": {"threads": nproc, "value": round(per_thread * nproc, 1)},
+                    "note": "linear in threads from the measured value (an upper bound: blocks are independent); "
+                            "not measured -- one GPU's box share is %d threads" % threads},
                 "sample": ("%d columns per run (blocks of %d cycling through %d columns of the workload), %s, median "
                            "of %d runs: the reference's Fortran rte_lw/rte_sw + network_type sgemm MLP (MKL, "
                            "sequential)%s compiled from its sources, OpenMP over blocks on %d threads "

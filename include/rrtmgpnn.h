@@ -90,8 +90,10 @@ int rrtmgpnn_context_create_owned(int device, rrtmgpnn_context **ctx);
  *   kernel writes it; `create`); both bits: upload if needed, then device newer.  A different size for the same
  *   address replaces the entry (host newer).
  * rrtmgpnn_present_update_host: copy a device-newer array back (`!$acc update host`) and wait for it.
- * rrtmgpnn_present_update_device: the host copy changed: it is uploaded at its next READ (`!$acc update device`).
+ * rrtmgpnn_present_update_device: the host copy changed: it is uploaded at its next READ (`!$acc update device`),
+ *   in every context of the process (the reference's OpenACC data environment is process-wide).
  * rrtmgpnn_present_delete: drop the entry (its buffer returns to the pool; `!$acc exit data delete`); no-op if absent.
+ *   Every other context's copy of that host array is stale from then on and is uploaded again at its next READ.
  * rrtmgpnn_stage_h2d / rrtmgpnn_scratch / rrtmgpnn_release: stream-ordered per-call buffers from the same pool
  *   (a call's inputs copied in, its intermediates); released buffers are reused by later work on the stream.
  * rrtmgpnn_copy_d2h / rrtmgpnn_copy_h2d / rrtmgpnn_copy_d2d: enqueue a copy on the context's stream (the device side complete after

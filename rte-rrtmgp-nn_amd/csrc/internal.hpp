@@ -70,6 +70,7 @@ struct rrtmgpnn_context {
     void *dev = nullptr;
     size_t bytes = 0;
     int state = 0;  // 0 host newer, 1 both current, 2 device newer
+    uint64_t gen = 0;  // the host array's process-wide generation this copy was made at (present.cpp)
   };
   std::multimap<size_t, void *> pool_free;      // capacity -> buffer
   std::unordered_map<void *, size_t> pool_live;  // buffer -> capacity

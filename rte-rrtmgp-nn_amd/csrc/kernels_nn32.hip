@@ -26,6 +26,7 @@
 #include "nn_device.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <vector>
 
@@ -464,6 +465,8 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
   }
 }
 
+constexpr int kOccDevices = 64;
+
 template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN,
           int NT = kMlp32Threads, int WPE = 1>
 static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
@@ -483,11 +486,18 @@ static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
   // grid of one round strides them and loads each weight image once per CU, instead of a partial second round that
   // loads it again for little work (the SW pair at C3: 184 VGPRs, one 8-wave block per CU, 422 blocks: step -1 %).
   // With many rounds the blocks' turnover lets the overlapped LW chain share the CUs (C4: one round was 1 % slower).
-  static int occ = 0;
-  if (!occ) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)kern, NT, lds) == hipSuccess && nb > 0) occ = nb;
-    else occ = -1;
+  // Cached per (instance, device): contexts of several host threads launch concurrently, and a function's occupancy
+  // is a property of the device it runs on.
+  static std::atomic<int> occ_cache[kOccDevices];
+  int occ = -1;
+  if (ctx->device >= 0 && ctx->device < kOccDevices) {
+    occ = occ_cache[ctx->device].load(std::memory_order_relaxed);
+    if (!occ) {
+      int nb = 0;
+      occ = (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void *)kern, NT, lds) == hipSuccess && nb > 0)
+                ? nb : -1;
+      occ_cache[ctx->device].store(occ, std::memory_order_relaxed);
+    }
   }
   if (occ > 0 && want <= 2LL * occ * ctx->num_cus) per_cu = std::min(per_cu, occ);
 #endif

@@ -6,9 +6,18 @@
 // steady state of a block loop allocates nothing.  Every use of a buffer is ordered on the context's one stream,
 // so a buffer released after enqueueing its last kernel can be handed to the next request at once: the next user's
 // work is enqueued behind it.
+//
+// Present map: one per context (each OpenMP thread of the Fortran drop-in has its own), but the invalidations are
+// process-wide, as the reference's single OpenACC data environment is.  `update_device` and `delete` of a host array
+// bump that array's generation in a process-wide table; a context's copy made at an older generation is taken as
+// "host newer" on its next READ, in every context.  So a host array shared by the worker threads (a gas
+// concentration set_vmr re-sets from the serial region between parallel block loops: drop, deallocate, allocate at
+// the same address) is uploaded again by every worker instead of being served from its stale cached copy.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "internal.hpp"
 
@@ -16,6 +25,22 @@ using namespace rrtmgpnn;
 
 namespace {
 constexpr size_t kPoolGrain = 256;  // bytes; capacities are rounded up to this
+
+std::mutex g_gen_mu;
+std::unordered_map<const void *, uint64_t> g_gen;  // host array -> generation (absent: 0)
+
+uint64_t generation(const void *host)
+{
+  std::lock_guard<std::mutex> lk(g_gen_mu);
+  auto it = g_gen.find(host);
+  return it == g_gen.end() ? 0 : it->second;
+}
+
+void invalidate_everywhere(const void *host)
+{
+  std::lock_guard<std::mutex> lk(g_gen_mu);
+  ++g_gen[host];
+}
 
 int check(rrtmgpnn_context *ctx)
 {
@@ -173,6 +198,11 @@ int rrtmgpnn_present(rrtmgpnn_context *ctx, const void *host, long long bytes, i
     it = m.emplace(host, p).first;
   }
   auto &p = it->second;
+  const uint64_t gen = generation(host);
+  if (p.gen != gen) {  // updated or deleted through some context since this copy was made: the host copy is newer
+    p.state = 0;
+    p.gen = gen;
+  }
   if ((mode & RRTMGPNN_PRESENT_READ) && p.state == 0) {
     if (int rc = ctx->h2d(p.dev, host, p.bytes)) return rc;
     p.state = 1;
@@ -196,6 +226,7 @@ int rrtmgpnn_present_update_host(rrtmgpnn_context *ctx, void *host)
 int rrtmgpnn_present_update_device(rrtmgpnn_context *ctx, const void *host)
 {
   if (int rc = check(ctx)) return rc;
+  invalidate_everywhere(host);  // every context's copy (this one's too) is reloaded on its next READ
   auto it = ctx->present.find(host);
   if (it != ctx->present.end()) it->second.state = 0;
   return RRTMGPNN_OK;
@@ -204,6 +235,7 @@ int rrtmgpnn_present_update_device(rrtmgpnn_context *ctx, const void *host)
 int rrtmgpnn_present_delete(rrtmgpnn_context *ctx, const void *host)
 {
   if (int rc = check(ctx)) return rc;
+  invalidate_everywhere(host);  // other contexts keep their buffers, but their copies are stale from here on
   auto it = ctx->present.find(host);
   if (it == ctx->present.end()) return RRTMGPNN_OK;
   ctx->pool_put(it->second.dev);

@@ -7,7 +7,8 @@
 ! 1scl: lw_solver_noscat_GaussQuad; 2str: the rescaled solution (default) or lw_solver_2stream
 ! (use_2stream).  ty_fluxes_flexible g-point fluxes through the *_gpt entries: no-scattering and rescaled solutions
 ! with one angle the g-point radiances (quirk B-5), with several the angle-summed fluxes; lw_solver_2stream the adding
-! fluxes.  lw_Ds on 1scl properties; the Jacobians an error string (compute_Jac = .false.).
+! fluxes.  lw_Ds on 1scl properties; flux_up_Jac / flux_dn_Jac accepted and left untouched (compute_Jac = .false.),
+! an error string only with use_2stream, as the reference.
 module mo_rte_lw
   use, intrinsic :: iso_c_binding
   use mo_rte_kind,         only: wp
@@ -90,9 +91,9 @@ contains
       end if
       nmus = n_gauss_angles
     end if
-    if (present(flux_up_Jac) .or. present(flux_dn_Jac)) then
-      error_msg = "rte_lw: compute_Jac is .false. in this configuration (mo_rte_rrtmgp_config.F90:28)"; return
-    end if
+    ! flux_up_Jac / flux_dn_Jac: accepted and left untouched, as in the reference, where compute_Jac is a .false.
+    ! parameter (mo_rte_rrtmgp_config.F90:28): no extent check (:160-163), no write; rejected only with use_2stream
+    ! on 2str properties (:252-253, below).
     if (associated(fluxes%gpt_flux_up)) then
       if (any(shape(fluxes%gpt_flux_up) /= [ngpt, nlay + 1, ncol])) then
         error_msg = "rte_lw: gpt_flux_up inconsistently sized"; return
@@ -125,12 +126,14 @@ contains
         end if
       end if
     type is (ty_optical_props_2str)
-      if (present(lw_Ds)) then
-        error_msg = "rte_lw: lw_Ds not valid input for _2str class"; return
-      end if
-      if (use_2s .and. nmus /= 1) then
-        error_msg = "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"; return
-      end if
+      ! (:248-253) each check overwrites error_msg, so the last failing one is returned; the Jacobian check tests
+      ! flux_up_Jac twice (`present(flux_up_Jac) .or. present(flux_up_Jac)`), so a lone flux_dn_Jac passes there too
+      if (present(lw_Ds)) error_msg = "rte_lw: lw_Ds not valid input for _2str class"
+      if (use_2s .and. nmus /= 1) &
+        error_msg = "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"
+      if (use_2s .and. present(flux_up_Jac)) &
+        error_msg = "rte_lw: can't provide Jacobian of fluxes w.r.t surface temperature with 2-stream"
+      if (error_msg /= '') return
       if (use_2s .or. check_values) error_msg = optical_props%validate()  ! unconditional for 2-stream (:360)
       if (error_msg /= '') return
       two_str = .true.

@@ -746,12 +746,21 @@ def rte_lw(optical_props, top_at_1, sources, sfc_emis, fluxes, inc_flux=None, n_
         return "lw_solver(...ty_optical_props_nstr...) not yet implemented"
     if not is2 and use_2stream:
         return "rte_lw: can't use two-stream methods with only absorption optical depth"
-    if is2 and lw_Ds is not None:
-        return "rte_lw: lw_Ds not valid input for _2str class"
-    if is2 and use_2stream and n_gauss_angles is not None and nmu != 1:
-        return "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"
-    if flux_up_Jac is not None or flux_dn_Jac is not None:
-        return "rte_lw: compute_Jac is .false. in this configuration (rte/mo_rte_rrtmgp_config.F90:28)"
+    if is2:
+        # The reference's 2str checks (:248-253) each overwrite error_msg, so the last failing one is returned.  The
+        # Jacobian check tests flux_up_Jac twice (`present(flux_up_Jac) .or. present(flux_up_Jac)`), so a lone
+        # flux_dn_Jac passes, as there.
+        e = ""
+        if lw_Ds is not None:
+            e = "rte_lw: lw_Ds not valid input for _2str class"
+        if use_2stream and nmu != 1:
+            e = "rte_lw: using_2stream=true incompatible with specifying n_gauss_angles"
+        if use_2stream and flux_up_Jac is not None:
+            e = "rte_lw: can't provide Jacobian of fluxes w.r.t surface temperature with 2-stream"
+        if e:
+            return e
+    # flux_up_Jac / flux_dn_Jac are otherwise accepted and left untouched: compute_Jac is a .false. parameter
+    # (rte/mo_rte_rrtmgp_config.F90:28), so the reference neither checks their extents (:160-163) nor writes them.
     ncol, nlay, ngpt = optical_props.tau.shape
     if lw_Ds is not None:  # (:239-246); Fortran extents (ncol, ngpt) = this tensor layout's (ngpt, ncol)
         if tuple(lw_Ds.shape) != (ngpt, ncol):

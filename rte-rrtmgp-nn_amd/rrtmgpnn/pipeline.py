@@ -398,3 +398,56 @@ class ClearSkyStep:
     def fluxes(self):
         """Host copies of the broadband fluxes, with SW zeroed where sza >= 90 is applied by the caller."""
         return {k: getattr(self, k).cpu().numpy() for k in ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir")}
+
+
+class ChunkedRank:
+    """A rank's column range [lo, hi) streamed through one step in chunks (bench.py --global: a C5 rank holds more
+    columns than one step's block).  Every chunk's inputs stay resident in HBM; `run()` copies each chunk's inputs
+    into the step's input tensors (device to device, on the step's stream), replays the step (its hipGraph when
+    captured) and copies its fluxes into the rank's flux slab `flux` (lw_up, lw_dn, sw_up, sw_dn, sw_dir; (hi - lo,
+    nlay + 1) each).  A short last chunk runs through a second step of its own shape.
+
+    problem(c0, c1) -> (prob, clouds): columns [c0, c1) of the global problem.  make_step(prob, clouds) -> a
+    ClearSkyStep of that block's shape."""
+
+    def __init__(self, lo, hi, chunk, problem, make_step, use_graph=True):
+        self.lo, self.hi = lo, hi
+        self.chunks = [(c, min(c + chunk, hi)) for c in range(lo, hi, chunk)] or [(lo, lo)]
+        self.steps, self._run_of, self.chunk_ins, self._step_of = [], [], [], []
+        for k, (c0, c1) in enumerate(self.chunks):
+            prob, clouds = problem(c0, c1)
+            if k == 0:
+                self.first = (prob, clouds)  # the first chunk's host problem (bench.py's CPU baseline samples it)
+            st = next((s for s in self.steps if s.ncol == c1 - c0), None)
+            if st is None:
+                st = make_step(prob, clouds)
+                self.steps.append(st)
+                ins, _ = st.io_tensors()
+                self.chunk_ins.append([t.clone() for t in ins] if len(self.chunks) > 1 else None)
+                if use_graph:
+                    st.capture()
+            else:
+                self.chunk_ins.append(st.inputs_for(prob, clouds))
+            self._step_of.append(st)
+        self.step = self.steps[0]
+        dev = self.step.dev
+        outs = self.step.io_tensors()[1]
+        self.single = len(self.chunks) == 1
+        self.flux = list(outs) if self.single else [
+            torch.empty((hi - lo,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev) for o in outs]
+        self.use_graph = use_graph
+
+    def run(self):
+        if self.single:
+            st = self.step
+            st.replay() if self.use_graph else st.step()
+            return
+        for (c0, c1), st, src in zip(self.chunks, self._step_of, self.chunk_ins):
+            ins, outs = st.io_tensors()
+            with torch.cuda.stream(st.ctx.stream):
+                for d, s in zip(ins, src):
+                    d.copy_(s, non_blocking=True)
+            st.replay() if self.use_graph else st.step()
+            with torch.cuda.stream(st.ctx.stream):
+                for r, o in zip(self.flux, outs):
+                    r[c0 - self.lo:c1 - self.lo].copy_(o, non_blocking=True)

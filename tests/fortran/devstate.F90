@@ -8,7 +8,10 @@
 !   and with three Gauss angles (d), and rte_sw on two-stream properties tau = 0.1 tau_a, ssa = 0.5, g = 0.3 over the
 !   same spectral discretisation with g-point fluxes (e: mu0 = 0.6, inc_flux = 1, albedos 0.2); rte_lw on those
 !   two-stream properties with g-point fluxes, rescaled (f) and use_2stream (g); rte_sw on the 1scl tau of (b) with
-!   gpt_flux_dn_dir (h: the spectral direct beam).
+!   gpt_flux_dn_dir (h: the spectral direct beam); rte_lw with flux_up_Jac / flux_dn_Jac (filled with -7) on the 1scl
+!   tau of (b) (i) and on the two-stream properties, rescaled (j): '' returned, the Jacobian arrays untouched (written
+!   out as jac_up_i/jac_dn_i/jac_up_j/jac_dn_j), the fluxes those of (b) and (f); with use_2stream the reference's
+!   message for flux_up_Jac, and '' for a lone flux_dn_Jac (the reference tests flux_up_Jac twice, :252).
 program devstate
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -30,6 +33,9 @@ program devstate
   real(wp), allocatable, target :: gup_e(:,:,:), gdn_e(:,:,:), gdir_e(:,:,:)
   real(wp), allocatable, target :: up_f(:,:), dn_f(:,:), gup_f(:,:,:), gdn_f(:,:,:)
   real(wp), allocatable, target :: up_g(:,:), dn_g(:,:), gup_g(:,:,:), gdn_g(:,:,:), dir_h(:,:), gdir_h(:,:,:)
+  real(wp), allocatable, target :: up_i(:,:), dn_i(:,:), up_j(:,:), dn_j(:,:)
+  real(wp), allocatable, target :: jup_i(:,:), jdn_i(:,:), jup_j(:,:), jdn_j(:,:)
+  type(ty_fluxes_flexible) :: fl5
   type(ty_fluxes_flexible) :: fl3, fl4
   real(wp), allocatable :: lw_ds(:,:), inc(:,:), alb(:,:), mu0(:)
   type(ty_optical_props_2str) :: op2
@@ -148,7 +154,30 @@ program devstate
   fl4%flux_dn_dir => dir_h
   fl4%gpt_flux_dn_dir => gdir_h
   call chk(rte_sw(op, top_at_1, mu0, inc, alb, alb, fl4))
-  u = rbin_write_begin(ofile, 33)
+  ! (i), (j) the Jacobian arguments: accepted, untouched (compute_Jac = .false., mo_rte_rrtmgp_config.F90:28)
+  allocate(up_i(nlay + 1, ncol), dn_i(nlay + 1, ncol), up_j(nlay + 1, ncol), dn_j(nlay + 1, ncol))
+  allocate(jup_i(nlay + 1, ncol), jdn_i(nlay + 1, ncol), jup_j(nlay + 1, ncol), jdn_j(nlay + 1, ncol))
+  jup_i = -7._wp; jdn_i = -7._wp; jup_j = -7._wp; jdn_j = -7._wp
+  fl5%flux_up => up_i
+  fl5%flux_dn => dn_i
+  call chk(rte_lw(op, top_at_1, src, emis, fl5, flux_up_Jac=jup_i, flux_dn_Jac=jdn_i))
+  fl5%flux_up => up_j
+  fl5%flux_dn => dn_j
+  call chk(rte_lw(op2, top_at_1, src, emis, fl5, flux_up_Jac=jup_j, flux_dn_Jac=jdn_j))
+  e = rte_lw(op2, top_at_1, src, emis, fl5, use_2stream=.true., flux_up_Jac=jup_j, flux_dn_Jac=jdn_j)
+  if (e /= "rte_lw: can't provide Jacobian of fluxes w.r.t surface temperature with 2-stream") then
+    write(*, '(a)') "use_2stream with flux_up_Jac returned: '" // trim(e) // "'"
+    error stop 2
+  end if
+  e = rte_lw(op2, top_at_1, src, emis, fl5, use_2stream=.true., flux_dn_Jac=jdn_j)
+  if (e /= "") then
+    write(*, '(a)') "use_2stream with a lone flux_dn_Jac returned: '" // trim(e) // "'"
+    error stop 3
+  end if
+  fl5%flux_up => up_j
+  fl5%flux_dn => dn_j
+  call chk(rte_lw(op2, top_at_1, src, emis, fl5, flux_up_Jac=jup_j, flux_dn_Jac=jdn_j))
+  u = rbin_write_begin(ofile, 41)
   call rbin_write_real(u, "tau", tau0, shape(tau0))
   call rbin_write_real(u, "lay_source", lay0, shape(lay0))
   call rbin_write_real(u, "lev_source", lev0, shape(lev0))
@@ -182,6 +211,14 @@ program devstate
   call rbin_write_real(u, "gpt_dn_g", gdn_g, shape(gdn_g))
   call rbin_write_real(u, "flux_dir_h", dir_h, shape(dir_h))
   call rbin_write_real(u, "gpt_dir_h", gdir_h, shape(gdir_h))
+  call rbin_write_real(u, "flux_up_i", up_i, shape(up_i))
+  call rbin_write_real(u, "flux_dn_i", dn_i, shape(dn_i))
+  call rbin_write_real(u, "flux_up_j", up_j, shape(up_j))
+  call rbin_write_real(u, "flux_dn_j", dn_j, shape(dn_j))
+  call rbin_write_real(u, "jac_up_i", jup_i, shape(jup_i))
+  call rbin_write_real(u, "jac_dn_i", jdn_i, shape(jdn_i))
+  call rbin_write_real(u, "jac_up_j", jup_j, shape(jup_j))
+  call rbin_write_real(u, "jac_dn_j", jdn_j, shape(jdn_j))
   call rbin_write_end(u)
 contains
   subroutine chk(msg)

@@ -214,3 +214,47 @@ def test_fortran_device_state_update_host_and_device(tmp_path, orc, rfmip):
                                    prob["top_at_1"], gpt=True)
     np.testing.assert_array_equal(got["flux_dir_h"], dr)
     np.testing.assert_array_equal(got["gpt_dir_h"], gdr)
+    # (i), (j) flux_up_Jac / flux_dn_Jac accepted and untouched (compute_Jac = .false.), fluxes unchanged; the
+    # use_2stream messages are checked inside the program (exit status 2 / 3)
+    want_j = orc.lw_solver(t2, go["lay_source"], go["lev_source"], emis, go["sfc_source"], prob["top_at_1"], ssa=w2,
+                           g=g2)
+    for tag, want in (("i", (got["flux_up_b"], got["flux_dn_b"])), ("j", want_j)):
+        np.testing.assert_array_equal(got["flux_up_" + tag], want[0], err_msg=tag)
+        np.testing.assert_array_equal(got["flux_dn_" + tag], want[1], err_msg=tag)
+        for k in ("jac_up_", "jac_dn_"):
+            assert (got[k + tag] == np.float32(-7)).all(), k + tag
+
+
+@pytest.mark.gpu
+@needs_fc
+def test_fortran_vmr_reset_between_parallel_loops(tmp_path, orc, rfmip):
+    """4 OpenMP threads, each with its own device context, run gas optics + rte_lw over 4 blocks; between two such
+    loops the serial region re-sets h2o and o3 of every block (set_vmr: drop, deallocate, allocate at the same size,
+    usually the same address).  The process-wide invalidation of the device data environment (csrc/present.cpp)
+    makes loop 2 read the new values in every worker context: both loops are bit-identical to the oracle on their
+    own gases (tests/fortran/reset_vmr.F90)."""
+    from rrtmgpnn import data, rbin
+    _make()
+    lib = os.path.join(ROOT, "rte-rrtmgp-nn_amd")
+    exe = str(tmp_path / "reset_vmr")
+    r = subprocess.run([FC, "-O1", "-fopenmp", "-I", FBUILD, os.path.join(ROOT, "tests", "fortran", "reset_vmr.F90"),
+                        "-o", exe, os.path.join(FBUILD, "librrtmgpnn_fortran.a"), "-L" + lib, "-lrrtmgpnn",
+                        "-Wl,-rpath," + lib], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    prob = subset(rfmip, np.arange(3, 1800, 9))  # 200 columns: 4 blocks of 50
+    fin, fout = str(tmp_path / "in.rbin"), str(tmp_path / "out.rbin")
+    write_problem(prob, fin)
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(["timeout", "-k", "10", "120", exe, fin, fout, data.DATA_DIR, "50"], capture_output=True,
+                       text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = rbin.read(fout)
+    models, kd = [data.load_model("lw_abs"), data.load_model("lw_pfrac")], data.load_kdist("lw")
+    prob2 = dict(prob, gases=dict(prob["gases"]))
+    prob2["gases"]["h2o"] = (np.float32(0.5) * np.asarray(prob["gases"]["h2o"], np.float32)).astype(np.float32)
+    prob2["gases"]["o3"] = (np.float32(0.25) * np.asarray(prob["gases"]["o3"], np.float32)).astype(np.float32)
+    for loop, pr in (("1", prob), ("2", prob2)):
+        lu, ld, _ = orc.clear_sky_lw(pr, models, kd)
+        np.testing.assert_array_equal(got["flux_up_" + loop], lu, err_msg="loop " + loop)
+        np.testing.assert_array_equal(got["flux_dn_" + loop], ld, err_msg="loop " + loop)
+    assert not np.array_equal(got["flux_up_1"], got["flux_up_2"])

@@ -133,6 +133,48 @@ def test_lw_scattering_argument_checks(dev, prob):
         "rte_lw: can't use two-stream methods with only absorption optical depth"
 
 
+@pytest.mark.parametrize("kind", ["1scl", "2str"])
+def test_rte_lw_jacobian_arguments_as_reference(dev, orc, prob, kind):
+    """rte/mo_rte_lw.F90:64, 82-85, 160-163, 252-253 with compute_Jac = .false. (mo_rte_rrtmgp_config.F90:28):
+    flux_up_Jac / flux_dn_Jac are accepted on 1scl and on rescaled 2str properties, the fluxes are bit-identical to a
+    call without them and the arrays are left untouched; with use_2stream, flux_up_Jac gives the reference's message
+    and a lone flux_dn_Jac passes (the reference tests flux_up_Jac twice)."""
+    from rrtmgpnn import api
+    p, kd = prob, prob["kd"]
+    ncol, nlay, _ = p["tau"].shape
+    op = api.OpticalProps2str() if kind == "2str" else api.OpticalProps1scl()
+    assert op.init(kd["band_lims_wvn"], kd["band_lims_gpt"]) == ""
+    if kind == "2str":
+        assert op.alloc_2str(ncol, nlay, device=dev) == ""
+        op.ssa.copy_(T(p["ssa"], dev)), op.g.copy_(T(p["g"], dev))
+    else:
+        assert op.alloc_1scl(ncol, nlay, device=dev) == ""
+    op.tau.copy_(T(p["tau"], dev))
+    src = api.SourceFuncLW()
+    assert src.alloc(ncol, nlay, op, device=dev) == ""
+    src.lay_source.copy_(T(p["lay"], dev)), src.lev_source.copy_(T(p["lev"], dev))
+    src.sfc_source.copy_(T(p["sfc"], dev))
+    emis = T(p["emis_band"], dev)
+    f = lambda: torch.empty((ncol, nlay + 1), device=dev)  # noqa: E731
+    jup, jdn = torch.full((ncol, nlay + 1), -7.0, device=dev), torch.full((ncol, nlay + 1), -7.0, device=dev)
+    fl = api.FluxesBroadband(f(), f())
+    assert api.rte_lw(op, True, src, emis, fl, flux_up_Jac=jup, flux_dn_Jac=jdn) == ""
+    torch.cuda.synchronize()
+    if kind == "2str":
+        want = orc.lw_solver(p["tau"], p["lay"], p["lev"], p["emis_gpt"], p["sfc"], True, ssa=p["ssa"], g=p["g"])
+    else:
+        want = orc.lw_solver(p["tau"], p["lay"], p["lev"], p["emis_gpt"], p["sfc"], True)
+    np.testing.assert_array_equal(fl.flux_up.cpu().numpy(), want[0])
+    np.testing.assert_array_equal(fl.flux_dn.cpu().numpy(), want[1])
+    assert bool((jup == -7.0).all()) and bool((jdn == -7.0).all())
+    if kind == "2str":
+        assert api.rte_lw(op, True, src, emis, fl, use_2stream=True, flux_up_Jac=jup, flux_dn_Jac=jdn) == \
+            "rte_lw: can't provide Jacobian of fluxes w.r.t surface temperature with 2-stream"
+        assert api.rte_lw(op, True, src, emis, fl, use_2stream=True, flux_dn_Jac=jdn) == ""
+        torch.cuda.synchronize()
+        assert bool((jdn == -7.0).all())
+
+
 def kd_spec(kd):
     from rrtmgpnn import api
     s = api.OpticalProps()
