@@ -126,6 +126,15 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 #define SW_BOUNDS
 #endif
 static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
+// LW no-scattering flush: one lane per partial sum over padded ring rows when ngpt % 4 == 0 (RRTMGPNN_LW_FLUSH_LANES=0:
+// the float4 walk of ring_flush over unpadded rows)
+#ifndef RRTMGPNN_LW_FLUSH_LANES
+#define RRTMGPNN_LW_FLUSH_LANES 1
+#endif
+__host__ __device__ constexpr int lw_ring_stride(int ngpt)
+{
+  return (RRTMGPNN_LW_FLUSH_LANES && (ngpt & 3) == 0) ? ngpt + 4 : ngpt;
+}
 // SW with a fused increment: park the incremented (tau, ssa, g) in workspace for pass 3 (1), or have pass 3
 // re-read the inputs and form the increment again (0: three fewer planes written, one fewer read)
 #ifndef RRTMGPNN_SW_INC_PARK
@@ -189,8 +198,10 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   float *btab = smem + kExpTabFloats;                        // fused: [nbnd][2*nlay+1] + [nbnd]
   const int brow = 2 * nlay + 1;
-  float *ring = btab + (kFused ? lw_btab_floats(bands.nbnd, nlay) : 0);  // [kRing][ngpt]
-  float *part = ring + (size_t)kRing * ngpt;                 // [2][nlev][4]: 0 = dn, 1 = up
+  // [kRing][rs]: rows of ngpt floats, padded by 4 when the flush walks one lane per partial (rows in different banks)
+  const int rs = lw_ring_stride(ngpt);
+  float *ring = btab + (kFused ? lw_btab_floats(bands.nbnd, nlay) : 0);
+  float *part = ring + (size_t)kRing * rs;                   // [2][nlev][4]: 0 = dn, 1 = up
   load_exp_table(etab);
   const ColArr Ttau(tau, (size_t)ngpt * nlay * icol, row * nlay);
   const ColArr Tlay(lay, (size_t)ngpt * nlay * icol, row * nlay);  // lay_source, or pfrac when fused
@@ -237,12 +248,17 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
         *w = acc ? *w + x : x;
       }
     } else if (on) {
-      ring[(size_t)r * ngpt + g] = v;
+      ring[(size_t)r * rs + g] = v;
     }
   };
   auto flush = [&](float *pq, int n, int lev0, int dl) {
 #ifndef RRTMGPNN_ABL_NO_BARRIER
-    if constexpr (!kMulti) ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
+    if constexpr (!kMulti) {
+      if (rs != ngpt)
+        ring_flush_lanes(ring, rs, pq, n, lev0, dl, ngpt);
+      else
+        ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
+    }
 #endif
   };
   // layer source and the level source on the side given by `li` (lev index, 0..nlay)
@@ -385,7 +401,7 @@ static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, i
   a.rad = gpt && nmus == 1;
   for (int i = 0; i < nmus; i++) { a.D[i] = Ds[i]; a.w[i] = wts[i]; }
   int threads = (ngpt + 63) / 64 * 64;
-  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kRing * ngpt + (size_t)2 * (nlay + 1) * 4);
+  size_t lds = sizeof(float) * (kExpTabFloats + (size_t)kRing * lw_ring_stride(ngpt) + (size_t)2 * (nlay + 1) * 4);
   if (kFused) lds += sizeof(float) * lw_btab_floats(bands.nbnd, nlay);
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "lw solver: too many layers for LDS partials");
   // per-g accumulators: the caller's g-point arrays, or (several angles) the context workspace

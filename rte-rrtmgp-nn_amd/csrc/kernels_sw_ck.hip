@@ -22,78 +22,93 @@
 #include "x2_device.hpp"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace rrtmgpnn {
 using namespace x2;
 
 namespace {
 
-struct Dif2 {
-  f2 Rdif, Tdif, RT, k, emk, em2k, gamma1, gamma2;
-};
-
-__device__ __forceinline__ Dif2 ck_dif(f2 tau, f2 w0, f2 g, const uint64_t *etab)
-{
-  const float k_min = 1.e-4f;
-  Dif2 d;
-  d.gamma1 = (8.0f - w0 * (5.0f + 3.0f * g)) * .25f;
-  d.gamma2 = 3.0f * (w0 * (1.0f - g)) * .25f;
-  d.k = sqrt2(vmax((d.gamma1 - d.gamma2) * (d.gamma1 + d.gamma2), splat(k_min)));
-  d.emk = exp2v(-tau * d.k, etab);
-  d.em2k = d.emk * d.emk;
-  d.RT = rcp2(d.k * (1.0f + d.em2k) + d.gamma1 * (1.0f - d.em2k));
-  d.Rdif = d.RT * d.gamma2 * (1.0f - d.em2k);
-  d.Tdif = d.RT * 2.0f * d.k * d.emk;
-  return d;
-}
-
+// V: one lane's g-points, f2 (two per lane, packed fp32) or float (one per lane)
+template <class V>
 struct Coef2 {
-  f2 Rdif, Tdif, Sup, Sdn;
+  V Rdif, Tdif, Sup, Sdn;
 };
 
-// sw_two_stream (kernels_rte.hip) term by term, with the direct-beam transmittance Tnoscat = exp(-tau/mu0) given
-template <bool kG0>
-__device__ __forceinline__ Coef2 ck_two_stream(f2 tau, f2 w0, f2 g, float mu0, f2 Tnoscat, f2 dir_inc,
-                                               const uint64_t *etab)
+// max-by-magnitude guard of sw_two_stream's 1 - (k mu0)^2 denominator, element by element
+__device__ __forceinline__ float ck_eps_guard(float v, float eps) { return (fabsf(v) >= eps) ? v : eps; }
+__device__ __forceinline__ f2 ck_eps_guard(f2 v, float eps) { return (f2){ck_eps_guard(v.x, eps), ck_eps_guard(v.y, eps)}; }
+
+// sw_two_stream (kernels_rte.hip) term by term for the K layers of a chunk, with the direct-beam transmittances
+// Tnoscat = exp(-tau/mu0) given, stage by stage so that the K layers' exps share one batch of table reads
+template <bool kG0, int K, class V>
+__device__ __forceinline__ void ck_two_stream_k(const V (&tau)[K], const V (&w0)[K], const V (&g)[K], float mu0,
+                                                const V (&Tnoscat)[K], const V (&dir_inc)[K], Coef2<V> (&c)[K],
+                                                const uint64_t *etab)
 {
-  const float eps = FLT_EPSILON;
-  Coef2 c;
-  const Dif2 d = ck_dif(tau, w0, g, etab);
-  const f2 gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
-  const f2 gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? splat(0.5f) : (2.0f - 3.0f * mu0 * g) * .25f;
-  const f2 gamma4 = 1.0f - gamma3;
-  const f2 alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
-  const f2 alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
-  const f2 k2e = 2.0f * k * emk;
-  c.Rdif = d.Rdif;
-  c.Tdif = d.Tdif;
-  const f2 k_mu = k * mu0, k_mu2 = k_mu * k_mu, k_g3 = k * gamma3, k_g4 = k * gamma4;
-  const f2 omk = 1.0f - k_mu2;
-  f2 dd;
-  dd.x = (fabsf(omk.x) >= eps) ? omk.x : eps;
-  dd.y = (fabsf(omk.y) >= eps) ? omk.y : eps;
-  const f2 RT = div2(w0 * d.RT, dd);
-  f2 Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
-                  k2e * (gamma3 - alpha2 * mu0) * Tnoscat);
-  f2 Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
-                  Tnoscat * ((1.0f + k_mu) * (alpha1 + k_g4) - (1.0f - k_mu) * (alpha1 - k_g4) * em2k));
-  Rdir = vmax(splat(0.0f), vmin(Rdir, (1.0f - Tnoscat)));
-  Tdir = vmax(splat(0.0f), vmin(Tdir, (1.0f - Tnoscat - Rdir)));
-  c.Sup = Rdir * dir_inc;
-  c.Sdn = Tdir * dir_inc;
-  return c;
+  const float eps = FLT_EPSILON, k_min = 1.e-4f;
+  V gamma1[K], gamma2[K], k[K], arg[K], emk[K];
+#pragma unroll
+  for (int p = 0; p < K; p++) {
+    gamma1[p] = (8.0f - w0[p] * (5.0f + 3.0f * g[p])) * .25f;
+    gamma2[p] = 3.0f * (w0[p] * (1.0f - g[p])) * .25f;
+    k[p] = sqrt2(vmax((gamma1[p] - gamma2[p]) * (gamma1[p] + gamma2[p]), (V)k_min));
+    arg[p] = -tau[p] * k[p];
+  }
+  exp_neg_batch(arg, emk, etab);
+#pragma unroll
+  for (int p = 0; p < K; p++) {
+    const V em2k = emk[p] * emk[p];
+    const V RTd = rcp2(k[p] * (1.0f + em2k) + gamma1[p] * (1.0f - em2k));
+    c[p].Rdif = RTd * gamma2[p] * (1.0f - em2k);
+    c[p].Tdif = RTd * 2.0f * k[p] * emk[p];
+    const V gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? (V)0.5f : (2.0f - 3.0f * mu0 * g[p]) * .25f;
+    const V gamma4 = 1.0f - gamma3;
+    const V alpha1 = gamma1[p] * gamma4 + gamma2[p] * gamma3;
+    const V alpha2 = gamma1[p] * gamma3 + gamma2[p] * gamma4;
+    const V k2e = 2.0f * k[p] * emk[p];
+    const V k_mu = k[p] * mu0, k_mu2 = k_mu * k_mu, k_g3 = k[p] * gamma3, k_g4 = k[p] * gamma4;
+    const V dd = ck_eps_guard(1.0f - k_mu2, eps);
+    const V RT = div2(w0[p] * RTd, dd);
+    const V Tn = Tnoscat[p];
+    V Rdir = RT * ((1.0f - k_mu) * (alpha2 + k_g3) - (1.0f + k_mu) * (alpha2 - k_g3) * em2k -
+                   k2e * (gamma3 - alpha2 * mu0) * Tn);
+    V Tdir = RT * (k2e * (gamma4 + alpha1 * mu0) -
+                   Tn * ((1.0f + k_mu) * (alpha1 + k_g4) - (1.0f - k_mu) * (alpha1 - k_g4) * em2k));
+    Rdir = vmax((V)0.0f, vmin(Rdir, (1.0f - Tn)));
+    Tdir = vmax((V)0.0f, vmin(Tdir, (1.0f - Tn - Rdir)));
+    c[p].Sup = Rdir * dir_inc[p];
+    c[p].Sdn = Tdir * dir_inc[p];
+  }
 }
 
-// inc_2stream_by_2stream_bybnd (rte/kernels/mo_optical_props_kernels.F90:430-463) for a pair, as inc_2str2
-__device__ __forceinline__ void ck_inc(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, f2 g2)
+// inc_2stream_by_2stream_bybnd (rte/kernels/mo_optical_props_kernels.F90:430-463) for a lane's g-points, as inc_2str2
+template <class V>
+__device__ __forceinline__ void ck_inc(V &t1, V &w1, V &g1, V t2, V w2, V g2)
 {
   const float eps = 3.0f * FLT_MIN;
-  const f2 tau12 = t1 + t2;
-  const f2 tauscat12 = t1 * w1 + t2 * w2;
-  g1 = (t1 * w1 * g1 + t2 * w2 * g2) / vmax(splat(eps), tauscat12);
-  w1 = tauscat12 / vmax(splat(eps), tau12);
+  const V tau12 = t1 + t2;
+  const V tauscat12 = t1 * w1 + t2 * w2;
+  g1 = (t1 * w1 * g1 + t2 * w2 * g2) / vmax((V)eps, tauscat12);
+  w1 = tauscat12 / vmax((V)eps, tau12);
   t1 = tau12;
 }
+
+// the flush walks the ordered sums one lane per partial (ring_flush_sw_lanes) when the block has the lanes for it
+#ifndef RRTMGPNN_SWCK_FLUSH_LANES
+#define RRTMGPNN_SWCK_FLUSH_LANES 1
+#endif
+constexpr bool kCkFlushLanes = RRTMGPNN_SWCK_FLUSH_LANES != 0;
+// stagger the blocks' flushes (see pass 3)
+#ifndef RRTMGPNN_SWCK_FLUSH_PHASE
+#define RRTMGPNN_SWCK_FLUSH_PHASE 1
+#endif
+constexpr bool kCkFlushPhase = RRTMGPNN_SWCK_FLUSH_PHASE != 0;
+// floats per row of the flux ring (RRTMGPNN_SWCK_RING_PAD: 4, or 0 for unpadded rows)
+#ifndef RRTMGPNN_SWCK_RING_PAD
+#define RRTMGPNN_SWCK_RING_PAD 4
+#endif
+__host__ __device__ constexpr int ck_ring_stride(int ngpt) { return ngpt + RRTMGPNN_SWCK_RING_PAD; }
 
 }  // namespace
 
@@ -110,12 +125,11 @@ __device__ __forceinline__ void ck_inc(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, f2 
 #ifndef RRTMGPNN_SWCK_WAVES
 #define RRTMGPNN_SWCK_WAVES 3
 #endif
-// KEEPD = 1: the walk up keeps each layer's adding denominator for the walk down (K more register pairs); 0: the walk
-// down forms it again (one more reciprocal per element, fewer registers)
-#ifndef RRTMGPNN_SWCK_KEEPD
-#define RRTMGPNN_SWCK_KEEPD 1
+// pass 1 loads kCkP1 chunks of optical depths per step (and the next step's while it computes)
+#ifndef RRTMGPNN_SWCK_P1
+#define RRTMGPNN_SWCK_P1 2
 #endif
-constexpr bool kCkKeepD = RRTMGPNN_SWCK_KEEPD != 0;
+constexpr int kCkP1 = RRTMGPNN_SWCK_P1;
 constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
 
 // Waves per SIMD of the clear-sky NN instance (g = NULL, no increment), which needs fewer registers: at 4 (128 VGPRs,
@@ -151,14 +165,22 @@ constexpr int kCkKSmall = RRTMGPNN_SWCK_K_SMALL, kCkRingSmall = RRTMGPNN_SWCK_RI
 #define RRTMGPNN_SWCK_TN_SMALL 1
 #endif
 constexpr bool kCkTnSmall = RRTMGPNN_SWCK_TN_SMALL != 0;
+// g-points per lane of the small-grid instance: 1 doubles the waves the grid has to hide latency with (packed fp32
+// issues at the same cost per element as scalar fp32 on gfx950, tools/valu_rates.hip)
+#ifndef RRTMGPNN_SWCK_NPL_SMALL
+#define RRTMGPNN_SWCK_NPL_SMALL 2
+#endif
+using VSmall = std::conditional_t<RRTMGPNN_SWCK_NPL_SMALL == 1, float, f2>;
 // the same for the all-sky instances (fused cloud increment), whatever the grid
 #ifndef RRTMGPNN_SWCK_TN_INC
 #define RRTMGPNN_SWCK_TN_INC 0
 #endif
 constexpr bool kCkTnInc = RRTMGPNN_SWCK_TN_INC != 0;
 
+// V: f2 (two g-points per lane) or float (one per lane)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
-          int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES, bool kTn = false>
+          int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES, bool kTn = false,
+          class V = f2>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -172,16 +194,20 @@ __global__ void __launch_bounds__(512, WAVES)
   static_assert(R % K == 0, "the flux ring must hold whole chunks");
   constexpr bool kG0 = !kHasG && !kInc;  // g is the literal 0 (the NN path)
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  // `ncb` columns per block: lane t works on column c = t / (ngpt/2), g-points g, g + 1
-  const int nlev = nlay + 1, lanes = ngpt / 2, nck = (nlay + K - 1) / K;
+  // `ncb` columns per block: lane t works on column c = t / (ngpt/NPL), g-points g .. g + NPL - 1
+  constexpr int NPL = sizeof(V) / sizeof(float);
+  using CA_ = ColArrV<V>;
+  const int nlev = nlay + 1, lanes = ngpt / NPL, nck = (nlay + K - 1) / K;
   const int icol0 = blockIdx.x * ncb, nc = min(ncb, ncol - icol0);
   const int craw = (int)threadIdx.x / lanes;
   const bool on = craw < nc;
   const int c = on ? craw : nc - 1;
-  const int g = 2 * ((int)threadIdx.x - craw * lanes);
-  const int gc = on ? g : ngpt - 2;
+  const int g = NPL * ((int)threadIdx.x - craw * lanes);
+  const int gc = on ? g : ngpt - NPL;
   const int icol = icol0 + c;
-  float *ring = smem + kExpTabFloats + (size_t)c * 3 * R * ngpt;  // this column's [3][R][ngpt]
+  // this column's ring [3][R][rs]: rows padded by 4 floats, so the flush threads' rows start in different LDS banks
+  const int rs = ck_ring_stride(ngpt);
+  float *ring = smem + kExpTabFloats + (size_t)c * 3 * R * rs;
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   load_exp_table(etab);
   __syncthreads();
@@ -189,214 +215,279 @@ __global__ void __launch_bounds__(512, WAVES)
   const uint32_t vL = 4u * (uint32_t)gc + (uint32_t)c * row * nlay;
   const size_t cl = (size_t)ngpt * nlay * icol0;
   const uint32_t bL = (uint32_t)nc * row * nlay;
-  const ColArr2 Ttau(tau, cl, bL), Tssa(ssa, cl, bL), Tg(kHasG ? gg : tau, cl, bL);
+  const CA_ Ttau(tau, cl, bL), Tssa(ssa, cl, bL), Tg(kHasG ? gg : tau, cl, bL);
   // checkpoints: beam (ngpt, nck, ncol), albedo and source (ngpt, nck+1, ncol)
   const size_t pB = (size_t)ngpt * nck * ncol, pA = (size_t)ngpt * (nck + 1) * ncol;
   const uint32_t vB = 4u * (uint32_t)gc + (uint32_t)c * row * nck, vA = 4u * (uint32_t)gc + (uint32_t)c * row * (nck + 1);
-  const ColArr2 CB(ws, (size_t)ngpt * nck * icol0, (uint32_t)nc * row * nck);
-  const ColArr2 CA(ws + pB, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
-  const ColArr2 CS(ws + pB + pA, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
+  const CA_ CB(ws, (size_t)ngpt * nck * icol0, (uint32_t)nc * row * nck);
+  const CA_ CA(ws + pB, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
+  const CA_ CS(ws + pB + pA, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
   // kTn: the beam transmittances (ngpt, nlay, ncol), addressed as tau
-  const ColArr2 CT(kTn ? ws + pB + 2 * pA : ws, kTn ? cl : 0, kTn ? bL : 0u);
+  const CA_ CT(kTn ? ws + pB + 2 * pA : ws, kTn ? cl : 0, kTn ? bL : 0u);
   const uint32_t vBs = on ? vB : kBufOOB, vAs = on ? vA : kBufOOB;
-  // band-resolved increments: one band offset per g-point of the pair
+  // band-resolved increments: one band offset per g-point of the lane
   const size_t cb = (size_t)bands.nbnd * nlay * icol0;
   const uint32_t brow = 4u * (uint32_t)bands.nbnd, vbc = (uint32_t)c * brow * nlay;
   const uint32_t vb0 = kInc ? 4u * (uint32_t)band_of(bands, gc) + vbc : 0u,
-                 vb1 = kInc ? 4u * (uint32_t)band_of(bands, gc + 1) + vbc : 0u;
+                 vb1 = kInc ? 4u * (uint32_t)band_of(bands, gc + NPL - 1) + vbc : 0u;
   const uint32_t bB = kInc ? (uint32_t)nc * brow * nlay : 0u;
-  const ColArr2 Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, bB), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, bB),
+  const CA_ Bt(kInc ? tau_bnd : tau, kInc ? cb : 0, bB), Bw(kInc ? ssa_bnd : tau, kInc ? cb : 0, bB),
       Bg(kInc ? g_bnd : tau, kInc ? cb : 0, bB);
-  auto ld_bnd = [&](const ColArr2 &a, int l) {
-    return kInc ? (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)} : splat(0.0f);
+  auto ld_bnd = [&](const CA_ &a, int l) -> V {
+    if constexpr (!kInc) return (V)0.0f;
+    else if constexpr (NPL == 2) return (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)};
+    else return a.ld1(vb0, brow * (uint32_t)l);
   };
   const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
   // j counts layers from the top (clamped to the last layer); the result is the array layer
   auto lay = [&](int j) { return top_at_1 ? min(j, nlay - 1) : nlay - 1 - min(j, nlay - 1); };
-  auto ld_col = [&](const float *p) { return on ? *(const f2 *)(p + gc + (size_t)ngpt * icol) : splat(0.0f); };
+  auto ld_col = [&](const float *p) -> V { return on ? *(const V *)(p + gc + (size_t)ngpt * icol) : (V)0.0f; };
   const int top = top_at_1 ? 0 : nlay;
-  const f2 Ftop = ld_col(inc_flux) * mu0;
+  const V Ftop = ld_col(inc_flux) * mu0;
 
-  // one chunk's optical properties (the band increment is formed as they are used, as inc_2str2 does)
+  // one chunk's optical properties (the band increment is formed as they are used, as inc_2str2 does), with the
+  // checkpoints the pass reads for it: fb the beam at the chunk's top (pass 2), ae / se the albedo and source at its
+  // bottom (pass 3)
   struct Chunk {
-    f2 t[K], w[K], g[K], qt[K], qw[K], qg[K], tn[K];
+    V t[K], w[K], g[K], qt[K], qw[K], qg[K], tn[K], fb, ae, se;
   };
-  auto load_chunk = [&](Chunk &ch, int ck, bool with_ssa) {
+  // pass: 2 or 3
+  auto load_chunk = [&](Chunk &ch, int ck, int pass) {
 #pragma unroll
     for (int p = 0; p < K; p++) {
       const int l = lay(ck * K + p);
       const uint32_t s = row * (uint32_t)l;
-      ch.t[p] = Ttau.ld(vL, s);
-      ch.tn[p] = kTn && with_ssa ? CT.ld(vL, s) : splat(0.0f);
-      ch.w[p] = with_ssa ? Tssa.ld(vL, s) : splat(0.0f);
-      ch.g[p] = kHasG && with_ssa ? Tg.ld(vL, s) : splat(0.0f);
+      ch.t[p] = Ttau.ldv(vL, s);
+      ch.tn[p] = kTn ? CT.ldv(vL, s) : (V)0.0f;
+      ch.w[p] = Tssa.ldv(vL, s);
+      ch.g[p] = kHasG ? Tg.ldv(vL, s) : (V)0.0f;
       if constexpr (kInc) {
         ch.qt[p] = ld_bnd(Bt, l);
-        ch.qw[p] = with_ssa ? ld_bnd(Bw, l) : splat(0.0f);
-        ch.qg[p] = with_ssa ? ld_bnd(Bg, l) : splat(0.0f);
+        ch.qw[p] = ld_bnd(Bw, l);
+        ch.qg[p] = ld_bnd(Bg, l);
       } else {
-        ch.qt[p] = ch.qw[p] = ch.qg[p] = splat(0.0f);
+        ch.qt[p] = ch.qw[p] = ch.qg[p] = (V)0.0f;
       }
+    }
+    if (pass == 2) {
+      ch.fb = CB.ldv(vB, row * (uint32_t)ck);
+    } else {
+      const uint32_t sE = row * (uint32_t)min(ck + 1, nck);
+      ch.ae = CA.ldv(vA, sE);
+      ch.se = CS.ldv(vA, sE);
     }
   };
   // the (incremented) properties of layer p of a chunk
-  auto props = [&](const Chunk &ch, int p, f2 &t, f2 &w, f2 &g0) {
+  auto props = [&](const Chunk &ch, int p, V &t, V &w, V &g0) {
     t = ch.t[p];
     w = ch.w[p];
-    g0 = kHasG ? ch.g[p] : splat(0.0f);
+    g0 = kHasG ? ch.g[p] : (V)0.0f;
     if constexpr (kInc) ck_inc(t, w, g0, ch.qt[p], ch.qw[p], ch.qg[p]);
+  };
+  // Each pass walks its chunks two at a time through two register buffers: the loads of the next chunk go to the other
+  // buffer while this one is computed, so no copy waits for them at the end of the step.  body(buf, ck, valid)
+  // computes chunk ck; idx(i) is the pass's i-th chunk.  With an odd count the last step's second body runs on the
+  // last chunk again with valid = false (no state change, no stores), so that no branch separates a prefetch from its
+  // use (the compiler sinks loads past such a branch); the scheduling fences keep each prefetch ahead of the compute.
+  auto walk = [&](auto &&load, auto &&body, int count, auto &&idx, auto &A, auto &B) {
+    load(A, idx(0));
+    for (int i = 0; i < count; i += 2) {
+      load(B, idx(min(i + 1, count - 1)));
+      __builtin_amdgcn_sched_barrier(0);
+      body(A, idx(i), true);
+      load(A, idx(min(i + 2, count - 1)));
+      __builtin_amdgcn_sched_barrier(0);
+      body(B, idx(min(i + 1, count - 1)), i + 1 < count);
+    }
   };
 
   // ---- pass 1: direct beam, checkpoint at every chunk top ----
-  f2 Fd = Ftop;
+  // Steps of P1 = kCkP1 * K layers: pass 1 has little arithmetic per layer, so it needs many loads in flight.
+  V Fd = Ftop;
   {
-    Chunk cur, nxt;
-    load_chunk(cur, 0, false);
-    for (int ck = 0; ck < nck; ck++) {
-      CB.st(Fd, vBs, row * (uint32_t)ck);
-      load_chunk(nxt, min(ck + 1, nck - 1), false);
-      const int n = min(K, nlay - ck * K);
-      f2 Tn[K];
+    constexpr int P1 = kCkP1 * K;
+    const int np1 = (nlay + P1 - 1) / P1;
+    struct Buf1 {
+      V t[P1];
+    } A1, B1;
+    auto load1 = [&](Buf1 &b, int c1) {
 #pragma unroll
-      for (int p = 0; p < K; p++) Tn[p] = exp2v_beam(-(kInc ? cur.t[p] + cur.qt[p] : cur.t[p]) * mu0_inv, etab);
+      for (int p = 0; p < P1; p++) {
+        const int l = lay(c1 * P1 + p);
+        b.t[p] = Ttau.ldv(vL, row * (uint32_t)l);
+        if constexpr (kInc) b.t[p] += ld_bnd(Bt, l);
+      }
+    };
+    auto body1 = [&](Buf1 &b, int c1, bool valid) {
+      const int n = valid ? min(P1, nlay - c1 * P1) : 0;
+      V arg[P1], Tn[P1];
+#pragma unroll
+      for (int p = 0; p < P1; p++) arg[p] = -b.t[p] * mu0_inv;
+      exp_beam_batch(arg, Tn, etab);
       if constexpr (kTn) {
 #pragma unroll
-        for (int p = 0; p < K; p++) CT.st(Tn[p], (on && p < n) ? vL : kBufOOB, row * (uint32_t)lay(ck * K + p));
+        for (int p = 0; p < P1; p++) CT.stv(Tn[p], (on && p < n) ? vL : kBufOOB, row * (uint32_t)lay(c1 * P1 + p));
       }
 #pragma unroll
-      for (int p = 0; p < K; p++)
-        if (p < n) Fd = Tn[p] * Fd;
-      cur = nxt;
-    }
+      for (int p = 0; p < P1; p++) {
+        if (p % K == 0) CB.stv(Fd, (p < n) ? vBs : kBufOOB, row * (uint32_t)(c1 * kCkP1 + p / K));
+        Fd = (p < n) ? Tn[p] * Fd : Fd;
+      }
+    };
+    walk(load1, body1, np1, [](int i) { return i; }, A1, B1);
   }
+#ifdef RRTMGPNN_ABL_SWCK_PASSES  // ablation builds only (timing of the passes; results are not produced)
+  if (RRTMGPNN_ABL_SWCK_PASSES < 2) return;
+#endif
   // ---- pass 2: bottom -> top adding; albedo / source checkpoint at every chunk top and at the surface ----
-  f2 alb_b = ld_col(alb_dif);
-  f2 src_b = Fd * ld_col(alb_dir);
-  CA.st(alb_b, vAs, row * (uint32_t)nck);
-  CS.st(src_b, vAs, row * (uint32_t)nck);
+  V alb_b = ld_col(alb_dif);
+  V src_b = Fd * ld_col(alb_dir);
+  CA.stv(alb_b, vAs, row * (uint32_t)nck);
+  CS.stv(src_b, vAs, row * (uint32_t)nck);
   {
-    Chunk cur, nxt;
-    load_chunk(cur, nck - 1, true);
-    f2 Fb = CB.ld(vB, row * (uint32_t)(nck - 1));
-    for (int ck = nck - 1; ck >= 0; ck--) {
-      const int n = min(K, nlay - ck * K);
-      load_chunk(nxt, max(ck - 1, 0), true);
-      const f2 Fbn = CB.ld(vB, row * (uint32_t)max(ck - 1, 0));
-      f2 t[K], w[K], g0[K], Tn[K], Fin[K];
+    Chunk A, B;
+    auto load2 = [&](Chunk &ch, int ck) { load_chunk(ch, ck, 2); };
+    auto body2 = [&](Chunk &cur, int ck, bool valid) {
+      const int n = valid ? min(K, nlay - ck * K) : 0;
+      V t[K], w[K], g0[K], Tn[K], Fin[K];
+      V Fb = cur.fb;
+#pragma unroll
+      for (int p = 0; p < K; p++) props(cur, p, t[p], w[p], g0[p]);
+      if constexpr (kTn) {
+#pragma unroll
+        for (int p = 0; p < K; p++) Tn[p] = cur.tn[p];  // pass 1's transmittances
+      } else {
+        V arg[K];
+#pragma unroll
+        for (int p = 0; p < K; p++) arg[p] = -t[p] * mu0_inv;
+        exp_beam_batch(arg, Tn, etab);  // pass 1's expressions, same bits
+      }
 #pragma unroll
       for (int p = 0; p < K; p++) {
-        props(cur, p, t[p], w[p], g0[p]);
-        Tn[p] = kTn ? cur.tn[p] : exp2v_beam(-t[p] * mu0_inv, etab);  // pass 1's transmittance, same bits
-        Fin[p] = Fb;                           // the beam at the layer's top
+        Fin[p] = Fb;  // the beam at the layer's top
         Fb = Tn[p] * Fb;
       }
+      // the chunk's coefficients (layers past nlay in the last chunk see the clamped last layer and are not used),
+      // then the adding recurrence
+      Coef2<V> cf[K];
+      ck_two_stream_k<kG0>(t, w, g0, mu0, Tn, Fin, cf, etab);
 #pragma unroll
       for (int p = K - 1; p >= 0; p--) {
-        if (p < n) {
-          const Coef2 cf = ck_two_stream<kG0>(t[p], w[p], g0[p], mu0, Tn[p], Fin[p], etab);
-          const f2 denom = rcp2(1.0f - cf.Rdif * alb_b);
-          const f2 alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
-          const f2 src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
-          alb_b = alb;
-          src_b = src;
-        }
+        const V denom = rcp2(1.0f - cf[p].Rdif * alb_b);
+        const V alb = cf[p].Rdif + cf[p].Tdif * cf[p].Tdif * alb_b * denom;
+        const V src = cf[p].Sup + cf[p].Tdif * denom * (src_b + alb_b * cf[p].Sdn);
+        alb_b = (p < n) ? alb : alb_b;
+        src_b = (p < n) ? src : src_b;
       }
-      CA.st(alb_b, ck > 0 ? vAs : kBufOOB, row * (uint32_t)ck);
-      CS.st(src_b, ck > 0 ? vAs : kBufOOB, row * (uint32_t)ck);
-      cur = nxt;
-      Fb = Fbn;
-    }
+      CA.stv(alb_b, valid && ck > 0 ? vAs : kBufOOB, row * (uint32_t)ck);
+      CS.stv(src_b, valid && ck > 0 ? vAs : kBufOOB, row * (uint32_t)ck);
+    };
+    walk(load2, body2, nck, [&](int i) { return nck - 1 - i; }, A, B);
   }
+#ifdef RRTMGPNN_ABL_SWCK_PASSES
+  if (RRTMGPNN_ABL_SWCK_PASSES < 3) return;
+#endif
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
+  // idle lanes (past the block's columns) store their ring values to one spare slot instead of branching around the
+  // stores; slots past the last level (the last chunk's padding layers) are written and never read
+  float *const spare = smem + kExpTabFloats + (size_t)ncb * 3 * R * rs;
   // level `lev` (array index) of the g-point outputs
-  auto put = [&](f2 up, f2 dif, f2 dir, int r, int lev) {
-    if (on) {
-      const f2 dn = kGpt ? dif + dir : dif;  // kGpt: the total, rounded once ("flux_dn is total", :665-666)
-      *(f2 *)&ring[(size_t)r * ngpt + g] = up;
-      *(f2 *)&ring[((size_t)R + r) * ngpt + g] = dn;
-      *(f2 *)&ring[((size_t)2 * R + r) * ngpt + g] = dir;
-      if constexpr (kGpt) {
+  auto put = [&](V up, V dif, V dir, int r, int lev, bool valid) {
+    const V dn = kGpt ? dif + dir : dif;  // kGpt: the total, rounded once ("flux_dn is total", :665-666)
+    *(V *)(on ? &ring[(size_t)r * rs + g] : spare) = up;
+    *(V *)(on ? &ring[((size_t)R + r) * rs + g] : spare) = dn;
+    *(V *)(on ? &ring[((size_t)2 * R + r) * rs + g] : spare) = dir;
+    if constexpr (kGpt) {
+      if (on && valid) {
         const size_t o = (size_t)g + (size_t)ngpt * ((size_t)lev + (size_t)nlev * icol);
-        *(f2 *)&gpt_up[o] = up;
-        *(f2 *)&gpt_dn[o] = dn;
-        *(f2 *)&gpt_dir[o] = dir;
+        *(V *)&gpt_up[o] = up;
+        *(V *)&gpt_dn[o] = dn;
+        *(V *)&gpt_dir[o] = dir;
       }
     }
   };
-  auto flush = [&](int n, int lev0, int dl) {
-    ring_flush_sw<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
-                           flux_dir);
+  auto flush = [&](int n, int lev0, int dl, int slot0 = 0) {
+#ifdef RRTMGPNN_ABL_SWCK_NO_FLUSH  // ablation builds only
+    return;
+#endif
+    if (kCkFlushLanes && (ngpt & 3) == 0 && 3 * ncb * n * 4 <= (int)blockDim.x)
+      ring_flush_sw_lanes<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
+                                   flux_dir, rs, slot0);
+    else
+      ring_flush_sw<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
+                             flux_dir, rs, slot0);
   };
+  // The ring holds M chunks; a block flushes it when its last group fills.  Blocks resident together run in near
+  // lockstep, and the flush (a barrier, then one wave walking the ordered sums) would stall them all at once: with
+  // kCkFlushPhase, a block's chunks are offset by `ph` groups (its first flush comes after M - ph chunks), so the blocks
+  // sharing a CU flush at different chunks and the others compute meanwhile.
+  constexpr int M = R / K;
+  const int ph = kCkFlushPhase ? (int)(((blockIdx.x >> 3) ^ (blockIdx.x >> 8)) % M) : 0;
   const int dl_dn = top_at_1 ? 1 : -1;
-  f2 Fdn = inc_dif ? ld_col(inc_dif) : splat(0.0f);
-  put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top);
+  V Fdn = inc_dif ? ld_col(inc_dif) : (V)0.0f;
+  put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top, true);
   flush(1, top, 1);
   {
-    Chunk cur, nxt;
-    load_chunk(cur, 0, true);
-    f2 albE = CA.ld(vA, row * 1u), srcE = CS.ld(vA, row * 1u);  // level min(K, nlay): the chunk's bottom
-    f2 Fd3 = Ftop;
-    for (int ck = 0; ck < nck; ck++) {
-      const int n = min(K, nlay - ck * K);
-      load_chunk(nxt, min(ck + 1, nck - 1), true);
-      const uint32_t sE = row * (uint32_t)min(ck + 2, nck);
-      const f2 albN = CA.ld(vA, sE), srcN = CS.ld(vA, sE);
+    Chunk A, B;
+    V Fd3 = Ftop;
+    auto load3 = [&](Chunk &ch, int ck) { load_chunk(ch, ck, 3); };
+    auto body3 = [&](Chunk &cur, int ck, bool valid) {
+      const int n = valid ? min(K, nlay - ck * K) : 0;
       // the chunk's coefficients, top down, the beam carried as pass 1 carries it
-      f2 Rd[K], Td[K], Su[K], Sd[K], Fdir[K];
+      V t[K], w[K], g0[K], Tn[K], Fin[K], Fdir[K];
+#pragma unroll
+      for (int p = 0; p < K; p++) props(cur, p, t[p], w[p], g0[p]);
+      if constexpr (kTn) {
+#pragma unroll
+        for (int p = 0; p < K; p++) Tn[p] = cur.tn[p];
+      } else {
+        V arg[K];
+#pragma unroll
+        for (int p = 0; p < K; p++) arg[p] = -t[p] * mu0_inv;
+        exp_beam_batch(arg, Tn, etab);
+      }
 #pragma unroll
       for (int p = 0; p < K; p++) {
-        f2 t, w, g0;
-        props(cur, p, t, w, g0);
-        const f2 Tn = kTn ? cur.tn[p] : exp2v_beam(-t * mu0_inv, etab);
-        const Coef2 cf = ck_two_stream<kG0>(t, w, g0, mu0, Tn, Fd3, etab);
-        Rd[p] = cf.Rdif;
-        Td[p] = cf.Tdif;
-        Su[p] = cf.Sup;
-        Sd[p] = cf.Sdn;
-        if (p < n) Fd3 = Tn * Fd3;
+        Fin[p] = Fd3;
+        Fd3 = (p < n) ? Tn[p] * Fd3 : Fd3;
         Fdir[p] = Fd3;  // the beam at the layer's bottom
       }
+      Coef2<V> cf[K];
+      ck_two_stream_k<kG0>(t, w, g0, mu0, Tn, Fin, cf, etab);
       // albedo / source at levels ck*K + p + 1 (A[p], S[p]), walked up from the checkpoint with pass 2's expressions;
       // D[p] = 1 / (1 - R_dif(p) * A[p]) is the adding denominator both walks use
-      f2 A[K], S[K], D[K];
+      V Al[K], S[K], D[K];
       {
-        f2 a = albE, s = srcE;
+        V a = cur.ae, s = cur.se;
 #pragma unroll
         for (int p = K - 1; p >= 0; p--) {
-          A[p] = a;
+          Al[p] = a;
           S[p] = s;
-          if (kCkKeepD) D[p] = splat(0.0f);
-          if (p < n) {
-            const f2 denom = rcp2(1.0f - Rd[p] * a);
-            if (kCkKeepD) D[p] = denom;
-            if (p > 0) {
-              const f2 an = Rd[p] + Td[p] * Td[p] * a * denom;
-              const f2 sn = Su[p] + Td[p] * denom * (s + a * Sd[p]);
-              a = an;
-              s = sn;
-            }
+          const V denom = rcp2(1.0f - cf[p].Rdif * a);
+          D[p] = denom;
+          if (p > 0) {
+            const V an = cf[p].Rdif + cf[p].Tdif * cf[p].Tdif * a * denom;
+            const V sn = cf[p].Sup + cf[p].Tdif * denom * (s + a * cf[p].Sdn);
+            a = (p < n) ? an : a;
+            s = (p < n) ? sn : s;
           }
         }
       }
       // fluxes down the chunk (adding :1583-1591, Eqs 12-13)
-      const int rbase = (ck * K) % R;
+      const int v = ck + ph, rbase = (v % M) * K;
 #pragma unroll
       for (int p = 0; p < K; p++) {
-        if (p < n) {
-          const f2 denom = kCkKeepD ? D[p] : rcp2(1.0f - Rd[p] * A[p]);
-          Fdn = (Td[p] * Fdn + Rd[p] * S[p] + Sd[p]) * denom;
-          const f2 up = Fdn * A[p] + S[p];
-          put(up, Fdn, Fdir[p], rbase + p, top + dl_dn * (ck * K + p + 1));
-        }
+        const V fdn = (cf[p].Tdif * Fdn + cf[p].Rdif * S[p] + cf[p].Sdn) * D[p];
+        Fdn = (p < n) ? fdn : Fdn;
+        put(fdn * Al[p] + S[p], fdn, Fdir[p], rbase + p, top + dl_dn * (ck * K + p + 1), p < n);
       }
-      if (rbase + K == R || ck == nck - 1) {
-        const int j0 = ck * K - rbase;  // first layer of this ring's levels
-        flush(min(R, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
+      if (valid && (v % M == M - 1 || ck == nck - 1)) {
+        const int cf = max(ck - v % M, 0);  // the ring's first chunk, its group and first layer
+        const int j0 = cf * K;
+        flush(min((ck + 1) * K, nlay) - j0, top + dl_dn * (j0 + 1), dl_dn, ((cf + ph) % M) * K);
       }
-      cur = nxt;
-      albE = albN;
-      srcE = srcN;
-    }
+    };
+    walk(load3, body3, nck, [](int i) { return i; }, A, B);
   }
 }
 
@@ -426,16 +517,16 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
 #ifndef RRTMGPNN_SWCK_NCB
 #define RRTMGPNN_SWCK_NCB 2
 #endif
-  const int ncb = RRTMGPNN_SWCK_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SWCK_NCB : 1;
-  const int threads = (ncb * (ngpt / 2) + 63) / 64 * 64;
+  const int ncb2 = RRTMGPNN_SWCK_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SWCK_NCB : 1;
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
-  const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
   const auto &ex = ctx->extras;
-  size_t lds = 0;
-  auto lds_for = [&](int ring) { return sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * ring * ngpt); };
-  auto go = [&](auto kern, const float *tb, const float *sb, const float *gb, int ring = kCkRing) -> int {
-    lds = lds_for(ring);
+  // npl g-points per lane, ncb columns per block
+  auto go = [&](auto kern, const float *tb, const float *sb, const float *gb, int ring = kCkRing, int npl = 2) -> int {
+    const int ncb = npl == 2 ? ncb2 : columns_per_block(ngpt);
+    const int threads = (ncb * (ngpt / npl) + 63) / 64 * 64;
+    const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
+    const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * ring * ck_ring_stride(ngpt) + 4);  // + spare
     if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: LDS ring exceeds 160 KiB");
     if (lds > 64 * 1024)
       if (int rc = raise_lds_limit((const void *)kern)) return rc;
@@ -459,8 +550,8 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
   if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
-    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall>, nullptr,
-              nullptr, nullptr, kCkRingSmall);
+    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall>,
+              nullptr, nullptr, nullptr, kCkRingSmall, RRTMGPNN_SWCK_NPL_SMALL);
   return go(sw_2stream_ck_kernel<false, false, kCkK>, nullptr, nullptr, nullptr);
 }
 

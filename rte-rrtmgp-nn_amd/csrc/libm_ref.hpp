@@ -152,6 +152,39 @@ __device__ __forceinline__ float ref_expf_neg(float x, const uint64_t *tab)
   return (x < -0x1.9fe368p6f) ? 0.0f : res;
 }
 
+// ref_expf_neg of M values with the M table reads issued back to back: the same operations per value, so the same bits,
+// but one LDS latency for the batch instead of one per exp (the compiler otherwise waits on each read as it is issued)
+template <int M>
+__device__ __forceinline__ void ref_expf_neg_batch(const float *x, float *y, const uint64_t *tab)
+{
+  const double InvLn2N = 0x1.71547652b82fep+0 * 32, SHIFT = 0x1.8p+52;
+  const double C0 = 0x1.c6af84b912394p-5 / 32 / 32 / 32, C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32,
+               C2 = 0x1.62e42ff0c52d6p-1 / 32;
+  double r[M];
+  uint64_t ki[M], t[M];
+#pragma unroll
+  for (int i = 0; i < M; i++) {
+    const double xd = (double)x[i];
+    double kd = __fma_rn(InvLn2N, xd, SHIFT);
+    ki[i] = f64_as_u64(kd);
+    kd -= SHIFT;
+    r[i] = __fma_rn(InvLn2N, xd, -kd);
+  }
+  __builtin_amdgcn_sched_barrier(0);  // the M table reads issue together (scheduled apart otherwise, each waited on)
+#pragma unroll
+  for (int i = 0; i < M; i++) t[i] = tab[ki[i] % 32];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int i = 0; i < M; i++) {
+    const double s = u64_as_f64(t[i] + (ki[i] << 47));
+    const double z = __fma_rn(C0, r[i], C1), r2 = r[i] * r[i];
+    double yy = __fma_rn(C2, r[i], 1.0);
+    yy = __fma_rn(z, r2, yy);
+    const float res = (float)(yy * s);
+    y[i] = (x[i] < -0x1.9fe368p6f) ? 0.0f : res;
+  }
+}
+
 // Copy the exp table into LDS (call with all threads of the block; a __syncthreads() must follow).
 __device__ __forceinline__ void load_exp_table(uint64_t *lds_tab)
 {

@@ -160,6 +160,27 @@ __device__ __forceinline__ void ring_flush(const float *ring, float *part, int n
   __syncthreads();
 }
 
+// ring_flush of one quantity (nq = 1, no dn_mode) for ngpt % 4 == 0 with one lane per partial: lane (s, j) walks
+// partial j of slot s (ring rows `stride` floats apart) and stores it to part[lev][j] -- the same partial sums as
+// ring_flush's float4 walk, in the same order, with a quarter of its instructions on the flushing wave.  With rows
+// padded to stride = ngpt + 4 the lanes' rows start in different LDS banks.
+__device__ __forceinline__ void ring_flush_lanes(const float *ring, int stride, float *part, int n, int lev0, int dl,
+                                                 int ngpt)
+{
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 4 * n) {
+    const int sl = t >> 2, j = t & 3;
+    const float *r = ring + (size_t)sl * stride + j;
+    const int n4 = ngpt >> 2;
+    float sum = 0.0f;
+#pragma unroll 8
+    for (int m = 0; m < n4; m++) sum = sum + r[4 * m];
+    part[(size_t)(lev0 + sl * dl) * 4 + j] = sum;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]) + p[2]) + p[3]; }
 
 // The SW solvers' flush for blocks that hold `ncb` columns: ring [ncb][3][R][ngpt] (up, dif, dir of column c at
@@ -168,17 +189,27 @@ __device__ __forceinline__ float combine4(const float *p) { return ((p[0] + p[1]
 // array: up, dn (= dif + dir, dn_mode) and dir.  Columns at or past ncol (the grid's last block) store nothing.
 // kTotal: the down slot already holds the total (diffuse + direct) g-point flux, as sw_solver_2stream forms it when it
 // saves g-point fluxes (:660-670): the down sum is s + total instead of (s + diffuse) + direct
+// stride: floats per ring row (ngpt, or ngpt padded so that the rows the flush threads walk together fall in different
+// LDS banks)
 template <int R, bool kTotal = false>
 __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n, int lev0, int dl, int ngpt, int nlev,
-                                              int icol0, int ncol, float *o_up, float *o_dn, float *o_dir)
+                                              int icol0, int ncol, float *o_up, float *o_dn, float *o_dir,
+                                              int stride = 0, int slot0 = 0)
 {
+#ifndef RRTMGPNN_ABL_FLUSH_NOBAR  // ablation builds only (timing; results are not produced)
   __syncthreads();
+#endif
   const int t = threadIdx.x;
+  const int rs = stride ? stride : ngpt;
+#ifdef RRTMGPNN_ABL_FLUSH_NOWORK
+  if (false) {
+#else
   if (t < 3 * ncb * n) {
+#endif
     const int c = t / (3 * n), rem = t - c * 3 * n, q = rem / n, s = rem - q * n;
-    const float *rc = ring + (size_t)c * 3 * R * ngpt;
-    const float *r = rc + ((size_t)q * R + s) * ngpt;
-    const float *r2 = rc + ((size_t)2 * R + s) * ngpt;
+    const float *rc = ring + (size_t)c * 3 * R * rs;
+    const float *r = rc + ((size_t)q * R + slot0 + s) * rs;
+    const float *r2 = rc + ((size_t)2 * R + slot0 + s) * rs;
     const bool dn = q == 1;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
     if ((ngpt & 3) == 0) {
@@ -205,6 +236,48 @@ __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n,
     if (icol < ncol) {
       float *o = q == 0 ? o_up : (q == 1 ? o_dn : o_dir);
       o[lev0 + s * dl + (size_t)nlev * icol] = ((s0 + s1) + s2) + s3;
+    }
+  }
+#ifndef RRTMGPNN_ABL_FLUSH_NOBAR
+  __syncthreads();
+#endif
+}
+
+// The same sums with one lane per partial (ngpt % 4 == 0): lane (q, c, s, j) walks partial j of quantity q, column c,
+// ring slot slot0 + s -- 4 words per step instead of a float4 per (q, c, s) -- and the four partials of a row are then
+// combined ((p0 + p1) + p2) + p3 by the row's lane j = 0 (partials fetched from lanes j = 1..3 of its quad).  Lanes
+// are ordered quantity-major, so with 64 lanes per (quantity) group a wave walks one quantity only: the down sums (two
+// adds per step) and the others do not share a wave's instruction stream.  Same partials, same additions, same order,
+// same bits as ring_flush_sw; about a quarter of its instructions on the critical wave.
+template <int R, bool kTotal = false>
+__device__ __forceinline__ void ring_flush_sw_lanes(const float *ring, int ncb, int n, int lev0, int dl, int ngpt,
+                                                    int nlev, int icol0, int ncol, float *o_up, float *o_dn,
+                                                    float *o_dir, int stride, int slot0 = 0)
+{
+  __syncthreads();
+  const int t = threadIdx.x;
+  const int per_q = ncb * n * 4;  // lanes per quantity
+  if (t < 3 * per_q) {  // idle lanes of the last wave walk nothing (the branch is per lane only in that wave)
+    const int q = t / per_q, rem = t - q * per_q, row = rem >> 2, j = rem & 3;
+    const int c = row / n, sl = row - c * n;
+    const float *rc = ring + (size_t)c * 3 * R * stride;
+    const float *r = rc + ((size_t)q * R + slot0 + sl) * stride + j;
+    const float *r2 = rc + ((size_t)2 * R + slot0 + sl) * stride + j;
+    const int n4 = ngpt >> 2;
+    float sum = 0.0f;
+    if (q == 1 && !kTotal) {
+#pragma unroll 8
+      for (int m = 0; m < n4; m++) sum = (sum + r[4 * m]) + r2[4 * m];
+    } else {
+#pragma unroll 8
+      for (int m = 0; m < n4; m++) sum = sum + r[4 * m];
+    }
+    // the quad's partials p0..p3 sit in lanes j = 0..3 of consecutive threads (per_q is a multiple of 4)
+    const float p1 = __shfl_down(sum, 1, 4), p2 = __shfl_down(sum, 2, 4), p3 = __shfl_down(sum, 3, 4);
+    const int icol = icol0 + c;
+    if (j == 0 && icol < ncol) {
+      float *o = q == 0 ? o_up : (q == 1 ? o_dn : o_dir);
+      o[lev0 + sl * dl + (size_t)nlev * icol] = ((sum + p1) + p2) + p3;
     }
   }
   __syncthreads();

@@ -10,9 +10,10 @@ namespace x2 {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 vmax(f2 a, f2 b) { return __builtin_elementwise_max(a, b); }
-__device__ __forceinline__ f2 vmin(f2 a, f2 b) { return __builtin_elementwise_min(a, b); }
+// vfma / vmax / vmin take f2 or float (the checkpointed kernel's one-g-point-per-lane instances)
+template <class V> __device__ __forceinline__ V vfma(V a, V b, V c) { return __builtin_elementwise_fma(a, b, c); }
+template <class V> __device__ __forceinline__ V vmax(V a, V b) { return __builtin_elementwise_max(a, b); }
+template <class V> __device__ __forceinline__ V vmin(V a, V b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ f2 splat(float x) { return (f2){x, x}; }
 
 // x <= 0 everywhere it is called (exp of -tau*k and -tau/mu0)
@@ -62,6 +63,48 @@ __device__ __forceinline__ f2 div2(f2 a, f2 b)
 #endif
 }
 
+// The same helpers for one g-point per lane: the scalar functions they pair (same bits element by element)
+__device__ __forceinline__ float exp2v(float x, const uint64_t *etab) { return solver_exp_neg(x, etab); }
+__device__ __forceinline__ float exp2v_beam(float x, const uint64_t *etab) { return solver_exp_beam(x, etab); }
+__device__ __forceinline__ float sqrt2(float x) { return sqrt_rn_normal(x); }
+__device__ __forceinline__ float rcp2(float b) { return rcp_rn_normal(b); }
+__device__ __forceinline__ float div2(float a, float b) { return solver_div(a, b); }
+
+// exps of N lane values (f2 or float) with the table reads batched (ref_expf_neg_batch); exp_neg_batch follows
+// solver_exp_neg (the tolerance build keeps its per-element hardware exp), exp_beam_batch solver_exp_beam
+template <int N, class V>
+__device__ __forceinline__ void exp_neg_batch(const V (&x)[N], V (&y)[N], const uint64_t *etab)
+{
+#if RRTMGPNN_FASTOPS && !RRTMGPNN_FAST_LIBM
+  constexpr int L = sizeof(V) / sizeof(float);
+  float xs[N * L], ys[N * L];
+#pragma unroll
+  for (int i = 0; i < N; i++) __builtin_memcpy(&xs[i * L], &x[i], sizeof(V));
+  ref_expf_neg_batch<N * L>(xs, ys, etab);
+#pragma unroll
+  for (int i = 0; i < N; i++) __builtin_memcpy(&y[i], &ys[i * L], sizeof(V));
+#else
+#pragma unroll
+  for (int i = 0; i < N; i++) y[i] = exp2v(x[i], etab);
+#endif
+}
+template <int N, class V>
+__device__ __forceinline__ void exp_beam_batch(const V (&x)[N], V (&y)[N], const uint64_t *etab)
+{
+#if RRTMGPNN_FASTOPS || RRTMGPNN_FAST_LIBM
+  constexpr int L = sizeof(V) / sizeof(float);
+  float xs[N * L], ys[N * L];
+#pragma unroll
+  for (int i = 0; i < N; i++) __builtin_memcpy(&xs[i * L], &x[i], sizeof(V));
+  ref_expf_neg_batch<N * L>(xs, ys, etab);
+#pragma unroll
+  for (int i = 0; i < N; i++) __builtin_memcpy(&y[i], &ys[i * L], sizeof(V));
+#else
+#pragma unroll
+  for (int i = 0; i < N; i++) y[i] = exp2v_beam(x[i], etab);
+#endif
+}
+
 // 8-byte column-local loads and stores (g-point pair at byte offset voff, layer at soff)
 struct ColArr2 {
   __amdgpu_buffer_rsrc_t r;
@@ -79,6 +122,22 @@ struct ColArr2 {
   {
     typedef unsigned int u2 __attribute__((ext_vector_type(2)));
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, voff, soff, 0);
+  }
+};
+
+// column-local loads and stores of one lane's g-points: V = f2 (8 bytes, ColArr2) or float (4 bytes)
+template <class V>
+struct ColArrV : ColArr2 {
+  __device__ __forceinline__ ColArrV(const float *base, size_t col_off, uint32_t bytes) : ColArr2(base, col_off, bytes) {}
+  __device__ __forceinline__ V ldv(uint32_t voff, uint32_t soff) const
+  {
+    if constexpr (sizeof(V) == 8) return ld(voff, soff);
+    else return ld1(voff, soff);
+  }
+  __device__ __forceinline__ void stv(V v, uint32_t voff, uint32_t soff) const
+  {
+    if constexpr (sizeof(V) == 8) st(v, voff, soff);
+    else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
   }
 };
 
