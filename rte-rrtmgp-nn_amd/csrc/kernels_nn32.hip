@@ -426,7 +426,12 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
           const uint32_t off = vo[r] + 128u * go;
           o0.st(tot, off);
           o1.st(ssa, off);
-          o2.st(0.0f, off);
+        }
+        // g = 0 only when the caller asked for the array (the fused step and the class layer's NN path pass none):
+        // one uniform branch per g-tile instead of a dropped store per element
+        if (a.out2) {
+#pragma unroll
+          for (int r = 0; r < 16; r++) o2.st(0.0f, vo[r] + 128u * go);
         }
       } else if constexpr (kPair) {
         const float bB = iB[LB.b3 + g];

@@ -99,11 +99,6 @@ __device__ __forceinline__ void ck_inc(V &t1, V &w1, V &g1, V t2, V w2, V g2)
 #define RRTMGPNN_SWCK_FLUSH_LANES 1
 #endif
 constexpr bool kCkFlushLanes = RRTMGPNN_SWCK_FLUSH_LANES != 0;
-// stagger the blocks' flushes (see pass 3)
-#ifndef RRTMGPNN_SWCK_FLUSH_PHASE
-#define RRTMGPNN_SWCK_FLUSH_PHASE 1
-#endif
-constexpr bool kCkFlushPhase = RRTMGPNN_SWCK_FLUSH_PHASE != 0;
 // floats per row of the flux ring (RRTMGPNN_SWCK_RING_PAD: 4, or 0 for unpadded rows)
 #ifndef RRTMGPNN_SWCK_RING_PAD
 #define RRTMGPNN_SWCK_RING_PAD 4
@@ -211,6 +206,7 @@ __global__ void __launch_bounds__(512, WAVES)
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   load_exp_table(etab);
   __syncthreads();
+  const int dl_dn = top_at_1 ? 1 : -1;
   const uint32_t row = 4u * (uint32_t)ngpt;
   const uint32_t vL = 4u * (uint32_t)gc + (uint32_t)c * row * nlay;
   const size_t cl = (size_t)ngpt * nlay * icol0;
@@ -417,13 +413,8 @@ __global__ void __launch_bounds__(512, WAVES)
       ring_flush_sw<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
                              flux_dir, rs, slot0);
   };
-  // The ring holds M chunks; a block flushes it when its last group fills.  Blocks resident together run in near
-  // lockstep, and the flush (a barrier, then one wave walking the ordered sums) would stall them all at once: with
-  // kCkFlushPhase, a block's chunks are offset by `ph` groups (its first flush comes after M - ph chunks), so the blocks
-  // sharing a CU flush at different chunks and the others compute meanwhile.
+  // the ring holds M = R / K chunks; the block flushes it when it is full (a barrier, the ordered sums, a barrier)
   constexpr int M = R / K;
-  const int ph = kCkFlushPhase ? (int)(((blockIdx.x >> 3) ^ (blockIdx.x >> 8)) % M) : 0;
-  const int dl_dn = top_at_1 ? 1 : -1;
   V Fdn = inc_dif ? ld_col(inc_dif) : (V)0.0f;
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top, true);
   flush(1, top, 1);
@@ -474,17 +465,16 @@ __global__ void __launch_bounds__(512, WAVES)
         }
       }
       // fluxes down the chunk (adding :1583-1591, Eqs 12-13)
-      const int v = ck + ph, rbase = (v % M) * K;
+      const int rbase = (ck % M) * K;
 #pragma unroll
       for (int p = 0; p < K; p++) {
         const V fdn = (cf[p].Tdif * Fdn + cf[p].Rdif * S[p] + cf[p].Sdn) * D[p];
         Fdn = (p < n) ? fdn : Fdn;
         put(fdn * Al[p] + S[p], fdn, Fdir[p], rbase + p, top + dl_dn * (ck * K + p + 1), p < n);
       }
-      if (valid && (v % M == M - 1 || ck == nck - 1)) {
-        const int cf = max(ck - v % M, 0);  // the ring's first chunk, its group and first layer
-        const int j0 = cf * K;
-        flush(min((ck + 1) * K, nlay) - j0, top + dl_dn * (j0 + 1), dl_dn, ((cf + ph) % M) * K);
+      if (valid && (rbase + K == R || ck == nck - 1)) {
+        const int j0 = ck * K - rbase;  // first layer of this ring's levels
+        flush(min(R, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     };
     walk(load3, body3, nck, [](int i) { return i; }, A, B);
