@@ -41,10 +41,12 @@ __device__ __forceinline__ f2 ck_eps_guard(f2 v, float eps) { return (f2){ck_eps
 
 // sw_two_stream (kernels_rte.hip) term by term for the K layers of a chunk, with the direct-beam transmittances
 // Tnoscat = exp(-tau/mu0) given, stage by stage so that the K layers' exps share one batch of table reads
-template <bool kG0, int K, class V>
+// kEmk: 0 forms exp(-tau k); 1 forms it and hands it out in emk_io; 2 takes it from emk_io (the value mode 1 handed
+// out for the same layer, same bits)
+template <bool kG0, int K, class V, int kEmk = 0>
 __device__ __forceinline__ void ck_two_stream_k(const V (&tau)[K], const V (&w0)[K], const V (&g)[K], float mu0,
                                                 const V (&Tnoscat)[K], const V (&dir_inc)[K], Coef2<V> (&c)[K],
-                                                const uint64_t *etab)
+                                                const uint64_t *etab, V (&emk_io)[K])
 {
   const float eps = FLT_EPSILON, k_min = 1.e-4f;
   V gamma1[K], gamma2[K], k[K], arg[K], emk[K];
@@ -55,7 +57,16 @@ __device__ __forceinline__ void ck_two_stream_k(const V (&tau)[K], const V (&w0)
     k[p] = sqrt2(vmax((gamma1[p] - gamma2[p]) * (gamma1[p] + gamma2[p]), (V)k_min));
     arg[p] = -tau[p] * k[p];
   }
-  exp_neg_batch(arg, emk, etab);
+  if constexpr (kEmk == 2) {
+#pragma unroll
+    for (int p = 0; p < K; p++) emk[p] = emk_io[p];
+  } else {
+    exp_neg_batch(arg, emk, etab);
+    if constexpr (kEmk == 1) {
+#pragma unroll
+      for (int p = 0; p < K; p++) emk_io[p] = emk[p];
+    }
+  }
 #pragma unroll
   for (int p = 0; p < K; p++) {
     const V em2k = emk[p] * emk[p];
@@ -166,6 +177,12 @@ constexpr bool kCkTnSmall = RRTMGPNN_SWCK_TN_SMALL != 0;
 #define RRTMGPNN_SWCK_NPL_SMALL 2
 #endif
 using VSmall = std::conditional_t<RRTMGPNN_SWCK_NPL_SMALL == 1, float, f2>;
+// the small-grid instance keeps pass 2's exp(-tau k) in a workspace plane that pass 3 reads (C3: SW solver -3.7 %,
+// step -3.7 %, alternating A/B on one box)
+#ifndef RRTMGPNN_SWCK_EMK_SMALL
+#define RRTMGPNN_SWCK_EMK_SMALL 1
+#endif
+constexpr bool kCkEmkSmall = RRTMGPNN_SWCK_EMK_SMALL != 0;
 // the same for the all-sky instances (fused cloud increment), whatever the grid
 #ifndef RRTMGPNN_SWCK_TN_INC
 #define RRTMGPNN_SWCK_TN_INC 0
@@ -175,7 +192,7 @@ constexpr bool kCkTnInc = RRTMGPNN_SWCK_TN_INC != 0;
 // V: f2 (two g-points per lane) or float (one per lane)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES, bool kTn = false,
-          class V = f2>
+          class V = f2, bool kEmk = false>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -218,8 +235,12 @@ __global__ void __launch_bounds__(512, WAVES)
   const CA_ CB(ws, (size_t)ngpt * nck * icol0, (uint32_t)nc * row * nck);
   const CA_ CA(ws + pB, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
   const CA_ CS(ws + pB + pA, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
-  // kTn: the beam transmittances (ngpt, nlay, ncol), addressed as tau
+  // kTn: the beam transmittances (ngpt, nlay, ncol), addressed as tau.  kEmk: pass 2's exp(-tau k) in the plane after
+  // it, which pass 3 reads instead of evaluating the exp again.  (Keeping all four coefficients R_dif, T_dif, S_up, S_dn
+  // instead, so that pass 3 forms none, was 23 % slower at C3: four planes written and read cost more than they save.)
+  const size_t plane = (size_t)ngpt * nlay * ncol;
   const CA_ CT(kTn ? ws + pB + 2 * pA : ws, kTn ? cl : 0, kTn ? bL : 0u);
+  const CA_ CE(kEmk ? ws + pB + 2 * pA + (kTn ? plane : 0) : ws, kEmk ? cl : 0, kEmk ? bL : 0u);
   const uint32_t vBs = on ? vB : kBufOOB, vAs = on ? vA : kBufOOB;
   // band-resolved increments: one band offset per g-point of the lane
   const size_t cb = (size_t)bands.nbnd * nlay * icol0;
@@ -245,7 +266,7 @@ __global__ void __launch_bounds__(512, WAVES)
   // checkpoints the pass reads for it: fb the beam at the chunk's top (pass 2), ae / se the albedo and source at its
   // bottom (pass 3)
   struct Chunk {
-    V t[K], w[K], g[K], qt[K], qw[K], qg[K], tn[K], fb, ae, se;
+    V t[K], w[K], g[K], qt[K], qw[K], qg[K], tn[K], em[K], fb, ae, se;
   };
   // pass: 2 or 3
   auto load_chunk = [&](Chunk &ch, int ck, int pass) {
@@ -255,6 +276,7 @@ __global__ void __launch_bounds__(512, WAVES)
       const uint32_t s = row * (uint32_t)l;
       ch.t[p] = Ttau.ldv(vL, s);
       ch.tn[p] = kTn ? CT.ldv(vL, s) : (V)0.0f;
+      ch.em[p] = (kEmk && pass == 3) ? CE.ldv(vL, s) : (V)0.0f;
       ch.w[p] = Tssa.ldv(vL, s);
       ch.g[p] = kHasG ? Tg.ldv(vL, s) : (V)0.0f;
       if constexpr (kInc) {
@@ -366,7 +388,12 @@ __global__ void __launch_bounds__(512, WAVES)
       // the chunk's coefficients (layers past nlay in the last chunk see the clamped last layer and are not used),
       // then the adding recurrence
       Coef2<V> cf[K];
-      ck_two_stream_k<kG0>(t, w, g0, mu0, Tn, Fin, cf, etab);
+      V em[K];
+      ck_two_stream_k<kG0, K, V, kEmk ? 1 : 0>(t, w, g0, mu0, Tn, Fin, cf, etab, em);
+      if constexpr (kEmk) {
+#pragma unroll
+        for (int p = 0; p < K; p++) CE.stv(em[p], (on && p < n) ? vL : kBufOOB, row * (uint32_t)lay(ck * K + p));
+      }
 #pragma unroll
       for (int p = K - 1; p >= 0; p--) {
         const V denom = rcp2(1.0f - cf[p].Rdif * alb_b);
@@ -444,7 +471,7 @@ __global__ void __launch_bounds__(512, WAVES)
         Fdir[p] = Fd3;  // the beam at the layer's bottom
       }
       Coef2<V> cf[K];
-      ck_two_stream_k<kG0>(t, w, g0, mu0, Tn, Fin, cf, etab);
+      ck_two_stream_k<kG0, K, V, kEmk ? 2 : 0>(t, w, g0, mu0, Tn, Fin, cf, etab, cur.em);
       // albedo / source at levels ck*K + p + 1 (A[p], S[p]), walked up from the checkpoint with pass 2's expressions;
       // D[p] = 1 / (1 - R_dif(p) * A[p]) is the adding denominator both walks use
       V Al[K], S[K], D[K];
@@ -491,7 +518,8 @@ bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bo
 // instance; small: plus the small-grid instance's plane of beam transmittances)
 size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc)
 {
-  const size_t tn = (small && kCkTnSmall) || (inc && kCkTnInc) ? (size_t)ngpt * nlay * ncol : 0;
+  const size_t tn = ((small && kCkTnSmall) || (inc && kCkTnInc) ? (size_t)ngpt * nlay * ncol : 0) +
+                    (small && kCkEmkSmall ? (size_t)ngpt * nlay * ncol : 0);
   const int k = std::min(kCkK, kCkKSmall);
   const size_t nck = (size_t)(nlay + k - 1) / k;
   return (size_t)ngpt * ncol * (nck + 2 * (nck + 1)) + tn;
@@ -540,7 +568,8 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
   if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
-    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall>,
+    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
+                                   kCkEmkSmall>,
               nullptr, nullptr, nullptr, kCkRingSmall, RRTMGPNN_SWCK_NPL_SMALL);
   return go(sw_2stream_ck_kernel<false, false, kCkK>, nullptr, nullptr, nullptr);
 }
