@@ -49,7 +49,6 @@ def parse():
                          "without a value the config's global size: C5 1e6 columns); default: N x the config's block")
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
-    ap.add_argument("--sw-after", default="", help="start the SW chain after this LW-chain call (e.g. predict_nn_lw)")
     ap.add_argument("--lw-after", default="", help="start the LW chain after this SW-chain call (e.g. predict_nn_sw; none: chains start together; default: the library pipeline's choice)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
@@ -223,17 +222,15 @@ def main():
     if args.sw_kernel:
         from rrtmgpnn import api
         api.set_sw_kernel_default(args.sw_kernel)
-    if args.lw_after:
-        os.environ["RRTMGPNN_LW_AFTER"] = args.lw_after
-    if args.sw_after:
-        os.environ["RRTMGPNN_SW_AFTER"] = args.sw_after
+    lw_after = None if not args.lw_after else ("" if args.lw_after == "none" else args.lw_after)
     use_graph = not args.no_graph
     # the rank's columns in chunks of at most one block (pipeline.ChunkedRank): with more than one chunk every chunk's
     # inputs are resident in HBM and copied into the step's buffers before its replay, its fluxes copied into the
     # rank's slab after it (device to device, inside the timed region); tests/test_gpu_chunked.py checks the slab
     rank_run = ChunkedRank(lo, hi, block, problem,
                            lambda p, c: ClearSkyStep(p, device=local, fused=not args.unfused, clouds=c,
-                                                     overlap=not args.no_overlap, sw=args.config not in ("c1", "c2")),
+                                                     overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
+                                                     lw_after=lw_after),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first
@@ -420,8 +417,7 @@ def main():
                        "parallelism": "column-sharded (shard.column_range), 1 process per GPU",
                        "launch": ("hipGraph replay" if use_graph else "eager") +
                                  (", LW and SW chains on two streams" if step.overlap else "") +
-                                 (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
-                                 (", the SW chain after %s" % step.sw_after if step.sw_after else ""),
+                                 (", the LW chain after %s" % step.lw_after if step.lw_after else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
                                    "fused Planck-in-LW-solver, g=0 elided" +
                                    (", cloud increments fused into both solvers" if step.allsky else ""))},

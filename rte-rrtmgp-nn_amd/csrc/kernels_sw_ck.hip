@@ -106,44 +106,24 @@ __device__ __forceinline__ void ck_inc(V &t1, V &w1, V &g1, V t2, V w2, V g2)
 }
 
 // the flush walks the ordered sums one lane per partial (ring_flush_sw_lanes) when the block has the lanes for it
-#ifndef RRTMGPNN_SWCK_FLUSH_LANES
-#define RRTMGPNN_SWCK_FLUSH_LANES 1
-#endif
-constexpr bool kCkFlushLanes = RRTMGPNN_SWCK_FLUSH_LANES != 0;
-// floats per row of the flux ring (RRTMGPNN_SWCK_RING_PAD: 4, or 0 for unpadded rows)
-#ifndef RRTMGPNN_SWCK_RING_PAD
-#define RRTMGPNN_SWCK_RING_PAD 4
-#endif
-__host__ __device__ constexpr int ck_ring_stride(int ngpt) { return ngpt + RRTMGPNN_SWCK_RING_PAD; }
+// (C3 flush 18 us from 31 us with one lane per column); flux-ring rows are padded by 4 floats, so the lanes of one
+// partial read different banks
+constexpr bool kCkFlushLanes = true;
+__host__ __device__ constexpr int ck_ring_stride(int ngpt) { return ngpt + 4; }
 
 }  // namespace
 
-// K: layers per chunk (checkpoint spacing); RING: levels staged for the ordered broadband sums (a multiple of K)
-#ifndef RRTMGPNN_SWCK_K
-#define RRTMGPNN_SWCK_K 3
-#endif
-#ifndef RRTMGPNN_SWCK_RING
-#define RRTMGPNN_SWCK_RING 6
-#endif
+// K: layers per chunk (checkpoint spacing); kCkRing: levels staged for the ordered broadband sums (a multiple of K).
 // K = 3 layers per chunk under a 3-waves-per-SIMD register budget (132 VGPRs, no spill; at 4 waves K = 3 spilled and
 // K = 2 fit): C3 step -3 %, C4 -1 % against K = 2 or the two-per-lane workspace kernel; K = 4 (148 VGPRs) was best
 // alone at C3 but 13 % slower at C4, K = 6 spilled (tools/gpu_ab.sh, round 2)
-#ifndef RRTMGPNN_SWCK_WAVES
-#define RRTMGPNN_SWCK_WAVES 3
-#endif
+constexpr int kCkK = 3, kCkRing = 6, kCkWaves = 3;
 // pass 1 loads kCkP1 chunks of optical depths per step (and the next step's while it computes)
-#ifndef RRTMGPNN_SWCK_P1
-#define RRTMGPNN_SWCK_P1 2
-#endif
-constexpr int kCkP1 = RRTMGPNN_SWCK_P1;
-constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
-
+constexpr int kCkP1 = 2;
 // Waves per SIMD of the clear-sky NN instance (g = NULL, no increment), which needs fewer registers: at 4 (128 VGPRs,
 // 2 spilled) the C3 grid (900 blocks of 4 waves) is resident at once instead of 768 + a second round of 132; SW solver
 // -2.5 % at C3, step -0.7 %, C5 shard equal (tools/gpu_ab.sh, round 2)
-#ifndef RRTMGPNN_SWCK_WAVES_NN
-#define RRTMGPNN_SWCK_WAVES_NN 4
-#endif
+constexpr int kCkWavesNN = 4;
 
 // kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
 // broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
@@ -151,47 +131,18 @@ constexpr int kCkK = RRTMGPNN_SWCK_K, kCkRing = RRTMGPNN_SWCK_RING;
 // chunk at 2 waves per SIMD (more independent layers per wave where there are too few waves to hide the exps'
 // latency), ring of 8 levels.  Whole-step A/B at C3 (one box, alternating): +1.3 %, SW solver -2.4 %; a ring of 4 was
 // 3 % slower, K = 2 at 4 waves +0.5 %.  With many columns (C4, C5) K = 3 at 3-4 waves stays (K = 4 was 13 % slower).
-#ifndef RRTMGPNN_SWCK_SMALL
-#define RRTMGPNN_SWCK_SMALL 1
-#endif
-#ifndef RRTMGPNN_SWCK_K_SMALL
-#define RRTMGPNN_SWCK_K_SMALL 4
-#endif
-#ifndef RRTMGPNN_SWCK_RING_SMALL
-#define RRTMGPNN_SWCK_RING_SMALL 8
-#endif
-#ifndef RRTMGPNN_SWCK_WAVES_SMALL
-#define RRTMGPNN_SWCK_WAVES_SMALL 2
-#endif
-constexpr int kCkKSmall = RRTMGPNN_SWCK_K_SMALL, kCkRingSmall = RRTMGPNN_SWCK_RING_SMALL,
-              kCkWavesSmall = RRTMGPNN_SWCK_WAVES_SMALL;
-// the small-grid instance keeps pass 1's beam transmittances exp(-tau/mu0) in a workspace plane and passes 2 and 3 read
-// them (one more plane written and two read) instead of evaluating the exp again
-#ifndef RRTMGPNN_SWCK_TN_SMALL
-#define RRTMGPNN_SWCK_TN_SMALL 1
-#endif
-constexpr bool kCkTnSmall = RRTMGPNN_SWCK_TN_SMALL != 0;
-// g-points per lane of the small-grid instance: 1 doubles the waves the grid has to hide latency with (packed fp32
-// issues at the same cost per element as scalar fp32 on gfx950, tools/valu_rates.hip)
-#ifndef RRTMGPNN_SWCK_NPL_SMALL
-#define RRTMGPNN_SWCK_NPL_SMALL 2
-#endif
-using VSmall = std::conditional_t<RRTMGPNN_SWCK_NPL_SMALL == 1, float, f2>;
-// the small-grid instance keeps pass 2's exp(-tau k) in a workspace plane that pass 3 reads (C3: SW solver -3.7 %,
-// step -3.7 %, alternating A/B on one box)
-#ifndef RRTMGPNN_SWCK_EMK_SMALL
-#define RRTMGPNN_SWCK_EMK_SMALL 1
-#endif
-constexpr bool kCkEmkSmall = RRTMGPNN_SWCK_EMK_SMALL != 0;
-// the same for the all-sky instances (fused cloud increment), whatever the grid
-#ifndef RRTMGPNN_SWCK_TN_INC
-#define RRTMGPNN_SWCK_TN_INC 0
-#endif
-constexpr bool kCkTnInc = RRTMGPNN_SWCK_TN_INC != 0;
+// The small-grid instance also keeps pass 1's beam transmittances exp(-tau/mu0) in a workspace plane that passes 2 and
+// 3 read instead of evaluating the exp again, and pass 2's exp(-tau k) in a second plane that pass 3 reads (C3: SW
+// solver -3.7 %, step -3.7 %, alternating A/B on one box).  One g-point per lane (twice the waves to hide latency with;
+// packed fp32 issues at the same cost per element as scalar fp32 on gfx950, tools/valu_rates.hip) measured slower than
+// two, and so did the transmittance plane in the all-sky (fused-increment) instances.
+constexpr int kCkKSmall = 4, kCkRingSmall = 8, kCkWavesSmall = 2;
+constexpr bool kCkTnSmall = true, kCkEmkSmall = true;
+using VSmall = f2;
 
 // V: f2 (two g-points per lane) or float (one per lane)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
-          int WAVES = (!kHasG && !kInc && !kGpt) ? RRTMGPNN_SWCK_WAVES_NN : RRTMGPNN_SWCK_WAVES, bool kTn = false,
+          int WAVES = (!kHasG && !kInc && !kGpt) ? kCkWavesNN : kCkWaves, bool kTn = false,
           class V = f2, bool kEmk = false>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
@@ -511,14 +462,14 @@ __global__ void __launch_bounds__(512, WAVES)
 bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bool inc, bool gpt)
 {
   // 2 g-points per lane; one round of 16 waves of 64 lanes per CU
-  return RRTMGPNN_SWCK_SMALL && !has_g && !inc && !gpt && (long long)ncol * (ngpt / 2) <= 64LL * 16 * ctx->num_cus;
+  return !has_g && !inc && !gpt && (long long)ncol * (ngpt / 2) <= 64LL * 16 * ctx->num_cus;
 }
 
 // workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either
 // instance; small: plus the small-grid instance's plane of beam transmittances)
 size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc)
 {
-  const size_t tn = ((small && kCkTnSmall) || (inc && kCkTnInc) ? (size_t)ngpt * nlay * ncol : 0) +
+  const size_t tn = (small && kCkTnSmall ? (size_t)ngpt * nlay * ncol : 0) +
                     (small && kCkEmkSmall ? (size_t)ngpt * nlay * ncol : 0);
   const int k = std::min(kCkK, kCkKSmall);
   const size_t nck = (size_t)(nlay + k - 1) / k;
@@ -532,10 +483,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
                          float *flux_dn, float *flux_dir)
 {
-#ifndef RRTMGPNN_SWCK_NCB
-#define RRTMGPNN_SWCK_NCB 2
-#endif
-  const int ncb2 = RRTMGPNN_SWCK_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SWCK_NCB : 1;
+  const int ncb2 = 2 * (ngpt / 2) <= 512 ? 2 : 1;  // two columns per block where 512 lanes hold them
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
   const auto &ex = ctx->extras;
@@ -561,16 +509,15 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     if (g) return go(sw_2stream_ck_kernel<true, false, kCkK, true>, nullptr, nullptr, nullptr);
     return go(sw_2stream_ck_kernel<false, false, kCkK, true>, nullptr, nullptr, nullptr);
   }
-  constexpr int kW = RRTMGPNN_SWCK_WAVES;
-  if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, kW, kCkTnInc>, tau_bnd, ssa_bnd, g_bnd);
-  if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, kW, kCkTnInc>, tau_bnd, ssa_bnd, g_bnd);
+  if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
+  if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
   if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
     return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
                                    kCkEmkSmall>,
-              nullptr, nullptr, nullptr, kCkRingSmall, RRTMGPNN_SWCK_NPL_SMALL);
+              nullptr, nullptr, nullptr, kCkRingSmall, 2);
   return go(sw_2stream_ck_kernel<false, false, kCkK>, nullptr, nullptr, nullptr);
 }
 

@@ -102,6 +102,7 @@ static void *pin_slice(rrtmgpnn_context *c, size_t bytes)
       c->pin = nullptr;
       c->pin_cap = 0;
       size_t cap = std::max(kPinMin, 2 * b);
+      // default flags: non-coherent and coherent allocations measured the same in the Fortran block loop
       if (hipHostMalloc(&c->pin, cap, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         c->pin = nullptr;

@@ -53,7 +53,7 @@ contains
     integer(c_int), allocatable :: lims(:,:)
     type(c_ptr) :: d_tau, d_ssa, d_g, d_lay, d_lev, d_sfc, d_jac, d_emis, d_emis_gpt, d_inc, d_up, d_dn
     type(c_ptr) :: d_ds, d_gup, d_gdn
-    logical :: two_str, use_2s, src_tmp, g_tmp, gpt
+    logical :: two_str, use_2s, src_tmp, g_tmp, gpt, du, dd
     real(wp), allocatable :: up(:,:), dn(:,:)
 
     ncol  = optical_props%get_ncol()
@@ -70,15 +70,19 @@ contains
     if (any(shape(sfc_emis) /= [nband, ncol])) then
       error_msg = "rte_lw: sfc_emis inconsistently sized"; return
     end if
-    if (check_values .and. any(sfc_emis < 0._wp .or. sfc_emis > 1._wp)) then
-      error_msg = "rte_lw: sfc_emis has values < 0 or > 1"; return
+    if (check_values) then
+      if (any(sfc_emis < 0._wp .or. sfc_emis > 1._wp)) then
+        error_msg = "rte_lw: sfc_emis has values < 0 or > 1"; return
+      end if
     end if
     if (present(inc_flux)) then
       if (any(shape(inc_flux) /= [ngpt, ncol])) then
         error_msg = "rte_lw: inc_flux inconsistently sized"; return
       end if
-      if (check_values .and. any(inc_flux < 0._wp)) then
-        error_msg = "rte_lw: inc_flux has values < 0"; return
+      if (check_values) then
+        if (any(inc_flux < 0._wp)) then
+          error_msg = "rte_lw: inc_flux has values < 0"; return
+        end if
       end if
     end if
     nmus = 1
@@ -211,10 +215,24 @@ contains
       end if
       if (g_tmp) call dev_release(d_g)
     end if
+    ! broadband fluxes go straight into the caller's arrays when they are contiguous (and no net flux is wanted from
+    ! them); otherwise into temporaries copied after the sync
+    du = .false.; dd = .false.
+    if (.not. associated(fluxes%flux_net)) then
+      du = direct_ok(fluxes%flux_up, nv); dd = direct_ok(fluxes%flux_dn, nv)
+    end if
     allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol))
     if (error_msg == '') then
-      call dev_copy_out(up, d_up, nv)
-      call dev_copy_out(dn, d_dn, nv)
+      if (du) then
+        call dev_copy_out(fluxes%flux_up, d_up, nv)
+      else
+        call dev_copy_out(up, d_up, nv)
+      end if
+      if (dd) then
+        call dev_copy_out(fluxes%flux_dn, d_dn, nv)
+      else
+        call dev_copy_out(dn, d_dn, nv)
+      end if
       if (gpt) then
         if (associated(fluxes%gpt_flux_up)) call dev_copy_out(fluxes%gpt_flux_up, d_gup, ngv)
         if (associated(fluxes%gpt_flux_dn)) call dev_copy_out(fluxes%gpt_flux_dn, d_gdn, ngv)
@@ -222,12 +240,20 @@ contains
     end if
     call rrtmgpnn_sync(error_msg, "rte_lw")
     if (error_msg == '') then
-      if (associated(fluxes%flux_up)) fluxes%flux_up = up
-      if (associated(fluxes%flux_dn)) fluxes%flux_dn = dn
+      if (associated(fluxes%flux_up) .and. .not. du) fluxes%flux_up = up
+      if (associated(fluxes%flux_dn) .and. .not. dd) fluxes%flux_dn = dn
       if (associated(fluxes%flux_net)) fluxes%flux_net = dn - up
     end if
     call dev_release(d_emis); call dev_release(d_emis_gpt); call dev_release(d_inc)
     call dev_release(d_up); call dev_release(d_dn)
     call dev_release(d_ds); call dev_release(d_gup); call dev_release(d_gdn)
   end function rte_lw
+
+  ! whether the device fluxes can be copied into f itself: associated, contiguous and n elements
+  logical function direct_ok(f, n)
+    real(wp), dimension(:,:), pointer, intent(in) :: f
+    integer(c_long_long), intent(in) :: n
+    direct_ok = .false.
+    if (associated(f)) direct_ok = is_contiguous(f) .and. size(f, kind=c_long_long) == n
+  end function direct_ok
 end module mo_rte_lw

@@ -31,7 +31,7 @@ contains
     integer(c_long_long) :: ng, nv, nsfc, ngv
     type(c_ptr) :: d_tau, d_ssa, d_g, d_mu0, d_inc, d_dif, d_adir, d_adif, d_up, d_dn, d_dir, d_gup, d_gdn, d_gdir
     real(wp), allocatable :: up(:,:), dn(:,:), dir(:,:)
-    logical :: two_str, gpt
+    logical :: two_str, gpt, du, dd, dr
 
     ncol = atmos%get_ncol()
     nlay = atmos%get_nlay()
@@ -58,34 +58,44 @@ contains
     if (size(mu0) /= ncol) then
       error_msg = "rte_sw: mu0 inconsistently sized"; return
     end if
-    if (check_values .and. any(mu0 < 0._wp .or. mu0 > 1._wp)) then
-      error_msg = "rte_sw: one or more mu0 <= 0 or > 1"; return
+    if (check_values) then
+      if (any(mu0 < 0._wp .or. mu0 > 1._wp)) then
+        error_msg = "rte_sw: one or more mu0 <= 0 or > 1"; return
+      end if
     end if
     if (any(shape(inc_flux) /= [ngpt, ncol])) then
       error_msg = "rte_sw: inc_flux inconsistently sized"; return
     end if
-    if (check_values .and. any(inc_flux < 0._wp)) then
-      error_msg = "rte_sw: one or more inc_flux < 0"; return
+    if (check_values) then
+      if (any(inc_flux < 0._wp)) then
+        error_msg = "rte_sw: one or more inc_flux < 0"; return
+      end if
     end if
     if (present(inc_flux_dif)) then
       if (any(shape(inc_flux_dif) /= [ngpt, ncol])) then
         error_msg = "rte_sw: inc_flux_dif inconsistently sized"; return
       end if
-      if (check_values .and. any(inc_flux_dif < 0._wp)) then
-        error_msg = "rte_sw: one or more inc_flux_dif < 0"; return
+      if (check_values) then
+        if (any(inc_flux_dif < 0._wp)) then
+          error_msg = "rte_sw: one or more inc_flux_dif < 0"; return
+        end if
       end if
     end if
     if (any(shape(sfc_alb_dir_gpt) /= [ngpt, ncol])) then
       error_msg = "rte_sw: sfc_alb_dir inconsistently sized"; return
     end if
-    if (check_values .and. any(sfc_alb_dir_gpt < 0._wp .or. sfc_alb_dir_gpt > 1._wp)) then
-      error_msg = "rte_sw: sfc_alb_dir out of bounds [0,1]"; return
+    if (check_values) then
+      if (any(sfc_alb_dir_gpt < 0._wp .or. sfc_alb_dir_gpt > 1._wp)) then
+        error_msg = "rte_sw: sfc_alb_dir out of bounds [0,1]"; return
+      end if
     end if
     if (any(shape(sfc_alb_dif_gpt) /= [ngpt, ncol])) then
       error_msg = "rte_sw: sfc_alb_dif inconsistently sized"; return
     end if
-    if (check_values .and. any(sfc_alb_dif_gpt < 0._wp .or. sfc_alb_dif_gpt > 1._wp)) then
-      error_msg = "rte_sw: sfc_alb_dif out of bounds [0,1]"; return
+    if (check_values) then
+      if (any(sfc_alb_dif_gpt < 0._wp .or. sfc_alb_dif_gpt > 1._wp)) then
+        error_msg = "rte_sw: sfc_alb_dif out of bounds [0,1]"; return
+      end if
     end if
 
     ng = int(ngpt, c_long_long) * nlay * ncol
@@ -137,11 +147,31 @@ contains
                                  merge(1_c_int, 0_c_int, top_at_1), d_inc, d_tau, d_mu0, d_dir, d_gdir), &
                                  "rte_sw: sw_solver_noscat")
     end select
+    ! broadband fluxes go straight into the caller's arrays when they are contiguous (and no net flux is wanted from
+    ! them); otherwise into temporaries copied after the sync
+    du = .false.; dd = .false.; dr = .false.
+    if (.not. associated(fluxes%flux_net)) then
+      du = direct_ok(fluxes%flux_up, nv); dd = direct_ok(fluxes%flux_dn, nv); dr = direct_ok(fluxes%flux_dn_dir, nv)
+    end if
     allocate(up(nlay + 1, ncol), dn(nlay + 1, ncol), dir(nlay + 1, ncol))
     if (error_msg == '') then
-      if (two_str) call dev_copy_out(up, d_up, nv)
-      if (two_str) call dev_copy_out(dn, d_dn, nv)
-      call dev_copy_out(dir, d_dir, nv)
+      if (two_str) then
+        if (du) then
+          call dev_copy_out(fluxes%flux_up, d_up, nv)
+        else
+          call dev_copy_out(up, d_up, nv)
+        end if
+        if (dd) then
+          call dev_copy_out(fluxes%flux_dn, d_dn, nv)
+        else
+          call dev_copy_out(dn, d_dn, nv)
+        end if
+      end if
+      if (dr) then
+        call dev_copy_out(fluxes%flux_dn_dir, d_dir, nv)
+      else
+        call dev_copy_out(dir, d_dir, nv)
+      end if
       if (gpt .and. two_str) then
         if (associated(fluxes%gpt_flux_up)) call dev_copy_out(fluxes%gpt_flux_up, d_gup, ngv)
         if (associated(fluxes%gpt_flux_dn)) call dev_copy_out(fluxes%gpt_flux_dn, d_gdn, ngv)
@@ -150,10 +180,10 @@ contains
     end if
     call rrtmgpnn_sync(error_msg, "rte_sw")
     if (error_msg == '') then
-      if (associated(fluxes%flux_dn_dir)) fluxes%flux_dn_dir = dir
+      if (associated(fluxes%flux_dn_dir) .and. .not. dr) fluxes%flux_dn_dir = dir
       if (two_str) then
-        if (associated(fluxes%flux_up))   fluxes%flux_up = up
-        if (associated(fluxes%flux_dn))   fluxes%flux_dn = dn
+        if (associated(fluxes%flux_up) .and. .not. du) fluxes%flux_up = up
+        if (associated(fluxes%flux_dn) .and. .not. dd) fluxes%flux_dn = dn
         if (associated(fluxes%flux_net))  fluxes%flux_net = dn - up
       end if
     end if
@@ -162,6 +192,14 @@ contains
     call dev_release(d_up); call dev_release(d_dn); call dev_release(d_dir)
     call dev_release(d_gup); call dev_release(d_gdn); call dev_release(d_gdir)
   end function rte_sw
+
+  ! whether the device fluxes can be copied into f itself: associated, contiguous and n elements
+  logical function direct_ok(f, n)
+    real(wp), dimension(:,:), pointer, intent(in) :: f
+    integer(c_long_long), intent(in) :: n
+    direct_ok = .false.
+    if (associated(f)) direct_ok = is_contiguous(f) .and. size(f, kind=c_long_long) == n
+  end function direct_ok
 
   ! whether two dummy arrays are the same actual array (same first element, same shape)
   logical function same_array(a, b)

@@ -43,8 +43,12 @@ program rrtmgpnn_rfmip_clear_sky
   type(ty_fluxes_flexible) :: fluxes
   character(len=128) :: e
   logical :: top_at_1
-  integer :: ncol, nlay, ngas, nmus, block_size, b0, b1, nb, icol, igpt, ig, u, nblocks, b, nrepeat, rep
-  integer(8) :: t0, t1, rate
+  integer :: ncol, nlay, ngas, nmus, block_size, b0, b1, nb, icol, igpt, ig, u, nblocks, b, nrepeat, rep, nb_alloc
+  integer(8) :: t0, t1, rate, ts(0:6)
+  ! per-section host times of thread 0 over the timed loops (printed when RRTMGPNN_SECTION_TIMES is set)
+  real(8) :: sect(6)
+  integer :: env_len, c0, c1, ngpt_sw
+  real(wp) :: s8(8)
   real(wp), allocatable :: vmr_all(:,:,:)
 
   if (command_argument_count() < 3) then
@@ -112,42 +116,81 @@ program rrtmgpnn_rfmip_clear_sky
     end do
   end do
 
+  sect = 0
   call system_clock(count_rate=rate)
+  ! One parallel region for every repetition: each thread allocates its optical properties, sources and spectral
+  ! boundary arrays once, for a full block, as the reference drivers allocate theirs before the block loop
+  ! (rrtmgp_rfmip_sw.F90:266-309); a shorter last block re-allocates.  (Allocated per block, the ~200 MB of host arrays
+  ! per thread and block were mapped and unmapped every block, and the host time per block grew with the thread count.)
+  !$omp parallel default(shared) &
+  !$omp   private(b, b0, b1, nb, icol, igpt, c0, c1, ngpt_sw, s8, op_lw, op_sw, sources, fluxes, sfc_emis_spec, toa_flux, sfc_alb_spec, &
+  !$omp           def_tsi, rep, nb_alloc, ts)
+  nb_alloc = 0
   do rep = 1, nrepeat
+    !$omp barrier
+    !$omp masked
     if (rep == 2) call system_clock(t0)
-    !$omp parallel do schedule(static) default(shared) &
-    !$omp   private(b, b0, b1, nb, icol, igpt, op_lw, op_sw, sources, fluxes, sfc_emis_spec, toa_flux, sfc_alb_spec, def_tsi)
+    !$omp end masked
+    !$omp do schedule(static)
     do b = 1, nblocks
       b0 = (b - 1) * block_size + 1
       b1 = min(ncol, b0 + block_size - 1)
       nb = b1 - b0 + 1
+      if (nb /= nb_alloc) then
+        if (nb_alloc > 0) then
+          call op_lw%finalize()
+          call sources%finalize()
+          call op_sw%finalize()
+          deallocate(sfc_emis_spec, toa_flux, sfc_alb_spec, def_tsi)
+        end if
+        call stop_on_err(op_lw%alloc_1scl(nb, nlay, kdist_lw))
+        call stop_on_err(sources%alloc(nb, nlay, kdist_lw))
+        call stop_on_err(op_sw%alloc_2str(nb, nlay, kdist_sw))
+        allocate(sfc_emis_spec(kdist_lw%get_nband(), nb))
+        allocate(toa_flux(kdist_sw%get_ngpt(), nb), sfc_alb_spec(kdist_sw%get_ngpt(), nb), def_tsi(nb))
+        nb_alloc = nb
+      end if
 
       ! ---- longwave (rrtmgp_rfmip_lw.F90:385-420) ----
-      call stop_on_err(op_lw%alloc_1scl(nb, nlay, kdist_lw))
-      call stop_on_err(sources%alloc(nb, nlay, kdist_lw))
-      allocate(sfc_emis_spec(kdist_lw%get_nband(), nb))
+      call system_clock(ts(0))
       do icol = 1, nb
         sfc_emis_spec(:, icol) = sfc_emis(b0 + icol - 1)
       end do
       call stop_on_err(kdist_lw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), tsfc(b0:b1), gas_concs(b), &
                                            op_lw, sources, tlev=tlev(:, b0:b1), neural_nets=nets_lw))
+      call system_clock(ts(1))
       fluxes%flux_up => lw_up(:, b0:b1)
       fluxes%flux_dn => lw_dn(:, b0:b1)
       fluxes%flux_dn_dir => NULL()
       call stop_on_err(rte_lw(op_lw, top_at_1, sources, sfc_emis_spec, fluxes, n_gauss_angles=nmus))
-      deallocate(sfc_emis_spec)
+      call system_clock(ts(2))
 
       ! ---- shortwave (rrtmgp_rfmip_sw.F90:370-470) ----
-      call stop_on_err(op_sw%alloc_2str(nb, nlay, kdist_sw))
-      allocate(toa_flux(kdist_sw%get_ngpt(), nb), sfc_alb_spec(kdist_sw%get_ngpt(), nb), def_tsi(nb))
       call stop_on_err(kdist_sw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), gas_concs(b), op_sw, &
                                            toa_flux, neural_nets=nets_sw))
-      do icol = 1, nb
+      call system_clock(ts(3))
+      ! def_tsi(icol) sums toa_flux(:, icol) in g-point order (rrtmgp_sw_eval_nn_rfmip.F90:365-369); eight columns at
+      ! a time keep eight independent sums in flight, each in its own column's order (so the same bits)
+      ngpt_sw = kdist_sw%get_ngpt()
+      c0 = 1
+      do while (c0 + 7 <= nb)
+        s8 = 0._wp
+        do igpt = 1, ngpt_sw
+          do c1 = 1, 8
+            s8(c1) = s8(c1) + toa_flux(igpt, c0 + c1 - 1)
+          end do
+        end do
+        def_tsi(c0:c0 + 7) = s8
+        c0 = c0 + 8
+      end do
+      do icol = c0, nb
         def_tsi(icol) = 0._wp
-        do igpt = 1, kdist_sw%get_ngpt()
+        do igpt = 1, ngpt_sw
           def_tsi(icol) = def_tsi(icol) + toa_flux(igpt, icol)
         end do
-        do igpt = 1, kdist_sw%get_ngpt()
+      end do
+      do icol = 1, nb
+        do igpt = 1, ngpt_sw
           toa_flux(igpt, icol) = toa_flux(igpt, icol) * tsi(b0 + icol - 1) / def_tsi(icol)
         end do
         sfc_alb_spec(:, icol) = sfc_alb(b0 + icol - 1)
@@ -155,27 +198,37 @@ program rrtmgpnn_rfmip_clear_sky
       fluxes%flux_up => sw_up(:, b0:b1)
       fluxes%flux_dn => sw_dn(:, b0:b1)
       fluxes%flux_dn_dir => sw_dir(:, b0:b1)
+      call system_clock(ts(4))
       call stop_on_err(rte_sw(op_sw, top_at_1, mu0(b0:b1), toa_flux, sfc_alb_spec, sfc_alb_spec, fluxes))
+      call system_clock(ts(5))
       do icol = 1, nb
         if (usecol(b0 + icol - 1) == 0._wp) then
           sw_up(:, b0 + icol - 1) = 0._wp
           sw_dn(:, b0 + icol - 1) = 0._wp
         end if
       end do
-      deallocate(toa_flux, sfc_alb_spec, def_tsi)
-      ! the thread's private objects give their device copies back to the context's pool (`!$acc exit data`): the
-      ! compiler does not finalise OpenMP private copies
-      call op_lw%finalize()
-      call sources%finalize()
-      call op_sw%finalize()
+      call system_clock(ts(6))
+      if (rep > 1 .and. b == 1) sect = sect + real(ts(1:6) - ts(0:5), 8)
     end do
-    !$omp end parallel do
+    !$omp end do
   end do
+  ! the thread's private objects give their device copies back to the context's pool (`!$acc exit data`): the
+  ! compiler does not finalise OpenMP private copies
+  if (nb_alloc > 0) then
+    call op_lw%finalize()
+    call sources%finalize()
+    call op_sw%finalize()
+    deallocate(sfc_emis_spec, toa_flux, sfc_alb_spec, def_tsi)
+  end if
+  !$omp end parallel
   if (nrepeat > 1) then
     call system_clock(t1)
     write(*, '(a,f12.4,a,i0,a,i0,a,i0,a)') "rrtmgpnn_rfmip_clear_sky: timing: ", &
       1000.0d0 * real(t1 - t0, 8) / real(rate, 8) / real(nrepeat - 1, 8), " ms per block loop (", nblocks, &
       " blocks of ", block_size, " columns, ", omp_get_max_threads(), " threads)"
+    call get_environment_variable("RRTMGPNN_SECTION_TIMES", length=env_len)
+    if (env_len > 0) write(*, '(a,6f10.1)') "rrtmgpnn_rfmip_clear_sky: block 1 us per loop (gas_optics_lw rte_lw "// &
+      "gas_optics_sw toa_norm rte_sw usecol):", 1.0d6 * sect / real(rate, 8) / real(nrepeat - 1, 8)
   end if
 
   ! heating rates of the longwave fluxes (extensions/mo_heating_rates), K/s

@@ -25,7 +25,6 @@ clouds=(lwp, iwp, rel, rei) makes it the all-sky step of examples/all-sky/rrtmgp
 :219), added to the LW absorption optical depth by band (1scl increment), and for SW delta-scaled and
 added as a two-stream increment; the SW solver then sees a non-zero asymmetry parameter.
 """
-import os
 
 import numpy as np
 import torch
@@ -51,8 +50,10 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True):
+                 sw=True, lw_after=None):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
+        # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
+        # "": the chains start together)
         self.dev = torch.device("cuda", device)
         self.allsky = clouds is not None
         self.fused = fused
@@ -236,10 +237,10 @@ class ClearSkyStep:
                  (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
-        self._finish(overlap)
+        self._finish(overlap, lw_after)
 
-    def _finish(self, overlap):
-        if self.fused and os.environ.get("RRTMGPNN_STEP_ORDER", "") != "class":
+    def _finish(self, overlap, lw_after=None):
+        if self.fused:
             # the small kernels that do not depend on a network's output go first in their chain, ahead of the big
             # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW
             # solver held while the LW solver, which needs it, could not start
@@ -254,29 +255,19 @@ class ClearSkyStep:
         # chip to itself).  Default: after the SW network when the SW solver's grid fits in one round of resident
         # waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane, against 16 per CU): the solver is then
         # latency-bound and its start is the step's critical path (C3: step -3 %); with more columns it is VALU-bound
-        # and the chains are better started together (C4: gating was 2.3 % slower).  RRTMGPNN_LW_AFTER=<SW-chain call>
-        # or "none" overrides.
+        # and the chains are better started together (C4: gating was 2.3 % slower).  Making the SW chain wait for
+        # the LW network instead, or both networks first, measured slower at C3.
         names = [n for n, _, _ in self.calls]
         gate = ""
         if overlap and self.fused and "predict_nn_sw" in names:
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
             if self.ncol * self.ng_sw <= 2048 * cus:
                 gate = "predict_nn_sw"
-        env = os.environ.get("RRTMGPNN_LW_AFTER", "")
-        self.lw_after = (env if env != "none" else "") if env else gate
-        if not overlap:
-            self.lw_after = ""
-        # RRTMGPNN_SW_AFTER=<LW-chain call>: the SW chain's calls issued after that LW call (all of them, or with the
-        # LW gate above only those after the SW network) wait for it to finish
-        self.sw_after = os.environ.get("RRTMGPNN_SW_AFTER", "") if overlap else ""
-        if self.sw_after:
-            if self.sw_after not in names or self.sw_after in SW_CHAIN or "get_col_dry" in names:
-                raise ValueError("RRTMGPNN_SW_AFTER: %r is not a call of this fused step's LW chain" % self.sw_after)
-            self._gate_sw = torch.cuda.Event()
+        self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
         if self.lw_after:
             names = [n for n, _, _ in self.calls]
             if self.lw_after not in names or self.lw_after not in SW_CHAIN or "get_col_dry" in names:
-                raise ValueError("RRTMGPNN_LW_AFTER: %r is not a call of this fused step's SW chain" % self.lw_after)
+                raise ValueError("lw_after: %r is not a call of this fused step's SW chain" % self.lw_after)
             cut = names.index(self.lw_after)
             head = [c for i, c in enumerate(self.calls) if c[0] in SW_CHAIN and i <= cut]
             self.calls = head + [c for c in self.calls if c not in head]
@@ -337,9 +328,6 @@ class ClearSkyStep:
             if self.overlap and name == self.lw_after:
                 self._gate.record(self.ctx2.stream)
                 self.ctx.stream.wait_event(self._gate)
-            if self.overlap and name == self.sw_after:
-                self._gate_sw.record(self.ctx.stream)
-                self.ctx2.stream.wait_event(self._gate_sw)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)

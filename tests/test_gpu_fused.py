@@ -158,7 +158,7 @@ def test_fused_gas_optics_equals_separate_calls(dev, rfmip, ncol, mlp_kernel):
 
 @pytest.mark.parametrize("allsky", [False, True])
 @pytest.mark.parametrize("lw_after", ["", "none", "sw_solver"])
-def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky, lw_after, monkeypatch):
+def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky, lw_after):
     """LW and SW chains on two streams (forked at the start, joined at the end; the LW chain started after the SW
     network by default at this size, with both started together, or after the SW solver), eager and as one
     hipGraph, give the single-stream step's fluxes bit for bit."""
@@ -167,11 +167,8 @@ def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky, lw_after, m
     prob = subset(rfmip, np.arange(0, 1800, 4))
     clouds = data.allsky_clouds(prob, data.load_cloud_optics("lw")) if allsky else None
     one = ClearSkyStep(prob, device=0, clouds=clouds, overlap=False)
-    if lw_after:
-        monkeypatch.setenv("RRTMGPNN_LW_AFTER", lw_after)
-    else:
-        monkeypatch.delenv("RRTMGPNN_LW_AFTER", raising=False)
-    two = ClearSkyStep(prob, device=0, clouds=clouds, overlap=True)
+    two = ClearSkyStep(prob, device=0, clouds=clouds, overlap=True,
+                       lw_after={"": None, "none": "", "sw_solver": "sw_solver"}[lw_after])
     assert two.lw_after == {"": "predict_nn_sw", "none": "", "sw_solver": "sw_solver"}[lw_after]
     one.step()
     two.step()

@@ -1,7 +1,9 @@
-"""Per host thread breakdown of a rocprofv3 --runtime-trace directory: for the last `--loops` seconds' worth of the
-trace, the time each thread spends inside each HIP API function, and the device's kernel / copy busy time.
+"""Per host thread breakdown of the steady-state block loops in a rocprofv3 --runtime-trace directory of the Fortran
+drop-in (tools/gpu_fortran_prof.sh): the window is the `nloops` loops of `loop_ms` each that end with the last SW
+solver kernel; for every thread, the time inside each HIP API function and outside HIP (host work: the staging
+memcpys, the Fortran code), and the device's kernel and copy busy time in the window.
 
-usage: trace_threads.py <rocprofv3 output dir>
+usage: trace_threads.py <rocprofv3 output dir> <loop_ms> [nloops=10]
 """
 import csv
 import glob
@@ -18,55 +20,40 @@ def rows(d, pat):
     return out
 
 
+def busy(iv):
+    tot, cs, ce = 0, None, None
+    for s, e in sorted(iv):
+        if ce is None or s > ce:
+            if ce is not None:
+                tot += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    return tot + (ce - cs if ce is not None else 0)
+
+
 def main():
-    d = sys.argv[1]
-    api = rows(d, "*hip_api_trace.csv")
-    ker = rows(d, "*kernel_trace.csv")
-    cpy = rows(d, "*memory_copy_trace.csv")
-    if not api:
-        raise SystemExit("no hip_api_trace.csv under " + d)
-    t_end = max(int(r["End_Timestamp"]) for r in api)
-    # the last half of the trace: the timed block loops (the first loop warms up)
-    t0 = min(int(r["Start_Timestamp"]) for r in api)
-    lo = t0 + (t_end - t0) // 2
+    d, loop_ms = sys.argv[1], float(sys.argv[2])
+    nloops = int(sys.argv[3]) if len(sys.argv) > 3 else 10
+    api, ker, cpy = rows(d, "*hip_api_trace.csv"), rows(d, "*kernel_trace.csv"), rows(d, "*memory_copy_trace.csv")
+    hi = max(int(r["End_Timestamp"]) for r in ker if "sw_2stream" in r["Kernel_Name"])
+    lo = hi - int(nloops * loop_ms * 1e6)
+    span = (hi - lo) / 1e3
+    print("window: last %d loops, %.1f us (%.1f us per loop)" % (nloops, span, span / nloops))
     per = defaultdict(lambda: defaultdict(float))
     for r in api:
-        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        if e < lo:
-            continue
-        per[r["Thread_Id"]][r["Function"]] += (e - max(s, lo)) * 1e-3
-    span = (t_end - lo) * 1e-3
-    print("window %.1f us" % span)
+        s, e = max(int(r["Start_Timestamp"]), lo), min(int(r["End_Timestamp"]), hi)
+        if e > s:
+            per[r["Thread_Id"]][r["Function"]] += (e - s) / 1e3
     for tid, fs in sorted(per.items()):
         tot = sum(fs.values())
-        top = sorted(fs.items(), key=lambda kv: -kv[1])[:6]
-        print("thread %s: in HIP %.1f us (%.0f%%): %s" % (tid, tot, 100 * tot / span,
-                                                        ", ".join("%s %.1f" % kv for kv in top)))
-
-    def busy(rs):
-        iv = sorted((max(int(r["Start_Timestamp"]), lo), int(r["End_Timestamp"])) for r in rs
-                    if int(r["End_Timestamp"]) > lo)
-        tot, cur_s, cur_e = 0, None, None
-        for s, e in iv:
-            if cur_e is None or s > cur_e:
-                if cur_e is not None:
-                    tot += cur_e - cur_s
-                cur_s, cur_e = s, e
-            else:
-                cur_e = max(cur_e, e)
-        if cur_e is not None:
-            tot += cur_e - cur_s
-        return tot * 1e-3, len(iv)
-
-    kb, kn = busy(ker)
-    cb, cn = busy(cpy)
-    print("device: kernels busy %.1f us (%d launches), copies busy %.1f us (%d copies)" % (kb, kn, cb, cn))
-    kern = defaultdict(float)
-    for r in ker:
-        if int(r["End_Timestamp"]) > lo:
-            kern[r["Kernel_Name"][:60]] += (int(r["End_Timestamp"]) - max(int(r["Start_Timestamp"]), lo)) * 1e-3
-    for k, v in sorted(kern.items(), key=lambda kv: -kv[1])[:8]:
-        print("  kernel %-60s %.1f us" % (k, v))
+        top = sorted(fs.items(), key=lambda kv: -kv[1])[:5]
+        print("thread %s per loop: host (outside HIP) %.1f us, in HIP %.1f us: %s" % (
+            tid, (span - tot) / nloops, tot / nloops, ", ".join("%s %.1f" % (k, v / nloops) for k, v in top)))
+    clip = lambda rs: [(max(int(r["Start_Timestamp"]), lo), min(int(r["End_Timestamp"]), hi)) for r in rs
+                       if int(r["End_Timestamp"]) > lo and int(r["Start_Timestamp"]) < hi]
+    print("device per loop: kernels busy %.1f us, copies busy %.1f us, either %.1f us" % (
+        busy(clip(ker)) / 1e3 / nloops, busy(clip(cpy)) / 1e3 / nloops, busy(clip(ker) + clip(cpy)) / 1e3 / nloops))
 
 
 if __name__ == "__main__":
