@@ -159,16 +159,12 @@ program rrtmgpnn_rfmip_clear_sky
       call stop_on_err(kdist_lw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), tsfc(b0:b1), gas_concs(b), &
                                            op_lw, sources, tlev=tlev(:, b0:b1), neural_nets=nets_lw))
       call system_clock(ts(1))
-      fluxes%flux_up => lw_up(:, b0:b1)
-      fluxes%flux_dn => lw_dn(:, b0:b1)
-      fluxes%flux_dn_dir => NULL()
-      call stop_on_err(rte_lw(op_lw, top_at_1, sources, sfc_emis_spec, fluxes, n_gauss_angles=nmus))
-      call system_clock(ts(2))
 
-      ! ---- shortwave (rrtmgp_rfmip_sw.F90:370-470) ----
+      ! ---- shortwave gas optics (rrtmgp_rfmip_sw.F90:370-405), issued before either solver: the networks run while
+      ! the host normalises the TSI ----
       call stop_on_err(kdist_sw%gas_optics(play(:, b0:b1), plev(:, b0:b1), tlay(:, b0:b1), gas_concs(b), op_sw, &
                                            toa_flux, neural_nets=nets_sw))
-      call system_clock(ts(3))
+      call system_clock(ts(2))
       ! def_tsi(icol) sums toa_flux(:, icol) in g-point order (rrtmgp_sw_eval_nn_rfmip.F90:365-369); eight columns at
       ! a time keep eight independent sums in flight, each in its own column's order (so the same bits)
       ngpt_sw = kdist_sw%get_ngpt()
@@ -195,18 +191,26 @@ program rrtmgpnn_rfmip_clear_sky
         end do
         sfc_alb_spec(:, icol) = sfc_alb(b0 + icol - 1)
       end do
+      call system_clock(ts(3))
+
+      ! ---- rte_sw (rrtmgp_rfmip_sw.F90:420-470), then rte_lw (rrtmgp_rfmip_lw.F90:405-420): rte_sw's host staging
+      ! overlaps the two networks, and rte_lw then waits for its solver alone ----
       fluxes%flux_up => sw_up(:, b0:b1)
       fluxes%flux_dn => sw_dn(:, b0:b1)
       fluxes%flux_dn_dir => sw_dir(:, b0:b1)
-      call system_clock(ts(4))
       call stop_on_err(rte_sw(op_sw, top_at_1, mu0(b0:b1), toa_flux, sfc_alb_spec, sfc_alb_spec, fluxes))
-      call system_clock(ts(5))
+      call system_clock(ts(4))
       do icol = 1, nb
         if (usecol(b0 + icol - 1) == 0._wp) then
           sw_up(:, b0 + icol - 1) = 0._wp
           sw_dn(:, b0 + icol - 1) = 0._wp
         end if
       end do
+      call system_clock(ts(5))
+      fluxes%flux_up => lw_up(:, b0:b1)
+      fluxes%flux_dn => lw_dn(:, b0:b1)
+      fluxes%flux_dn_dir => NULL()
+      call stop_on_err(rte_lw(op_lw, top_at_1, sources, sfc_emis_spec, fluxes, n_gauss_angles=nmus))
       call system_clock(ts(6))
       if (rep > 1 .and. b == 1) sect = sect + real(ts(1:6) - ts(0:5), 8)
     end do
@@ -227,8 +231,8 @@ program rrtmgpnn_rfmip_clear_sky
       1000.0d0 * real(t1 - t0, 8) / real(rate, 8) / real(nrepeat - 1, 8), " ms per block loop (", nblocks, &
       " blocks of ", block_size, " columns, ", omp_get_max_threads(), " threads)"
     call get_environment_variable("RRTMGPNN_SECTION_TIMES", length=env_len)
-    if (env_len > 0) write(*, '(a,6f10.1)') "rrtmgpnn_rfmip_clear_sky: block 1 us per loop (gas_optics_lw rte_lw "// &
-      "gas_optics_sw toa_norm rte_sw usecol):", 1.0d6 * sect / real(rate, 8) / real(nrepeat - 1, 8)
+    if (env_len > 0) write(*, '(a,6f10.1)') "rrtmgpnn_rfmip_clear_sky: block 1 us per loop (gas_optics_lw gas_optics_sw "// &
+      "toa_norm rte_sw usecol rte_lw):", 1.0d6 * sect / real(rate, 8) / real(nrepeat - 1, 8)
   end if
 
   ! heating rates of the longwave fluxes (extensions/mo_heating_rates), K/s
