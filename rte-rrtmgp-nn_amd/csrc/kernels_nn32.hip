@@ -248,25 +248,10 @@ __device__ __forceinline__ void mlp32_hidden(const float *__restrict__ img, cons
   }
 }
 
-#ifndef RRTMGPNN_MLP32_UNROLL
-#define RRTMGPNN_MLP32_UNROLL 2
-#endif
-#ifndef RRTMGPNN_MLP32_THREADS
-#define RRTMGPNN_MLP32_THREADS 512
-#endif
-constexpr int kMlp32Threads = RRTMGPNN_MLP32_THREADS;
-// the SW pair's block size and waves per SIMD (its 42 KB image leaves room for several blocks per CU)
-#ifndef RRTMGPNN_MLP32_SW_THREADS
-#define RRTMGPNN_MLP32_SW_THREADS 512
-#endif
-#ifndef RRTMGPNN_MLP32_SW_WPE
-#define RRTMGPNN_MLP32_SW_WPE 1
-#endif
-constexpr int kSwNT = RRTMGPNN_MLP32_SW_THREADS, kSwWPE = RRTMGPNN_MLP32_SW_WPE;
-// grid sized by the occupancy the runtime reports (1) or by the LDS footprint alone (0)
-#ifndef RRTMGPNN_MLP32_OCC
-#define RRTMGPNN_MLP32_OCC 1
-#endif
+// 8-wave blocks, output g-tiles unrolled by 2.  The SW pair keeps the same block: 4- and 12-wave blocks and an
+// unroll of 1 measured equal or slower at C3 and C4 (SW network alone, alternating on one box, round 3: 12 waves
+// +29 % at C3; 4 waves +1 %)
+constexpr int kMlp32Threads = 512, kSwNT = 512, kSwWPE = 1;
 
 // A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  The host guarantees that the
 // g-tiles are full: ngpt = 32 NGT (LW pair) or 2 ngpt = 32 NGT (LW both).  Dynamic LDS: the weight images, then 32
@@ -465,7 +450,7 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
         }
       }
     };
-#pragma unroll RRTMGPNN_MLP32_UNROLL
+#pragma unroll 2
     for (int go = 0; go < NGT; go++) out_tile(go);
   }
 }
@@ -486,7 +471,6 @@ static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
   const int wpb = NT / 64;
   int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / NT);
   const long long want = (ntiles + wpb - 1) / wpb;
-#if RRTMGPNN_MLP32_OCC
   // Blocks a CU actually holds (registers included).  When the tiles fill less than two rounds of resident blocks, a
   // grid of one round strides them and loads each weight image once per CU, instead of a partial second round that
   // loads it again for little work (the SW pair at C3: 184 VGPRs, one 8-wave block per CU, 422 blocks: step -1 %).
@@ -505,22 +489,10 @@ static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
     }
   }
   if (occ > 0 && want <= 2LL * occ * ctx->num_cus) per_cu = std::min(per_cu, occ);
-#endif
   const long long grid = std::max<long long>(1, std::min<long long>(want, (long long)ctx->num_cus * per_cu));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp32_kernel");
   return RRTMGPNN_OK;
-}
-
-// RRTMGPNN_MLP32=0 in the environment selects the 16x16x4 kernel for every network (whole-process A/B runs; read
-// once); rrtmgpnn_context_set_mlp_kernel selects per context
-static bool mlp32_enabled()
-{
-  static const bool on = [] {
-    const char *e = std::getenv("RRTMGPNN_MLP32");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 
 static bool shape32(const rrtmgpnn_network *n, int KS, int HT1, int N2, int HT2, int N3, int NGT)
@@ -536,7 +508,7 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
                  float *out2, const MlpInputs *in)
 {
   const int kmode = ctx->mlp_kernel >= 0 ? ctx->mlp_kernel : g_mlp_kernel_default;
-  if (kmode == 1 || !mlp32_enabled() || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH && mode != MLP_SW_PAIR))
+  if (kmode == 1 || (mode != MLP_LW_PAIR && mode != MLP_LW_BOTH && mode != MLP_SW_PAIR))
     return RRTMGPNN_ERR_UNSUPPORTED;
   const bool pair = mode != MLP_LW_BOTH;
   auto std_acts = [](const rrtmgpnn_network *n) {
