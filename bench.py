@@ -39,6 +39,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-s", type=float, default=1.0,
+                    help="untimed steps for this many seconds before the warmup steps (the GPU's clocks ramp up over "
+                         "the first ~0.1 s of steps: 20 steps after 5 warmup steps ran 0.53 ms/step at C3 where "
+                         "steady state is 0.44-0.45); reported as settle_s / settle_steps")
     ap.add_argument("--config", default="c3", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="c3: RFMIP 1800x60 LW+SW (default, the metric's config); c1: the first 100 RFMIP columns, LW "
                          "only (BASELINE configs[0], the reference's CPU case); c2: the 1800 columns, LW only "
@@ -238,6 +242,14 @@ def main():
     run_one = step.replay if use_graph else step.step
     run = rank_run.run
 
+    # settle: untimed steps until the GPU runs at its steady clocks (reported in the line), then the warmup steps
+    settle_steps, ts0 = 0, time.perf_counter()
+    while time.perf_counter() - ts0 < args.settle_s:
+        for _ in range(8):
+            run()
+        settle_steps += 8
+        torch.cuda.synchronize(dev)
+    settle_s = time.perf_counter() - ts0
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize(dev)
@@ -409,7 +421,8 @@ def main():
     if rank == 0:
         out = {
             "metric": metric, "value": round(value, 1), "unit": "columns/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "warmup": args.warmup, "settle_s": round(settle_s, 3) if args.settle_s > 0 else 0.0,
+            "settle_steps": settle_steps, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data_desc,
             "config": {"workload": workload, "global_columns": global_cols, "ncol_per_gpu": hi - lo,
                        "chunk_columns": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
