@@ -11,7 +11,8 @@
 !   gpt_flux_dn_dir (h: the spectral direct beam); rte_lw with flux_up_Jac / flux_dn_Jac (filled with -7) on the 1scl
 !   tau of (b) (i) and on the two-stream properties, rescaled (j): '' returned, the Jacobian arrays untouched (written
 !   out as jac_up_i/jac_dn_i/jac_up_j/jac_dn_j), the fluxes those of (b) and (f); with use_2stream the reference's
-!   message for flux_up_Jac, and '' for a lone flux_dn_Jac (the reference tests flux_up_Jac twice, :252).
+!   message for flux_up_Jac, and '' for a lone flux_dn_Jac (the reference tests flux_up_Jac twice, :252); (k) rte_lw
+!   as (b) and (l) rte_sw as (e) with flux_net associated too (the fluxes through temporaries).
 program devstate
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -35,6 +36,8 @@ program devstate
   real(wp), allocatable, target :: up_g(:,:), dn_g(:,:), gup_g(:,:,:), gdn_g(:,:,:), dir_h(:,:), gdir_h(:,:,:)
   real(wp), allocatable, target :: up_i(:,:), dn_i(:,:), up_j(:,:), dn_j(:,:)
   real(wp), allocatable, target :: jup_i(:,:), jdn_i(:,:), jup_j(:,:), jdn_j(:,:)
+  real(wp), allocatable, target :: up_k(:,:), dn_k(:,:), net_k(:,:), up_l(:,:), dn_l(:,:), dir_l(:,:), net_l(:,:)
+  type(ty_fluxes_flexible) :: fl6
   type(ty_fluxes_flexible) :: fl5
   type(ty_fluxes_flexible) :: fl3, fl4
   real(wp), allocatable :: lw_ds(:,:), inc(:,:), alb(:,:), mu0(:)
@@ -177,7 +180,27 @@ program devstate
   fl5%flux_up => up_j
   fl5%flux_dn => dn_j
   call chk(rte_lw(op2, top_at_1, src, emis, fl5, flux_up_Jac=jup_j, flux_dn_Jac=jdn_j))
-  u = rbin_write_begin(ofile, 41)
+  ! (k) rte_lw on the tau of (b) and (l) rte_sw on the properties of (e) with flux_net wanted too: the broadband
+  ! fluxes then go through temporaries (net = dn - up on the host) instead of straight into the caller's arrays
+  allocate(up_k(nlay + 1, ncol), dn_k(nlay + 1, ncol), net_k(nlay + 1, ncol))
+  allocate(up_l(nlay + 1, ncol), dn_l(nlay + 1, ncol), dir_l(nlay + 1, ncol), net_l(nlay + 1, ncol))
+  fl6%flux_up => up_k
+  fl6%flux_dn => dn_k
+  fl6%flux_net => net_k
+  call chk(rte_lw(op, top_at_1, src, emis, fl6))
+  fl6%flux_up => up_l
+  fl6%flux_dn => dn_l
+  fl6%flux_dn_dir => dir_l
+  fl6%flux_net => net_l
+  call chk(rte_sw(op2, top_at_1, mu0, inc, alb, alb, fl6))
+  u = rbin_write_begin(ofile, 48)
+  call rbin_write_real(u, "flux_up_k", up_k, shape(up_k))
+  call rbin_write_real(u, "flux_dn_k", dn_k, shape(dn_k))
+  call rbin_write_real(u, "flux_net_k", net_k, shape(net_k))
+  call rbin_write_real(u, "flux_up_l", up_l, shape(up_l))
+  call rbin_write_real(u, "flux_dn_l", dn_l, shape(dn_l))
+  call rbin_write_real(u, "flux_dir_l", dir_l, shape(dir_l))
+  call rbin_write_real(u, "flux_net_l", net_l, shape(net_l))
   call rbin_write_real(u, "tau", tau0, shape(tau0))
   call rbin_write_real(u, "lay_source", lay0, shape(lay0))
   call rbin_write_real(u, "lev_source", lev0, shape(lev0))

@@ -223,6 +223,16 @@ def test_fortran_device_state_update_host_and_device(tmp_path, orc, rfmip):
         np.testing.assert_array_equal(got["flux_dn_" + tag], want[1], err_msg=tag)
         for k in ("jac_up_", "jac_dn_"):
             assert (got[k + tag] == np.float32(-7)).all(), k + tag
+    # (k), (l) with flux_net associated: rte_lw as (b); rte_sw as (e) but without g-point outputs (whose broadband
+    # down flux is summed from the g-point totals, :572-588), so against the oracle's plain solver; net = dn - up
+    want_l = orc.sw_solver(t2, np.full_like(t2, 0.5), np.full_like(t2, 0.3), np.full(ncol, 0.6, np.float32),
+                           np.ones((ncol, ngpt), np.float32), np.full((ncol, ngpt), 0.2, np.float32),
+                           np.full((ncol, ngpt), 0.2, np.float32), prob["top_at_1"])
+    for tag, (up, dn) in (("k", (got["flux_up_b"], got["flux_dn_b"])), ("l", want_l[:2])):
+        np.testing.assert_array_equal(got["flux_up_" + tag], up, err_msg=tag)
+        np.testing.assert_array_equal(got["flux_dn_" + tag], dn, err_msg=tag)
+        np.testing.assert_array_equal(got["flux_net_" + tag], dn - up, err_msg=tag)
+    np.testing.assert_array_equal(got["flux_dir_l"], want_l[2])
 
 
 @pytest.mark.gpu
