@@ -6,7 +6,9 @@ configs[2] "RFMIP clear-sky LW+SW, 1800 columns x 60 layers, NN gas optics both 
 (the real RFMIP inputs shipped with the reference + the reference's NN weights).  A step is
 gas_optics(LW, NN) + rte_lw + gas_optics(SW, NN) + rte_sw over the block, inputs resident in HBM.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+Multi-GPU: `python bench.py --gpus N` starts its own N rank processes (torch.distributed.run, rendezvous
+on 127.0.0.1) before touching the GPU, and the driver's `python -m torch.distributed.run --nproc-per-node
+N bench.py --gpus N` runs the same ranks directly (WORLD_SIZE must then equal N).  One process per
 GPU.  The job is one global problem partitioned by rrtmgpnn.shard.column_range (the gloo-tested
 partition): by default N x the config's block (weak scaling, N x 1800 RFMIP columns at C3, each rank
 a 1800-column block); with --global the config's fixed global size (C5: 1e6 synthetic columns x 137
@@ -14,7 +16,8 @@ layers, strong scaling), each rank streaming its range through the step in chunk
 125 000 columns.  No collective in the data path; barrier + synchronize around the timed region, max
 over ranks.  After timing, the broadband fluxes are all-gathered once with shard.gather_columns over
 RCCL (the final flux reduction the north star names), timed as "gather_ms" and folded into
-"end_to_end" (all columns / (timed steps + gather)), never into `value`.
+"end_to_end" (all columns / (timed steps + gather)), never into `value`; every rank then checks the
+gathered array against every rank's own slab ("gather_check"; a failure exits non-zero).
 
 Prints ONE JSON line on rank 0.
 """
@@ -68,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
                     help="auto: the reference's own Fortran (oracle/_ref) when built, else the C restatement")
+    ap.add_argument("--cpu-bind", default="close", choices=["none", "close", "spread"],
+                    help="OpenMP thread placement of the CPU baseline (OMP_PROC_BIND with OMP_PLACES=cores; none: "
+                         "unbound)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "pmc_sq.json"),
                     help="committed SQ counters per config/stage (tools/profile_configs.sh): valu_busy")
@@ -165,12 +171,25 @@ def main():
         return
     import torch
     import torch.distributed as dist
+    from rrtmgpnn import shard
+
+    # --gpus N: under an outer launcher (torch.distributed.run) this process is one rank and WORLD_SIZE must equal
+    # N; without one, N > 1 starts N rank processes here, before any GPU call in this process (a child process,
+    # never an exec), and exits with their status -- rank 0 prints the line.  N = 1 runs in this process.
+    try:
+        plan = shard.launch_plan(args.gpus, os.environ)
+    except ValueError as e:
+        sys.stderr.write("bench.py: %s\n" % e)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(shard.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:], torch.cuda.device_count()))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     # one process per GPU; with more ranks than GPUs (rehearsing the N-rank path on a smaller box) ranks share
     # devices round-robin, and RRTMGPNN_DIST_BACKEND=gloo replaces RCCL, which refuses two ranks on one GPU
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    ndev = max(1, torch.cuda.device_count())
+    local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
     backend = os.environ.get("RRTMGPNN_DIST_BACKEND", "nccl")
     if world > 1:
         kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
@@ -178,7 +197,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from rrtmgpnn import data, shard
+    from rrtmgpnn import data
     from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
 
     # ---- the global problem and this rank's part of it (shard.column_range) ----
@@ -242,6 +261,30 @@ def main():
     run_one = step.replay if use_graph else step.step
     run = rank_run.run
 
+    def warm_and_time():
+        """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize; max over ranks (s)."""
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            run()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    # unsettled: the first W + K steps of the process, exactly as the driver's command would time them without the
+    # settle phase (reported beside `value` as ms_per_step_unsettled, for comparison with rounds 1-2)
+    elapsed_unsettled = warm_and_time() if args.settle_s > 0 else None
     # settle: untimed steps until the GPU runs at its steady clocks (reported in the line), then the warmup steps
     settle_steps, ts0 = 0, time.perf_counter()
     while time.perf_counter() - ts0 < args.settle_s:
@@ -250,24 +293,7 @@ def main():
         settle_steps += 8
         torch.cuda.synchronize(dev)
     settle_s = time.perf_counter() - ts0
-    for _ in range(args.warmup):
-        run()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = warm_and_time()
     ms_per_step = elapsed / args.steps * 1e3
     total_cols = global_cols * args.steps
     value = total_cols / elapsed
@@ -397,6 +423,7 @@ def main():
     # tested exchange, of the rank's (ncol, 5, nlev) flux slab into the global (global_cols, 5, nlev) array ----
     gather_ms = None
     end_to_end = None
+    gather_check = None
     if world > 1:
         local_slab = torch.stack(list(rank_run.flux), dim=1)
         torch.cuda.synchronize(dev)
@@ -409,20 +436,35 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         gather_ms = float(t.item())
         assert full.shape[0] == global_cols
+        # every rank checks the gathered array: its own slab in place bit for bit, every rank's slab in place by an
+        # exact checksum of its bits, finite fluxes; the verdict is reduced over ranks
+        chk = shard.verify_gather(full, local_slab, global_cols, rank, world)
+        ok = torch.tensor([1 if chk["ok"] else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        gather_check = dict(chk, ok=bool(ok.item()), ranks_checked=world,
+                            note="rank 0's view; ok is the minimum over ranks of (own slab bitwise, every slab's "
+                                 "checksum in place, finite)")
         del full
+        if not gather_check["ok"]:
+            sys.stderr.write("bench.py: flux all-gather check failed on some rank: %s\n" % chk)
         end_to_end = {"value": round(total_cols / (elapsed + gather_ms * 1e-3), 1), "unit": "columns/s",
                       "note": "all ranks' columns over the timed steps plus one final flux all-gather"}
 
     # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(prob, clouds, args.cpu_seconds, args.cpu_kind, sw=step.sw)
+        cpu = cpu_baseline(prob, clouds, args.cpu_seconds, args.cpu_kind, sw=step.sw, bind=args.cpu_bind)
 
     if rank == 0:
         out = {
             "metric": metric, "value": round(value, 1), "unit": "columns/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "settle_s": round(settle_s, 3) if args.settle_s > 0 else 0.0,
-            "settle_steps": settle_steps, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "settle_steps": settle_steps, "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step_unsettled": (None if elapsed_unsettled is None else
+                                      round(elapsed_unsettled / args.steps * 1e3, 4)),
+            "value_unsettled": (None if elapsed_unsettled is None else
+                                round(total_cols / elapsed_unsettled, 1)),
+            "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data_desc,
             "config": {"workload": workload, "global_columns": global_cols, "ncol_per_gpu": hi - lo,
                        "chunk_columns": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
@@ -441,12 +483,20 @@ def main():
             "stages_overlapped_ms": None if stages_ov is None else {k: round(v, 4) for k, v in stages_ov.items()},
             "stage_roofline": stage_roofs,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "gather_check": gather_check,
             "end_to_end": end_to_end,
             "host_resident": pcie,
         }
+        if world > 1:
+            out["ranks"] = {"launcher": ("bench.py --gpus %d (torch.distributed.run child)" % world
+                                         if os.environ.get("RRTMGPNN_VISIBLE_DEVICES") else "outer launcher"),
+                            "world_size": world, "visible_devices": ndev, "backend": backend,
+                            "ranks_per_device": -(-world // ndev)}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+        if not gather_check["ok"]:
+            sys.exit(1)
 
 
 def _subset(prob, idx):
@@ -463,7 +513,7 @@ def _cpu_block(ncol):
     return max(d for d in range(1, min(36, ncol) + 1) if ncol % d == 0)
 
 
-def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
+def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5, bind="close"):
     """CPU path on the host cores over a bounded sample of the same workload (rank 0, N=1 only).
 
     kind "reference" (default when oracle/_ref is built): oracle/_ref/rrtmgp_cpu_bench (oracle/cpu_bench.F90), the
@@ -474,16 +524,32 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
     netcdf-fortran).  Blocks cycle through up to 3 600 columns of the workload; `reps` timed runs, the median
     reported (tests/test_cpu_bench.py checks the program's fluxes against the oracle bit for bit).
 
-    Threads: `value` is measured on the box's CPU share for one GPU (OMP_NUM_THREADS, 16 on the GPU box; this
-    process may not use more).  `thread_sweep` adds measured 1- and 8-thread points, and `extrapolated` scales the
-    16-thread value linearly to the per-GPU share of the whole node (nproc / 8 logical CPUs) and to all nproc: the
-    blocks are independent, so linear scaling is an upper bound on the CPU path there, not a measurement.
+    Threads: `value` is measured on the CPU share the GPU box gives one GPU's job -- OMP_NUM_THREADS, which the box
+    sets to 16 (its rules size every worker pool to that share), capped by the process's affinity mask; the line
+    records both (`cpu_allotment`).  The threads are placed with OMP_PROC_BIND=`bind`, OMP_PLACES=cores (unbound
+    threads migrated and the 16-thread runs spread by 31 % in round 3).  `thread_sweep` adds measured 1- and
+    8-thread points, and `extrapolated` scales the measured value linearly to nproc / 8 logical CPUs (one GPU's
+    share of the node's CPUs) and to all nproc: the blocks are independent, so linear scaling is an upper bound on
+    the CPU path there, not a measurement.
     kind "port": the C restatement alone, OpenMP over columns (when oracle/_ref is absent)."""
     import statistics
     import subprocess
     import tempfile
     from rrtmgpnn import data
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    omp_env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(omp_env or 16, affinity)
+    allot = {"omp_num_threads_env": omp_env or None, "affinity_cpus": affinity, "nproc": os.cpu_count(),
+             "bind": bind}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            allot["cgroup_cpu_max"] = f.read().strip()
+    except OSError:
+        pass
+    bind_env = {} if bind == "none" else {"OMP_PROC_BIND": bind, "OMP_PLACES": "cores"}
     exe = os.path.join(ROOT, "oracle", "_ref", "rrtmgp_cpu_bench")
     what = "%s gas optics%s + RTE" % ("LW+SW" if sw else "LW",
                                       " + cloud optics/increment/delta-scale" if clouds is not None else "")
@@ -499,7 +565,10 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
 
             def run(nthr, ncols, nreps):
                 env = dict(os.environ, OMP_NUM_THREADS=str(nthr), OMP_STACKSIZE="256M",
-                           MKL_THREADING_LAYER="SEQUENTIAL")
+                           MKL_THREADING_LAYER="SEQUENTIAL", **bind_env)
+                if bind == "none":
+                    env.pop("OMP_PROC_BIND", None)
+                    env.pop("OMP_PLACES", None)
                 r = subprocess.run([exe, path, data.DATA_DIR, str(nthr), str(block), str(ncols), str(int(sw)),
                                     str(nreps)], capture_output=True, text=True, env=env, timeout=600)
                 if r.returncode != 0:
@@ -531,18 +600,21 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5):
         return {"value": round(value, 1), "unit": "columns/s", "cores": threads, "kind": "reference",
                 "nproc": nproc, "runs_s": [round(t, 4) for t in secs],
                 "spread": round((max(secs) - min(secs)) / med, 4),
-                "thread_sweep": sweep,
+                "thread_sweep": sweep, "cpu_allotment": allot,
                 "extrapolated": {
-                    "per_gpu_share": {"threads": max(1, nproc // 8), "value": round(per_thread * max(1, nproc // 8), 1)},
+                    "node_share_per_gpu": {"threads": max(1, nproc // 8),
+                                           "value": round(per_thread * max(1, nproc // 8), 1)},
                     "node": {"threads": nproc, "value": round(per_thread * nproc, 1)},
-                    "note": "linear in threads from the measured value (an upper bound: blocks are independent); "
-                            "not measured -- one GPU's box share is %d threads" % threads},
+                    "note": "not measured: linear in threads from the %d-thread value (an upper bound, the blocks are "
+                            "independent), to nproc/8 and nproc logical CPUs; the measured %d threads are the CPU "
+                            "share the GPU box allots this job (OMP_NUM_THREADS)" % (threads, threads)},
                 "sample": ("%d columns per run (blocks of %d cycling through %d columns of the workload), %s, median "
                            "of %d runs: the reference's Fortran rte_lw/rte_sw + network_type sgemm MLP (MKL, "
-                           "sequential)%s compiled from its sources, OpenMP over blocks on %d threads "
+                           "sequential)%s compiled from its sources, OpenMP over blocks on %d threads (%s) "
                            "(oracle/cpu_bench.F90, as rrtmgp_rfmip_lw.F90:364-446); NN glue from the C restatement"
                            % (res["columns"], block, nsamp, what, len(secs),
-                              " + ty_cloud_optics" if clouds is not None else "", threads))}
+                              " + ty_cloud_optics" if clouds is not None else "", threads,
+                              "unbound" if bind == "none" else "OMP_PROC_BIND=%s, OMP_PLACES=cores" % bind))}
     # the C restatement alone (bit-identical to the reference on the solvers and MLP), OpenMP over columns
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:

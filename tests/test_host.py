@@ -107,9 +107,19 @@ def _shard_worker(rank, world, port, q):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     ncol = 1001
     lo, hi = shard.column_range(ncol, rank, world)
-    local = torch.arange(lo, hi, dtype=torch.float32)[:, None].repeat(1, 3)
+    # flux-like slabs (ncol_local, 5 quantities, nlev): per-rank values from a seeded generator
+    g = torch.Generator().manual_seed(100 + rank)
+    local = torch.rand((hi - lo, 5, 61), generator=g) * 400.0
+    local[:, 0, 0] = torch.arange(lo, hi, dtype=torch.float32)
     full = shard.gather_columns(local, ncol, world)
-    q.put((rank, lo, hi, bool(torch.equal(full[:, 0], torch.arange(ncol, dtype=torch.float32)))))
+    chk = shard.verify_gather(full, local, ncol, rank, world)
+    # a gathered array with two of the other rank's columns swapped must fail the checksum on this rank
+    bad = full.clone()
+    o_lo, o_hi = shard.column_range(ncol, 1 - rank, world)
+    bad[[o_lo, o_lo + 1]] = bad[[o_lo + 1, o_lo]]
+    chk_bad = shard.verify_gather(bad, local, ncol, rank, world)
+    q.put((rank, lo, hi, bool(torch.equal(full[:, 0, 0], torch.arange(ncol, dtype=torch.float32))), chk["ok"],
+           chk_bad["ok"], chk_bad["own_slab_bitwise"]))
     dist.destroy_process_group()
 
 
@@ -131,6 +141,56 @@ def test_column_sharding_gloo_world2():
         p.join(timeout=60)
     assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == 1001
     assert res[0][3] and res[1][3]
+    assert res[0][4] and res[1][4]              # the gather check passes on the true gather
+    assert not res[0][5] and not res[1][5]      # ... and catches another rank's misplaced columns
+    assert res[0][6] and res[1][6]              # (the rank's own slab was untouched)
+
+
+def test_bench_launch_plan():
+    """bench.py --gpus N: one rank in-process at N = 1, self-launch at N > 1, the outer launcher's world must be N."""
+    from rrtmgpnn import shard
+    assert shard.launch_plan(1, {}) == "single"
+    assert shard.launch_plan(8, {}) == "spawn"
+    assert shard.launch_plan(4, {"WORLD_SIZE": "4"}) == "rank"
+    assert shard.launch_plan(1, {"WORLD_SIZE": "1"}) == "rank"
+    with pytest.raises(ValueError):
+        shard.launch_plan(8, {"WORLD_SIZE": "2"})
+    with pytest.raises(ValueError):
+        shard.launch_plan(0, {})
+    cmd = shard.launch_command(8, "/x/bench.py", ["--gpus", "8", "--steps", "20"], 29500)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
+    assert cmd[-5:] == ["/x/bench.py", "--gpus", "8", "--steps", "20"]
+
+
+def test_bench_rejects_gpus_world_mismatch():
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "disagrees" in r.stderr
+
+
+def test_spawn_ranks_starts_n_processes(tmp_path):
+    """spawn_ranks runs the script as N torch.distributed.run ranks (no GPU: the script only reports its env)."""
+    from rrtmgpnn import shard
+    out = tmp_path / "ranks"
+    out.mkdir()
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys\n"
+                      "open(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write("
+                      "'%s %s %s %s' % (os.environ['WORLD_SIZE'], os.environ['LOCAL_RANK'], "
+                      "os.environ.get('RRTMGPNN_DIST_BACKEND'), sys.argv[2]))\n")
+    env_backup = os.environ.pop("RRTMGPNN_DIST_BACKEND", None)
+    try:
+        rc = shard.spawn_ranks(2, str(script), [str(out), "--gpus"], visible_devices=1)
+    finally:
+        if env_backup is not None:
+            os.environ["RRTMGPNN_DIST_BACKEND"] = env_backup
+    assert rc == 0
+    got = sorted((p.name, p.read_text()) for p in out.iterdir())
+    assert got == [("0", "2 0 gloo --gpus"), ("1", "2 1 gloo --gpus")]
 
 
 def test_synthetic_problem_column_ranges_are_slices_of_the_whole():
