@@ -94,6 +94,11 @@ int rrtmgpnn_context_create_owned(int device, rrtmgpnn_context **ctx);
  *   in every context of the process (the reference's OpenACC data environment is process-wide).
  * rrtmgpnn_present_delete: drop the entry (its buffer returns to the pool; `!$acc exit data delete`); no-op if absent.
  *   Every other context's copy of that host array is stale from then on and is uploaded again at its next READ.
+ * Cross-thread contract of update_device / delete: the host copy wins in every context.  A copy another context holds
+ *   as device newer (a kernel result not yet copied back with update_host) is discarded too; a thread that still needs
+ *   such a result must update_host it before any thread updates or deletes the same host array.  The process-wide
+ *   generation table behind this keeps one 16-byte entry per host address ever updated or deleted (bounded by the
+ *   distinct addresses the host program's allocator hands out).
  * rrtmgpnn_stage_h2d / rrtmgpnn_scratch / rrtmgpnn_release: stream-ordered per-call buffers from the same pool
  *   (a call's inputs copied in, its intermediates); released buffers are reused by later work on the stream.
  * rrtmgpnn_copy_d2h / rrtmgpnn_copy_h2d / rrtmgpnn_copy_d2d: enqueue a copy on the context's stream (the device side complete after

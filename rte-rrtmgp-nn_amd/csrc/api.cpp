@@ -208,14 +208,14 @@ int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream)
   if (int rc = check_ctx(ctx)) return rc;
   // The device data environment orders every use of a pooled buffer, a pinned-ring slice and a queued device-to-host
   // copy on the context's one stream: finish the old stream's work (and the pending copies, resetting the ring)
-  // before work on the new stream can be handed those buffers, whoever owns the old stream.  Not while either stream
-  // is being captured into a hipGraph: a capture cannot be synchronised, and the graph orders its own nodes.
-  hipStreamCaptureStatus cap_old = hipStreamCaptureStatusNone, cap_new = hipStreamCaptureStatusNone;
+  // before work on the new stream can be handed those buffers, whoever owns the old stream -- also when the new stream
+  // is being captured into a hipGraph (the old stream's queued copies and ring slices must be complete before the
+  // capture's nodes reuse them).  Only a capturing old stream is left alone: a capture cannot be synchronised, and
+  // the graph orders its own nodes.
+  hipStreamCaptureStatus cap_old = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(ctx->stream, &cap_old);
-  (void)hipStreamIsCapturing((hipStream_t)hip_stream, &cap_new);
   (void)hipGetLastError();
-  if ((ctx->stream != (hipStream_t)hip_stream || ctx->own_stream) && cap_old == hipStreamCaptureStatusNone &&
-      cap_new == hipStreamCaptureStatusNone)
+  if ((ctx->stream != (hipStream_t)hip_stream || ctx->own_stream) && cap_old == hipStreamCaptureStatusNone)
     if (int rc = ctx->sync()) return rc;
   if (ctx->own_stream) {
     (void)hipStreamDestroy(ctx->stream);

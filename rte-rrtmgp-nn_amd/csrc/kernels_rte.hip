@@ -126,6 +126,9 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 #define SW_BOUNDS
 #endif
 static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
+// ring_flush_lanes walks slot s's 4 partials with lanes 4s .. 4s+3: a flush of kRing slots needs 4 * kRing lanes, and
+// the smallest LW block (ngpt <= 64) has 64
+static_assert(4 * kRing <= 64, "the LW ring's lane-per-partial flush needs 4 lanes per slot within one wave");
 // LW no-scattering flush: one lane per partial sum over padded ring rows when ngpt % 4 == 0 (RRTMGPNN_LW_FLUSH_LANES=0:
 // the float4 walk of ring_flush over unpadded rows)
 #ifndef RRTMGPNN_LW_FLUSH_LANES
@@ -546,7 +549,13 @@ __device__ __forceinline__ void inc_2str(float &t1, float &w1, float &g1, float 
 //
 // One column per block: packing two 224-g-point columns into 7 full waves (as the two-per-lane kernel does) was
 // measured slower here (C3 0.312 vs 0.288 ms): its 72 VGPRs allow 7 waves per SIMD, and this kernel wants 8.
-template <bool kHasG, bool kInc, int kPF>
+//
+// kGpt: also store the g-point fluxes (ty_fluxes_flexible; (ngpt, nlay+1, ncol) each): up, the total down flux
+// (diffuse + direct, rounded once: "adding computes only diffuse flux; flux_dn is total", :665-666, and for ngpt not
+// a multiple of 4 radn_dn = radn_dn + radn_dir, :682) and direct, with the broadband down flux summed from the
+// total as sw_solver_2stream does when it saves them (:660-684).  This is the g-point kernel for odd ngpt; even ngpt
+// takes the checkpointed kernel's g-point instance.
+template <bool kHasG, bool kInc, int kPF, bool kGpt = false>
 __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int top_at_1,
                                             const float *__restrict__ inc_flux, const float *__restrict__ inc_dif,
                                             const float *__restrict__ tau, const float *__restrict__ ssa,
@@ -555,7 +564,9 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
                                             BandArgs bands, const float *__restrict__ tau_bnd,
                                             const float *__restrict__ ssa_bnd, const float *__restrict__ g_bnd,
                                             float *__restrict__ ws, float *__restrict__ flux_up,
-                                            float *__restrict__ flux_dn, float *__restrict__ flux_dir)
+                                            float *__restrict__ flux_dn, float *__restrict__ flux_dir,
+                                            float *__restrict__ gpt_up, float *__restrict__ gpt_dn,
+                                            float *__restrict__ gpt_dir)
 {
   static_assert(kRingSw % kPF == 0, "prefetch depth must divide the ring");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -681,21 +692,25 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
     }
   }
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
-  auto put = [&](float up, float dif, float dir, int r) {
+  // lev: the level's array index (the g-point outputs)
+  auto put = [&](float up, float dif, float dir, int r, int lev) {
     if (on) {
+      const float dn = kGpt ? dif + dir : dif;  // kGpt: the total, summed as such (dn_mode off below)
       ring[(size_t)r * ngpt + g] = up;
-      ring[((size_t)kRingSw + r) * ngpt + g] = dif;
+      ring[((size_t)kRingSw + r) * ngpt + g] = dn;
       ring[((size_t)2 * kRingSw + r) * ngpt + g] = dir;
+      if constexpr (kGpt) {
+        const size_t o = (size_t)g + (size_t)ngpt * ((size_t)lev + (size_t)nlev * icol);
+        gpt_up[o] = up;
+        gpt_dn[o] = dn;
+        gpt_dir[o] = dir;
+      }
     }
   };
-  auto flush = [&](int n, int lev0, int dl) {
-#ifndef RRTMGPNN_ABL_NO_BARRIER
-    ring_flush<kRingSw>(ring, part, 3, n, lev0, dl, ngpt, nlev, true);
-#endif
-  };
+  auto flush = [&](int n, int lev0, int dl) { ring_flush<kRingSw>(ring, part, 3, n, lev0, dl, ngpt, nlev, !kGpt); };
   const int dl_dn = top_at_1 ? 1 : -1;
   float Fdn = (on && inc_dif) ? inc_dif[gcol] : 0.0f;
-  put(Fdn * alb_b + src_b, Fdn, Ftop, 0);  // Eq 12 at the top; alb_b/src_b hold the top level's values
+  put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top);  // Eq 12 at the top; alb_b/src_b hold the top level's values
   flush(1, top, 1);
   {
     float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
@@ -728,7 +743,7 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
           const float denom = rcp_rn_normal(1.0f - d.Rdif * alb);
           Fdn = (d.Tdif * Fdn + d.Rdif * src + Sdn) * denom;  // Eq 13 (adding :1583-1591)
           const float up = Fdn * alb + src;                    // Eq 12
-          put(up, Fdn, Fdir, r);
+          put(up, Fdn, Fdir, r, top + dl_dn * (j + 1));
         }
       }
       flush(min(kRingSw, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
@@ -741,16 +756,18 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   }
 }
 
-template <bool kHasG, bool kInc>
+template <bool kHasG, bool kInc, bool kGpt = false>
 static void sw_launch(rrtmgpnn_context *ctx, size_t lds, int threads, int ngpt, int nlay, int ncol,
                       int top_at_1, const float *inc_flux, const float *inc_flux_dif, const float *tau,
                       const float *ssa, const float *g, const float *mu0, const float *alb_dir, const float *alb_dif,
                       const BandArgs &bands, const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws,
                       float *flux_up, float *flux_dn, float *flux_dir)
 {
-  hipLaunchKernelGGL((sw_2stream_kernel<kHasG, kInc, RRTMGPNN_SW_PF>), dim3(ncol), dim3(threads), lds, ctx->stream,
-                     ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0,
-                     alb_dir, alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, (float *)ws, flux_up, flux_dn, flux_dir);
+  const auto &ex = ctx->extras;
+  hipLaunchKernelGGL((sw_2stream_kernel<kHasG, kInc, RRTMGPNN_SW_PF, kGpt>), dim3(ncol), dim3(threads), lds,
+                     ctx->stream, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
+                     alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, (float *)ws, flux_up, flux_dn, flux_dir, ex.gpt_up,
+                     ex.gpt_dn, ex.gpt_dir);
 }
 
 int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
@@ -765,9 +782,12 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   // per launch at C3, whole step C3 -3 %, C4 -1 % against kernels_sw_x2.hip, tools/gpu_ab.sh); mode 2 forces the
   // workspace-plane kernel, mode 1 one g-point per lane (also the odd-ngpt kernel).
   const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
-  // g-point outputs (the *_gpt entries) are written by the checkpointed kernel, whatever the mode
+  // g-point outputs (the *_gpt entries) are written by the checkpointed kernel for even ngpt, whatever the mode, and
+  // by the one-per-lane kernel for odd ngpt
   const bool gpt = ctx->extras.gpt_up || ctx->extras.gpt_dn || ctx->extras.gpt_dir;
-  if (gpt && ngpt % 2) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: g-point outputs need an even ngpt");
+  if (gpt && (!ctx->extras.gpt_up || !ctx->extras.gpt_dn || !ctx->extras.gpt_dir))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "sw solver: g-point outputs need gpt_flux_up, gpt_flux_dn and gpt_flux_dn_dir");
+  if (gpt && inc) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: g-point outputs with a fused increment");
   const bool ck = (ngpt % 2) == 0 && (mode == 3 || mode == 0 || gpt);
   const bool x2 = !ck && kSwX2 && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
@@ -787,7 +807,13 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (lds > 64 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many layers for LDS partials");
   const BandArgs nob{};
   const BandArgs &b = inc ? *bands : nob;
-  if (inc && g)
+  if (gpt && g)
+    sw_launch<true, false, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
+                                 mu0, alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
+  else if (gpt)
+    sw_launch<false, false, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
+                                  mu0, alb_dir, alb_dif, b, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir);
+  else if (inc && g)
     sw_launch<true, true>(ctx, lds, threads, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g,
                           mu0, alb_dir, alb_dif, b, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
   else if (inc)

@@ -201,6 +201,7 @@ int rrtmgpnn_present(rrtmgpnn_context *ctx, const void *host, long long bytes, i
   auto &p = it->second;
   const uint64_t gen = generation(host);
   if (p.gen != gen) {  // updated or deleted through some context since this copy was made: the host copy is newer
+    // (also over a device-newer copy of this context: the host wins, include/rrtmgpnn.h)
     p.state = 0;
     p.gen = gen;
   }

@@ -64,6 +64,8 @@ contains
     if (.not. fluxes%are_desired()) then
       error_msg = "rte_lw: no space allocated for fluxes"; return
     end if
+    error_msg = fluxes%check_extents(nlay + 1, ncol)
+    if (error_msg /= '') return
     if (any([sources%get_ncol(), sources%get_nlay(), sources%get_ngpt()] /= [ncol, nlay, ngpt])) then
       error_msg = "rte_lw: sources and optical properties inconsistently sized"; return
     end if
@@ -249,7 +251,8 @@ contains
     call dev_release(d_ds); call dev_release(d_gup); call dev_release(d_gdn)
   end function rte_lw
 
-  ! whether the device fluxes can be copied into f itself: associated, contiguous and n elements
+  ! whether the device fluxes can be copied into f itself: associated, contiguous and n elements (the extents were
+  ! checked on entry, fluxes%check_extents)
   logical function direct_ok(f, n)
     real(wp), dimension(:,:), pointer, intent(in) :: f
     integer(c_long_long), intent(in) :: n

@@ -40,6 +40,8 @@ contains
     if (.not. fluxes%are_desired()) then
       error_msg = "rte_sw: no space allocated for fluxes"; return
     end if
+    error_msg = fluxes%check_extents(nlay + 1, ncol)
+    if (error_msg /= '') return
     if (associated(fluxes%gpt_flux_up)) then
       if (any(shape(fluxes%gpt_flux_up) /= [ngpt, nlay + 1, ncol])) then
         error_msg = "rte_sw: gpt_flux_up inconsistently sized"; return

@@ -12,7 +12,9 @@
 !   tau of (b) (i) and on the two-stream properties, rescaled (j): '' returned, the Jacobian arrays untouched (written
 !   out as jac_up_i/jac_dn_i/jac_up_j/jac_dn_j), the fluxes those of (b) and (f); with use_2stream the reference's
 !   message for flux_up_Jac, and '' for a lone flux_dn_Jac (the reference tests flux_up_Jac twice, :252); (k) rte_lw
-!   as (b) and (l) rte_sw as (e) with flux_net associated too (the fluxes through temporaries).
+!   as (b) and (l) rte_sw as (e) with flux_net associated too (the fluxes through temporaries); (m) a flux_up of the
+!   transposed shape (ncol, nlay+1) and a flux_dn_dir with one level too many are refused with reduce_broadband's
+!   messages (exit status 4 / 5), the caller's array untouched.
 program devstate
   use mo_rte_kind,           only: wp
   use mo_optical_props,      only: ty_optical_props_1scl, ty_optical_props_2str
@@ -37,7 +39,8 @@ program devstate
   real(wp), allocatable, target :: up_i(:,:), dn_i(:,:), up_j(:,:), dn_j(:,:)
   real(wp), allocatable, target :: jup_i(:,:), jdn_i(:,:), jup_j(:,:), jdn_j(:,:)
   real(wp), allocatable, target :: up_k(:,:), dn_k(:,:), net_k(:,:), up_l(:,:), dn_l(:,:), dir_l(:,:), net_l(:,:)
-  type(ty_fluxes_flexible) :: fl6
+  type(ty_fluxes_flexible) :: fl6, fl7
+  real(wp), allocatable, target :: bad_t(:,:), bad_l(:,:)
   type(ty_fluxes_flexible) :: fl5
   type(ty_fluxes_flexible) :: fl3, fl4
   real(wp), allocatable :: lw_ds(:,:), inc(:,:), alb(:,:), mu0(:)
@@ -193,6 +196,24 @@ program devstate
   fl6%flux_dn_dir => dir_l
   fl6%flux_net => net_l
   call chk(rte_sw(op2, top_at_1, mu0, inc, alb, alb, fl6))
+  ! (m) broadband arrays of the wrong shape are refused before any device work, with reduce_broadband's messages
+  ! (rte/mo_fluxes.F90:143-162): the same number of elements in the transposed shape, and one level too many
+  allocate(bad_t(ncol, nlay + 1), bad_l(nlay + 2, ncol))
+  bad_t = -3._wp
+  fl7%flux_up => bad_t
+  fl7%flux_dn => dn_k
+  e = rte_lw(op, top_at_1, src, emis, fl7)
+  if (e /= "reduce: flux_up array incorrectly sized" .or. any(bad_t /= -3._wp)) then
+    write(*, '(a)') "rte_lw with a (ncol, nlay+1) flux_up returned: '" // trim(e) // "'"
+    error stop 4
+  end if
+  fl7%flux_up => up_k
+  fl7%flux_dn_dir => bad_l
+  e = rte_sw(op2, top_at_1, mu0, inc, alb, alb, fl7)
+  if (e /= "reduce: flux_dn_dir array incorrectly sized") then
+    write(*, '(a)') "rte_sw with a (nlay+2, ncol) flux_dn_dir returned: '" // trim(e) // "'"
+    error stop 5
+  end if
   u = rbin_write_begin(ofile, 48)
   call rbin_write_real(u, "flux_up_k", up_k, shape(up_k))
   call rbin_write_real(u, "flux_dn_k", dn_k, shape(dn_k))

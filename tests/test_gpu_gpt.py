@@ -95,12 +95,16 @@ def test_lw_planck_gpt_matches_oracle(dev, orc, rfmip, top_at_1, nmus):
 
 @pytest.mark.parametrize("top_at_1", [True, False])
 @pytest.mark.parametrize("with_g", [False, True])
-def test_sw_gpt_matches_oracle(dev, orc, top_at_1, with_g):
+@pytest.mark.parametrize("ngpt", [224, 223, 222])
+def test_sw_gpt_matches_oracle(dev, orc, top_at_1, with_g, ngpt):
+    """224: the checkpointed kernel's g-point instance; 222 (even, not a multiple of 4): the same kernel with the
+    sequential broadband sums; 223 (odd): the one-g-point-per-lane kernel's g-point instance (sw_solver_2stream saves
+    g-point fluxes for any ngpt, rte/kernels/mo_rte_solver_kernels.F90:567-588, 660-684)."""
     from rrtmgpnn import _lib
     from rrtmgpnn._lib import check
     from rrtmgpnn.api import context
     rng = np.random.default_rng(5)
-    ncol, nlay, ngpt = 29, 41, 224
+    ncol, nlay = 29, 41
     tau = rng.lognormal(-2, 2, size=(ncol, nlay, ngpt)).astype(np.float32)
     ssa = rng.uniform(0, 1, size=(ncol, nlay, ngpt)).astype(np.float32)
     g = rng.uniform(0, 0.9, size=(ncol, nlay, ngpt)).astype(np.float32) if with_g else np.zeros_like(tau)
