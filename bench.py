@@ -71,9 +71,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
                     help="auto: the reference's own Fortran (oracle/_ref) when built, else the C restatement")
-    ap.add_argument("--cpu-bind", default="close", choices=["none", "close", "spread"],
+    ap.add_argument("--cpu-bind", default="none", choices=["none", "close", "spread"],
                     help="OpenMP thread placement of the CPU baseline (OMP_PROC_BIND with OMP_PLACES=cores; none: "
-                         "unbound)")
+                         "unbound, the default: on the GPU box 'close' put all 16 threads on 2 places, 10x slower)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--sq-json", default=os.path.join(ROOT, "profiles", "pmc_sq.json"),
                     help="committed SQ counters per config/stage (tools/profile_configs.sh): valu_busy")
@@ -513,7 +513,7 @@ def _cpu_block(ncol):
     return max(d for d in range(1, min(36, ncol) + 1) if ncol % d == 0)
 
 
-def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5, bind="close"):
+def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=7, bind="none"):
     """CPU path on the host cores over a bounded sample of the same workload (rank 0, N=1 only).
 
     kind "reference" (default when oracle/_ref is built): oracle/_ref/rrtmgp_cpu_bench (oracle/cpu_bench.F90), the
@@ -526,8 +526,9 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=5, bind="clo
 
     Threads: `value` is measured on the CPU share the GPU box gives one GPU's job -- OMP_NUM_THREADS, which the box
     sets to 16 (its rules size every worker pool to that share), capped by the process's affinity mask; the line
-    records both (`cpu_allotment`).  The threads are placed with OMP_PROC_BIND=`bind`, OMP_PLACES=cores (unbound
-    threads migrated and the 16-thread runs spread by 31 % in round 3).  `thread_sweep` adds measured 1- and
+    records both (`cpu_allotment`, with the cgroup CPU quota).  Threads are unbound by default: OMP_PROC_BIND=close
+    with OMP_PLACES=cores put all 16 threads on the 2 places the runtime found on the GPU box (4.97 k columns/s
+    against 49 k unbound, profiles/r04/cpu_bind_close.json); the median of `reps` runs is the value.  `thread_sweep` adds measured 1- and
     8-thread points, and `extrapolated` scales the measured value linearly to nproc / 8 logical CPUs (one GPU's
     share of the node's CPUs) and to all nproc: the blocks are independent, so linear scaling is an upper bound on
     the CPU path there, not a measurement.

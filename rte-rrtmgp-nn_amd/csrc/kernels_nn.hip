@@ -164,9 +164,6 @@ __device__ __forceinline__ float activate(int act, float x)
 template <int ACTS>
 __device__ __forceinline__ float act_hidden(int act, float x)
 {
-#ifdef RRTMGPNN_ABL_MLP_CHEAP_ACT  // ablation only: breaks parity
-  if constexpr (ACTS == 1) return x * 0.5f;
-#endif
   if constexpr (ACTS == 1) return softsign(x);  // nn_device.hpp (mod_activation.F90:107-128)
   else return activate(act, x);
 }
@@ -327,39 +324,13 @@ __device__ __forceinline__ floatx4 mlp_out_tile(const float *__restrict__ img, i
   return acc;
 }
 
-// Threads per MLP block (tools/solver_variants.sh knob): the weight images live once per block in LDS,
-// so a wider block raises the waves per SIMD that share one copy of them.
-#ifndef RRTMGPNN_MLP_THREADS
-#define RRTMGPNN_MLP_THREADS 512
-#endif
-#ifndef RRTMGPNN_MLP_GO_UNROLL
-#define RRTMGPNN_MLP_GO_UNROLL 1
-#endif
-constexpr int kMlpThreads = RRTMGPNN_MLP_THREADS, kGoUnroll = RRTMGPNN_MLP_GO_UNROLL;
-// A 1024-thread instance of the LW pair with in-kernel inputs (4 waves per SIMD instead of 2 under the 108 KB weight
-// image, 128 VGPRs) for batches below RRTMGPNN_MLP_BIG_MAX_TILES tiles: alone it is 13 % faster at C3 (6 750 tiles,
-// no 4th-round tail), but it takes every register of every SIMD while it runs, the SW chain can no longer overlap it,
-// and the C3 step got 18 % slower (0.66 vs 0.56 ms, tools/ab_trees.sh).  Off by default (0).
-#ifndef RRTMGPNN_MLP_BIG_THREADS
-#define RRTMGPNN_MLP_BIG_THREADS 1024
-#endif
-#ifndef RRTMGPNN_MLP_BIG_MAX_TILES
-#define RRTMGPNN_MLP_BIG_MAX_TILES 0
-#endif
-// Compile-time output g-tile count for the shipped pairs (LW 16, SW 14): the output loop unrolls completely and the
-// next tile's inputs are loaded before this tile's stores, so the wait for them (vmcnt counts loads and stores
-// together, in order) no longer drains the stores.  0 compiles the runtime-count loop only.
-#ifndef RRTMGPNN_MLP_NGT_CT
-#define RRTMGPNN_MLP_NGT_CT 1
-#endif
-// output tiles unrolled per loop trip when NGTC > 0 (tools/solver_variants.sh: LW 4 -5 % C3 / -7 % C4 against the
-// runtime loop, full unrolling spills; SW 2 -9 % at C4)
-#ifndef RRTMGPNN_MLP_CT_UNROLL_LW
-#define RRTMGPNN_MLP_CT_UNROLL_LW 4
-#endif
-#ifndef RRTMGPNN_MLP_CT_UNROLL_SW
-#define RRTMGPNN_MLP_CT_UNROLL_SW 2
-#endif
+// Threads per MLP block: the weight images live once per block in LDS, so a wider block raises the waves per SIMD
+// that share one copy of them (a 1024-thread LW instance was 13 % faster alone at C3 but took every register of every
+// SIMD, and the overlapped C3 step got 18 % slower).  The shipped pairs' output g-tile counts are compiled in (LW 16,
+// SW 14): the output loop then unrolls (LW 4 tiles per trip: -5 % C3 / -7 % C4 against the runtime loop, full
+// unrolling spills; SW 2: -9 % at C4), and the next tile's inputs are loaded before this tile's stores, so the wait
+// for them (vmcnt counts loads and stores together, in order) no longer drains the stores.
+constexpr int kMlpThreads = 512, kGoUnroll = 1;
 
 // XIN: the inputs are formed in-kernel (compute_nn_inputs + get_col_dry per sample, the expressions of
 // nn_inputs_kernel and col_dry_kernel) instead of read from nn_inputs / col_dry arrays.  Lane (j, q) needs inputs
@@ -547,9 +518,6 @@ __global__ __launch_bounds__(NT) void mlp_pair_kernel(MlpArgs a)
               tau[r] = pow8(t) * cd;
               pf[r] = p * p;
             }
-#ifdef RRTMGPNN_ABL_MLP_NOSTORE  // ablation only: stores skipped unless a value is a nan
-            if (tau[0] != tau[0] || pf[0] != pf[0])
-#endif
             {
               put4(a.out0, ngpt, g0, tau);  // tau
               put4(a.out1, ngpt, g0, pf);   // pfrac
@@ -576,10 +544,10 @@ __global__ __launch_bounds__(NT) void mlp_pair_kernel(MlpArgs a)
       }
     };
     if constexpr (NGTC > 0 && MODE == MLP_LW_PAIR) {
-#pragma unroll RRTMGPNN_MLP_CT_UNROLL_LW
+#pragma unroll 4
       for (int go = 0; go < NGTC; go++) out_tile(go);
     } else if constexpr (NGTC > 0) {
-#pragma unroll RRTMGPNN_MLP_CT_UNROLL_SW
+#pragma unroll 2
       for (int go = 0; go < NGTC; go++) out_tile(go);
     } else {
 #pragma unroll kGoUnroll
@@ -622,13 +590,11 @@ static int launch_mlp_t(rrtmgpnn_context *ctx, MlpArgs &a)
     // the shipped pairs' output tile counts compiled in: LW g256 (16 tiles), SW g224 (14)
     constexpr bool lw = MODE == MLP_LW_PAIR && AK == 5 && AH1 == 4 && AH2 == 4 && BH1 == 1 && BH2 == 1;
     constexpr bool sw = MODE == MLP_SW_PAIR && AK == 2 && AH1 == 1 && AH2 == 1 && BH1 == 1 && BH2 == 1;
-    if constexpr (RRTMGPNN_MLP_NGT_CT && lw) {
-      if (a.ngt == 16 && a.play && (a.nbatch + 15) / 16 < RRTMGPNN_MLP_BIG_MAX_TILES)
-        return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16, true, RRTMGPNN_MLP_BIG_THREADS>(ctx, a);
+    if constexpr (lw) {
       if (a.ngt == 16 && a.play) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16, true>(ctx, a);
       if (a.ngt == 16) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 16>(ctx, a);
     }
-    if constexpr (RRTMGPNN_MLP_NGT_CT && sw) {
+    if constexpr (sw) {
       if (a.ngt == 14 && a.play) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 14, true>(ctx, a);
       if (a.ngt == 14) return launch_mlp_acts<AK, AH1, AH2, BK, BH1, BH2, MODE, 1, 14>(ctx, a);
     }

@@ -426,11 +426,7 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
           t = t + mnA;
           const float p = yB[r] + bB;
           const float tau = pow8(t) * cdr[r], pf = p * p;
-#ifdef RRTMGPNN_ABL_MLP32_NOSTORE  // ablation only: stores dropped unless a value is a nan
-          const uint32_t off = (tau != tau || pf != pf) ? vo[r] + 128u * go : kOOB;
-#else
           const uint32_t off = vo[r] + 128u * go;
-#endif
           o0.st(tau, off);
           o1.st(pf, off);
         }

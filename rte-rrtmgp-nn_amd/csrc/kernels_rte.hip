@@ -16,11 +16,6 @@
 
 namespace rrtmgpnn {
 
-// Ablation switches for tools/ablate_solvers.sh (never set in the product build): they break parity
-// on purpose to attribute solver time.  RRTMGPNN_ABL_NO_REDUCE: skip the ordered broadband reduction (barriers
-// kept); RRTMGPNN_ABL_NO_BARRIER: skip staging and flushing entirely.  (The hardware-exp variant is the opt-in
-// tolerance build RRTMGPNN_FAST_LIBM, rte_device.hpp.)
-
 __device__ __forceinline__ float wave_sum(float v)
 {
 #pragma unroll
@@ -89,69 +84,21 @@ int launch_planck_source(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, in
 // ------------------------------------------------------------------------------------------
 // Solver tuning (the ordered broadband reduction and buffer addressing live in rte_device.hpp).
 // ------------------------------------------------------------------------------------------
-// Tuning knobs (overridable with -D for tools/solver_variants.sh):
-//   kRing : levels staged in LDS per ordered flush;
-//   *_PF  : layers of inputs kept in flight per lane (software prefetch) -- LW, fused LW, SW;
-//   *_WAVES : __launch_bounds__ minimum waves per SIMD (0 = none; > 0 caps blocks at 256 threads).
-#ifndef RRTMGPNN_RING
-#define RRTMGPNN_RING 8
-#endif
-#ifndef RRTMGPNN_SW_RING
-#define RRTMGPNN_SW_RING 6
-#endif
-#ifndef RRTMGPNN_LW_PF
-#define RRTMGPNN_LW_PF 4
-#endif
-#ifndef RRTMGPNN_LWF_PF
-#define RRTMGPNN_LWF_PF 2
-#endif
-#ifndef RRTMGPNN_SW_PF
-#define RRTMGPNN_SW_PF 2
-#endif
-#ifndef RRTMGPNN_LW_WAVES
-#define RRTMGPNN_LW_WAVES 8
-#endif
-#ifndef RRTMGPNN_SW_WAVES
-#define RRTMGPNN_SW_WAVES 8
-#endif
-#define BOUNDS_(w) __launch_bounds__(256, w)
-#if RRTMGPNN_LW_WAVES > 0
-#define LW_BOUNDS BOUNDS_(RRTMGPNN_LW_WAVES)
-#else
-#define LW_BOUNDS
-#endif
-#if RRTMGPNN_SW_WAVES > 0
-#define SW_BOUNDS BOUNDS_(RRTMGPNN_SW_WAVES)
-#else
-#define SW_BOUNDS
-#endif
-static constexpr int kRing = RRTMGPNN_RING, kRingSw = RRTMGPNN_SW_RING;
+// Solver constants (each chosen by A/B on one box, rounds 1-3):
+//   kRing / kRingSw : levels staged in LDS per ordered flush (LW, one-g-point-per-lane SW);
+//   k*Pf            : layers of inputs kept in flight per lane (software prefetch) -- LW, fused LW, SW;
+//   __launch_bounds__(256, 8): 8 waves per SIMD, blocks of at most 256 threads (one column, lane = g-point).
+#define LW_BOUNDS __launch_bounds__(256, 8)
+#define SW_BOUNDS __launch_bounds__(256, 8)
+static constexpr int kRing = 8, kRingSw = 6;
+static constexpr int kLwPf = 4, kLwfPf = 2, kSwPf = 2;
 // ring_flush_lanes walks slot s's 4 partials with lanes 4s .. 4s+3: a flush of kRing slots needs 4 * kRing lanes, and
 // the smallest LW block (ngpt <= 64) has 64
 static_assert(4 * kRing <= 64, "the LW ring's lane-per-partial flush needs 4 lanes per slot within one wave");
-// LW no-scattering flush: one lane per partial sum over padded ring rows when ngpt % 4 == 0 (RRTMGPNN_LW_FLUSH_LANES=0:
-// the float4 walk of ring_flush over unpadded rows)
-#ifndef RRTMGPNN_LW_FLUSH_LANES
-#define RRTMGPNN_LW_FLUSH_LANES 1
-#endif
-__host__ __device__ constexpr int lw_ring_stride(int ngpt)
-{
-  return (RRTMGPNN_LW_FLUSH_LANES && (ngpt & 3) == 0) ? ngpt + 4 : ngpt;
-}
-// SW with a fused increment: park the incremented (tau, ssa, g) in workspace for pass 3 (1), or have pass 3
-// re-read the inputs and form the increment again (0: three fewer planes written, one fewer read)
-#ifndef RRTMGPNN_SW_INC_PARK
-#define RRTMGPNN_SW_INC_PARK 1
-#endif
-static constexpr bool kSwIncPark = RRTMGPNN_SW_INC_PARK != 0;
-// SW solver with two g-points per lane and packed fp32 (kernels_sw_x2.hip) for even ngpt, when the context's
-// mode (rrtmgpnn_context_set_sw_kernel) or the problem size picks it; 0 compiles it out
-#ifndef RRTMGPNN_SW_X2
-#define RRTMGPNN_SW_X2 1
-#endif
-static constexpr bool kSwX2 = RRTMGPNN_SW_X2 != 0;
-static constexpr int kLwMaxG = RRTMGPNN_LW_WAVES > 0 ? 256 : 1024;  // g-points per column block
-static constexpr int kSwMaxG = RRTMGPNN_SW_WAVES > 0 ? 256 : 1024;
+// LW no-scattering flush: one lane per partial sum over ring rows padded by 4 floats when ngpt % 4 == 0 (the float4
+// walk of ring_flush over unpadded rows otherwise)
+__host__ __device__ constexpr int lw_ring_stride(int ngpt) { return (ngpt & 3) == 0 ? ngpt + 4 : ngpt; }
+static constexpr int kLwMaxG = 256, kSwMaxG = 256;  // g-points per column block
 // ------------------------------------------------------------------------------------------
 // LW no-scattering solver.  block = one column, lane = g-point.  The down pass stores nothing: the
 // up pass re-reads its layer's inputs (L2/MALL-hot) and recomputes trans and the source, bitwise
@@ -255,14 +202,12 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     }
   };
   auto flush = [&](float *pq, int n, int lev0, int dl) {
-#ifndef RRTMGPNN_ABL_NO_BARRIER
     if constexpr (!kMulti) {
       if (rs != ngpt)
         ring_flush_lanes(ring, rs, pq, n, lev0, dl, ngpt);
       else
         ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
     }
-#endif
   };
   // layer source and the level source on the side given by `li` (lev index, 0..nlay)
   auto lay_src = [&](float y, int l) { return kFused ? y * bl[l] : y; };
@@ -419,7 +364,7 @@ static int launch_lw_impl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, i
     gup = gdn + nv;
     gcs = 2 * nv;
   }
-  constexpr int PF = kFused ? RRTMGPNN_LWF_PF : RRTMGPNN_LW_PF;
+  constexpr int PF = kFused ? kLwfPf : kLwPf;
   if (nmus > 1 || gpt)
     hipLaunchKernelGGL((lw_noscat_kernel<kFused, kInc, PF, true>), dim3(ncol), dim3(threads), lds, ctx->stream, ngpt,
                        nlay, ncol, top_at_1, a, inc_flux, tau, lay_or_pfrac, kFused ? lay_or_pfrac : lev_source,
@@ -509,7 +454,7 @@ __device__ __forceinline__ SwCoef sw_two_stream(float tau, float w0, float g, fl
   const SwDif d = sw_dif(tau, w0, g, etab);
   const float gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
   float Tnoscat = solver_exp_beam(-tau * mu0_inv, etab);
-  float gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? 0.5f : (2.0f - 3.0f * mu0 * g) * .25f;
+  float gamma3 = kG0 ? 0.5f : (2.0f - 3.0f * mu0 * g) * .25f;
   float gamma4 = 1.0f - gamma3;
   float alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   float alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
@@ -667,11 +612,9 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
         const float Fin = pf[p];
         if constexpr (kInc) {
           inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);
-          if (kSwIncPark) {
-            WT.st(t, vls, row * l);
-            WW.st(w0, vls, row * l);
-            WG.st(g0, vls, row * l);
-          }
+          WT.st(t, vls, row * l);
+          WW.st(w0, vls, row * l);
+          WG.st(g0, vls, row * l);
         }
         load2(p, lay_of_up(min(j + kPF, nlay - 1)));
         float alb = alb_b, src = src_b, Sdn = 0.0f;
@@ -713,16 +656,13 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top);  // Eq 12 at the top; alb_b/src_b hold the top level's values
   flush(1, top, 1);
   {
-    float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
+    float pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF];
     auto load = [&](int p, int l) {
       const uint32_t s = row * l, sb = row * lev_below(l);
-      if constexpr (kInc && kSwIncPark) {
+      if constexpr (kInc) {
         pt[p] = WT.ld(vL, s); pw[p] = WW.ld(vL, s); pg[p] = WG.ld(vL, s);
       } else {
         pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s);
-      }
-      if constexpr (kInc && !kSwIncPark) {
-        qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
       pd[p] = WD.ld(vV, s);
       pa[p] = WB.ld(vV, sb); ps[p] = WS.ld(vV, sb); pf[p] = WA.ld(vV, sb);
@@ -733,9 +673,8 @@ __global__ void SW_BOUNDS sw_2stream_kernel(int ngpt, int nlay, int ncol, int to
 #pragma unroll
       for (int r = 0; r < kRingSw; r++) {
         const int j = j0 + r, p = r % kPF;
-        float t = pt[p], w0 = pw[p], g0 = kHasG || (kInc && kSwIncPark) ? pg[p] : 0.0f;
+        const float t = pt[p], w0 = pw[p], g0 = kHasG || kInc ? pg[p] : 0.0f;
         const float Sdn = pd[p], alb = pa[p], src = ps[p], Fdir = pf[p];
-        if constexpr (kInc && !kSwIncPark) inc_2str(t, w0, g0, qt[p], qw[p], qg[p]);  // pass 2's increment again
         load(p, lay_of_down(min(j + kPF, nlay - 1)));
         if (j < nlay) {
           // R_dif, T_dif exactly as pass 2 computed them (same inputs, same expressions -> same bits)
@@ -764,7 +703,7 @@ static void sw_launch(rrtmgpnn_context *ctx, size_t lds, int threads, int ngpt, 
                       float *flux_up, float *flux_dn, float *flux_dir)
 {
   const auto &ex = ctx->extras;
-  hipLaunchKernelGGL((sw_2stream_kernel<kHasG, kInc, RRTMGPNN_SW_PF, kGpt>), dim3(ncol), dim3(threads), lds,
+  hipLaunchKernelGGL((sw_2stream_kernel<kHasG, kInc, kSwPf, kGpt>), dim3(ncol), dim3(threads), lds,
                      ctx->stream, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
                      alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, (float *)ws, flux_up, flux_dn, flux_dir, ex.gpt_up,
                      ex.gpt_dn, ex.gpt_dir);
@@ -789,9 +728,9 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
     return fail(RRTMGPNN_ERR_ARGUMENT, "sw solver: g-point outputs need gpt_flux_up, gpt_flux_dn and gpt_flux_dn_dir");
   if (gpt && inc) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: g-point outputs with a fused increment");
   const bool ck = (ngpt % 2) == 0 && (mode == 3 || mode == 0 || gpt);
-  const bool x2 = !ck && kSwX2 && (ngpt % 2) == 0 && mode != 1;
+  const bool x2 = !ck && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
-  const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc && kSwIncPark ? 3 : 0);
+  const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc ? 3 : 0);
   const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), inc)
                         : 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
   int rc = ctx->workspace(sizeof(float) * nws, &ws);

@@ -73,7 +73,7 @@ __device__ __forceinline__ void ck_two_stream_k(const V (&tau)[K], const V (&w0)
     const V RTd = rcp2(k[p] * (1.0f + em2k) + gamma1[p] * (1.0f - em2k));
     c[p].Rdif = RTd * gamma2[p] * (1.0f - em2k);
     c[p].Tdif = RTd * 2.0f * k[p] * emk[p];
-    const V gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? (V)0.5f : (2.0f - 3.0f * mu0 * g[p]) * .25f;
+    const V gamma3 = kG0 ? (V)0.5f : (2.0f - 3.0f * mu0 * g[p]) * .25f;
     const V gamma4 = 1.0f - gamma3;
     const V alpha1 = gamma1[p] * gamma4 + gamma2[p] * gamma3;
     const V alpha2 = gamma1[p] * gamma3 + gamma2[p] * gamma4;
@@ -305,9 +305,6 @@ __global__ void __launch_bounds__(512, WAVES)
     };
     walk(load1, body1, np1, [](int i) { return i; }, A1, B1);
   }
-#ifdef RRTMGPNN_ABL_SWCK_PASSES  // ablation builds only (timing of the passes; results are not produced)
-  if (RRTMGPNN_ABL_SWCK_PASSES < 2) return;
-#endif
   // ---- pass 2: bottom -> top adding; albedo / source checkpoint at every chunk top and at the surface ----
   V alb_b = ld_col(alb_dif);
   V src_b = Fd * ld_col(alb_dir);
@@ -358,9 +355,6 @@ __global__ void __launch_bounds__(512, WAVES)
     };
     walk(load2, body2, nck, [&](int i) { return nck - 1 - i; }, A, B);
   }
-#ifdef RRTMGPNN_ABL_SWCK_PASSES
-  if (RRTMGPNN_ABL_SWCK_PASSES < 3) return;
-#endif
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
   // idle lanes (past the block's columns) store their ring values to one spare slot instead of branching around the
   // stores; slots past the last level (the last chunk's padding layers) are written and never read
@@ -381,9 +375,6 @@ __global__ void __launch_bounds__(512, WAVES)
     }
   };
   auto flush = [&](int n, int lev0, int dl, int slot0 = 0) {
-#ifdef RRTMGPNN_ABL_SWCK_NO_FLUSH  // ablation builds only
-    return;
-#endif
     if (kCkFlushLanes && (ngpt & 3) == 0 && 3 * ncb * n * 4 <= (int)blockDim.x)
       ring_flush_sw_lanes<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
                                    flux_dir, rs, slot0);

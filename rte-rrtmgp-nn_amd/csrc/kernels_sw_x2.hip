@@ -37,16 +37,16 @@ struct SwCoef2 {
 };
 
 // sw_two_stream of kernels_rte.hip, term by term
-template <bool kG0 = false, bool kTn = false>
+template <bool kG0 = false>
 __device__ __forceinline__ SwCoef2 sw_two_stream2(f2 tau, f2 w0, f2 g, float mu0, float mu0_inv, f2 dir_inc,
-                                                 const uint64_t *etab, f2 Tn_in = (f2){0.0f, 0.0f})
+                                                 const uint64_t *etab)
 {
   const float eps = FLT_EPSILON;
   SwCoef2 c;
   const SwDif2 d = sw_dif2(tau, w0, g, etab);
   const f2 gamma1 = d.gamma1, gamma2 = d.gamma2, k = d.k, emk = d.emk, em2k = d.em2k;
-  const f2 Tnoscat = kTn ? Tn_in : exp2v_beam(-tau * mu0_inv, etab);  // kTn: pass 1's value of the same expression
-  const f2 gamma3 = (kG0 && RRTMGPNN_FASTOPS) ? splat(0.5f) : (2.0f - 3.0f * mu0 * g) * .25f;  // g == 0: exactly 0.5
+  const f2 Tnoscat = exp2v_beam(-tau * mu0_inv, etab);
+  const f2 gamma3 = kG0 ? splat(0.5f) : (2.0f - 3.0f * mu0 * g) * .25f;  // g == 0: exactly 0.5
   const f2 gamma4 = 1.0f - gamma3;
   const f2 alpha1 = gamma1 * gamma4 + gamma2 * gamma3;
   const f2 alpha2 = gamma1 * gamma3 + gamma2 * gamma4;
@@ -85,75 +85,25 @@ __device__ __forceinline__ void inc_2str2(f2 &t1, f2 &w1, f2 &g1, f2 t2, f2 w2, 
 }  // namespace
 
 // layers of inputs in flight per lane: 3 for the NN path's g = NULL kernel (C3 -1.5 %, C4 -2 %, no spill), 2 for the
-// kernels that also read g (3 spilled there) and for the fused cloud increment (RRTMGPNN_SW2_PF_INC)
-#ifndef RRTMGPNN_SW2_PF
-#define RRTMGPNN_SW2_PF 2
-#endif
-#ifndef RRTMGPNN_SW2_PF_NOG
-#define RRTMGPNN_SW2_PF_NOG 3
-#endif
-#ifndef RRTMGPNN_SW2_PF_INC
-#define RRTMGPNN_SW2_PF_INC 2
-#endif
-#ifndef RRTMGPNN_SW2_WAVES
-#define RRTMGPNN_SW2_WAVES 4
-#endif
-// RECOMP = 1: pass 3 recomputes the direct beam and the layer's full two-stream coefficients (S_dn included) instead
-// of reading them back (3 fewer plane transfers per launch: the S_dn store + load, the beam's second read, for the
-// ~250 VALU of a second sw_two_stream per g-point and layer).  RECOMP = 0 stores S_dn in pass 2 and reads it and the
-// beam back, so pass 3 evaluates only R_dif / T_dif.  Chosen per instantiation by whole-step A/B (tools/ab_trees.sh,
-// alternating runs of two trees on one box): the clear-sky NN path recomputes (storing was 1 % slower at C3); with the
-// fused cloud increment (formed again in pass 3, INC_RECOMP) storing is 4.5 % faster alone and the C4 step 4 % faster.
-// Storing more (R_dif / T_dif, the beam transmittance: STORE_DIF / STORE_TNS below) was 5-10 % slower: more planes
-// cost more than the VALU they save.
-#ifndef RRTMGPNN_SW2_RECOMP
-#define RRTMGPNN_SW2_RECOMP 1
-#endif
-#ifndef RRTMGPNN_SW2_RECOMP_INC
-#define RRTMGPNN_SW2_RECOMP_INC 0
-#endif
-constexpr bool kSw2RecompInc = RRTMGPNN_SW2_RECOMP_INC != 0;
-constexpr bool kSw2Recomp = RRTMGPNN_SW2_RECOMP != 0;
-#ifndef RRTMGPNN_SW2_RING
-#define RRTMGPNN_SW2_RING 6
-#endif
-constexpr int kSw2Ring = RRTMGPNN_SW2_RING;
-// Layer steps without the uniform `j < nlay` branch around their arithmetic: padding steps (nlay not a multiple of
-// the prefetch depth / ring) compute on the clamped last layer and a select keeps the recurrences' previous values.
-// One basic block per unrolled group lets the scheduler overlap the layer-independent coefficient algebra of the
-// kPF layers in flight (only the adding / beam recurrences chain them).  Used by the NN path's instantiation (g = NULL,
-// no increment): C3 SW solver -2 %; the all-sky (increment) instantiation was 2 % slower with it and keeps the branch.
-#ifndef RRTMGPNN_SW2_BRANCHLESS
-#define RRTMGPNN_SW2_BRANCHLESS 0
-#endif
-constexpr bool kSw2Branchless = RRTMGPNN_SW2_BRANCHLESS != 0;
-// Fused cloud increment: pass 3 forms the incremented (tau, ssa, g) again from the gas arrays and the band-resolved
-// cloud arrays (same expressions, same bits) instead of reading three g-resolved planes pass 2 parked in workspace:
-// 3 plane stores and 1 plane load fewer per launch (the band arrays are 16x smaller and stay in cache).
-#ifndef RRTMGPNN_SW2_INC_RECOMP
-#define RRTMGPNN_SW2_INC_RECOMP 1
-#endif
-constexpr bool kSw2IncRecomp = RRTMGPNN_SW2_INC_RECOMP != 0;
-// Trading VALU work for plane transfers.  In the benchmarked step the two chains share the chip's VALU issue slots
-// (every stage is throughput-bound), so an exp or a square root saved counts more than a plane moved:
-//  STORE_DIF: pass 2 stores R_dif, T_dif (two layer planes) and pass 3 reads them instead of tau, ssa (and the cloud
-//             arrays): pass 3 keeps only the adding arithmetic.  Needs the S_dn plane (RECOMP = 0).
-//  STORE_TNS: pass 1 stores the direct-beam transmittance (one layer plane) and pass 2 reads it instead of evaluating
-//             exp(-tau/mu0) again.
-#ifndef RRTMGPNN_SW2_STORE_DIF
-#define RRTMGPNN_SW2_STORE_DIF 0
-#endif
-#ifndef RRTMGPNN_SW2_STORE_TNS
-#define RRTMGPNN_SW2_STORE_TNS 0
-#endif
-constexpr bool kSw2StoreDif = RRTMGPNN_SW2_STORE_DIF != 0, kSw2StoreTns = RRTMGPNN_SW2_STORE_TNS != 0;
-static_assert(!(kSw2StoreDif && (kSw2Recomp || kSw2RecompInc)),
-              "STORE_DIF reads S_dn and the beam back (RRTMGPNN_SW2_RECOMP=0, RRTMGPNN_SW2_RECOMP_INC=0)");
-// layer planes of the x2 kernel's workspace after the 4 level planes: [inc park: tau, ssa, g][R_dif, T_dif][T_noscat]
-constexpr int kSw2Park = kSw2IncRecomp ? 0 : 3, kSw2DifOff = kSw2Park, kSw2TnOff = kSw2DifOff + (kSw2StoreDif ? 2 : 0);
+// kernels that also read g (3 spilled there) and for the fused cloud increment
+constexpr int kSw2Pf = 2, kSw2PfNoG = 3, kSw2PfInc = 2;
+constexpr int kSw2Waves = 4;  // __launch_bounds__ minimum waves per SIMD
+// Pass 3 of the clear-sky kernels recomputes the direct beam and the layer's full two-stream coefficients (S_dn
+// included) instead of reading them back (3 fewer plane transfers per launch: the S_dn store + load, the beam's second
+// read, for the ~250 VALU of a second sw_two_stream per g-point and layer); with the fused cloud increment pass 2
+// stores S_dn and pass 3 reads it and the beam back, evaluating only R_dif / T_dif.  Chosen per instantiation by
+// whole-step A/B (tools/ab_trees.sh, alternating runs of two trees on one box): the clear-sky NN path recomputes
+// (storing was 1 % slower at C3); with the increment storing is 4.5 % faster alone and the C4 step 4 % faster.
+// Storing more (R_dif / T_dif, the beam transmittance) was 5-10 % slower: more planes cost more than the VALU they
+// save; a branch-free layer step was 2 % slower with the increment and within noise without (rounds 1-2).
+constexpr bool kSw2Recomp = true, kSw2RecompInc = false;
+constexpr int kSw2Ring = 6;  // levels staged per ordered flush (2, 4, 8 were 2-25 % slower)
+// With the fused cloud increment, pass 3 forms the incremented (tau, ssa, g) again from the gas arrays and the
+// band-resolved cloud arrays (same expressions, same bits) instead of reading three g-resolved planes pass 2 would park
+// in workspace: 3 plane stores and 1 plane load fewer per launch (the band arrays are 16x smaller and stay in cache).
 
 template <bool kHasG, bool kInc, int kPF>
-__global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
+__global__ void __launch_bounds__(512, kSw2Waves)
     sw_2stream_x2_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
                          const float *__restrict__ ssa, const float *__restrict__ gg, const float *__restrict__ mu0p,
@@ -163,7 +113,6 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
                          float *__restrict__ flux_dn, float *__restrict__ flux_dir)
 {
   static_assert(kSw2Ring % kPF == 0, "prefetch depth must divide the ring");
-  constexpr bool kBl = kSw2Branchless && !kHasG && !kInc;
   constexpr bool kRc = kInc ? kSw2RecompInc : kSw2Recomp;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // `ncb` columns per block (as sw_2stream_kernel): lane t works on column c = t / (ngpt/2), g-points g, g + 1
@@ -185,11 +134,6 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
   const uint32_t bL = (uint32_t)nc * row * nlay, bV = (uint32_t)nc * row * nlev;
   const ColArr2 Ttau(tau, cl, bL), Tssa(ssa, cl, bL), Tg(kHasG ? gg : tau, cl, bL);
   const ColArr2 WA(ws, cv, bV), WB(ws + plane, cv, bV), WS(ws + 2 * plane, cv, bV), WD(ws + 3 * plane, cv, bV);
-  const size_t lplane = (size_t)ngpt * nlay * ncol;
-  float *wi = ws + 4 * plane;
-  const ColArr2 WT(wi, cl, bL), WW(wi + lplane, cl, bL), WG(wi + 2 * lplane, cl, bL);
-  const ColArr2 WRd(wi + kSw2DifOff * lplane, cl, bL), WTd(wi + (kSw2DifOff + 1) * lplane, cl, bL),
-      WTn(wi + kSw2TnOff * lplane, cl, bL);
   // band-resolved increments: one band offset per g-point of the pair
   const size_t cb = (size_t)bands.nbnd * nlay * icol0;
   const uint32_t brow = 4u * (uint32_t)bands.nbnd, vbc = (uint32_t)c * brow * nlay;
@@ -214,7 +158,7 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
   // ---- pass 1: direct beam ----
   // Straight-line layer steps as in sw_2stream_kernel: memory operations on every step (idle lanes and steps past
   // nlay store at kBufOOB), arithmetic alone under the uniform `j < nlay` branch.
-  const uint32_t vVs = on ? vV : kBufOOB, vLs = on ? vL : kBufOOB;
+  const uint32_t vVs = on ? vV : kBufOOB;
   f2 Fd = Ftop;
   WA.st(Fd, vVs, row * top);
   {
@@ -236,16 +180,7 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
           pt[p] = Ttau.ld(vL, row * ln);
           pi[p] = ld_bnd(Bt, ln);
         }
-        if constexpr (kBl) {
-          const f2 Tn = exp2v_beam(-t * mu0_inv, etab);
-          if constexpr (kSw2StoreTns) WTn.st(Tn, j < nlay ? vLs : kBufOOB, row * l);
-          const f2 Fn = Tn * Fd;
-          Fd = j < nlay ? Fn : Fd;  // uniform select
-        } else if (j < nlay) {
-          const f2 Tn = exp2v_beam(-t * mu0_inv, etab);
-          if constexpr (kSw2StoreTns) WTn.st(Tn, vLs, row * l);
-          Fd = Tn * Fd;
-        }
+        if (j < nlay) Fd = exp2v_beam(-t * mu0_inv, etab) * Fd;
         WA.st(Fd, j < nlay ? vVs : kBufOOB, row * lev_below(l));
       }
     }
@@ -256,11 +191,10 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
   WB.st(alb_b, vVs, row * sfcl);
   WS.st(src_b, vVs, row * sfcl);
   {
-    f2 pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF], pn[kPF];
+    f2 pt[kPF], pw[kPF], pg[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load2 = [&](int p, int l) {
       const uint32_t s = row * l;
       pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s); pf[p] = WA.ld(vV, row * lev_above(l));
-      if constexpr (kSw2StoreTns) pn[p] = WTn.ld(vL, s);
       if constexpr (kInc) {
         qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
@@ -272,33 +206,18 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
       for (int p = 0; p < kPF; p++) {
         const int j = j0 + p;
         const int l = lay_of_up(min(j, nlay - 1));
-        const uint32_t vs = j < nlay ? vVs : kBufOOB, vls = j < nlay ? vLs : kBufOOB;
+        const uint32_t vs = j < nlay ? vVs : kBufOOB;
         f2 t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : splat(0.0f);
-        const f2 Fin = pf[p], Tn = kSw2StoreTns ? pn[p] : splat(0.0f);
-        if constexpr (kInc) {
-          inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
-          if constexpr (!kSw2IncRecomp) {
-            WT.st(t, vls, row * l);
-            WW.st(w0, vls, row * l);
-            WG.st(g0, vls, row * l);
-          }
-        }
+        const f2 Fin = pf[p];
+        if constexpr (kInc) inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
         load2(p, lay_of_up(min(j + kPF, nlay - 1)));
         f2 alb = alb_b, src = src_b, Sdn = splat(0.0f);
-        if (kBl || j < nlay) {
-          const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc, kSw2StoreTns>(t, w0, g0, mu0, mu0_inv, Fin, etab, Tn);
-          if constexpr (kSw2StoreDif) {
-            WRd.st(cf.Rdif, vls, row * l);
-            WTd.st(cf.Tdif, vls, row * l);
-          }
+        if (j < nlay) {
+          const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fin, etab);
           const f2 denom = rcp2(1.0f - cf.Rdif * alb_b);
           alb = cf.Rdif + cf.Tdif * cf.Tdif * alb_b * denom;
           src = cf.Sup + cf.Tdif * denom * (src_b + alb_b * cf.Sdn);
           Sdn = cf.Sdn;
-          if constexpr (kBl) {
-            alb = j < nlay ? alb : alb_b;
-            src = j < nlay ? src : src_b;
-          }
         }
         const uint32_t sa = row * lev_above(l);
         WB.st(alb, vs, sa);
@@ -329,14 +248,8 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
     f2 pt[kPF], pw[kPF], pg[kPF], pd[kPF], pa[kPF], ps[kPF], pf[kPF], qt[kPF], qw[kPF], qg[kPF];
     auto load = [&](int p, int l) {
       const uint32_t s = row * l, sb = row * lev_below(l);
-      if constexpr (kSw2StoreDif) {
-        pt[p] = WRd.ld(vL, s); pw[p] = WTd.ld(vL, s);  // R_dif, T_dif
-      } else if constexpr (kInc && !kSw2IncRecomp) {
-        pt[p] = WT.ld(vL, s); pw[p] = WW.ld(vL, s); pg[p] = WG.ld(vL, s);
-      } else {
-        pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s);
-      }
-      if constexpr (kInc && kSw2IncRecomp && !kSw2StoreDif) {
+      pt[p] = Ttau.ld(vL, s); pw[p] = Tssa.ld(vL, s); pg[p] = ld_g(s);
+      if constexpr (kInc) {
         qt[p] = ld_bnd(Bt, l); qw[p] = ld_bnd(Bw, l); qg[p] = ld_bnd(Bg, l);
       }
       pa[p] = WB.ld(vV, sb); ps[p] = WS.ld(vV, sb);
@@ -352,13 +265,12 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
 #pragma unroll
       for (int r = 0; r < kSw2Ring; r++) {
         const int j = j0 + r, p = r % kPF;
-        f2 t = pt[p], w0 = pw[p], g0 = (kHasG || (kInc && !kSw2IncRecomp)) ? pg[p] : splat(0.0f);
-        if constexpr (kInc && kSw2IncRecomp && !kSw2StoreDif) inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
+        f2 t = pt[p], w0 = pw[p], g0 = kHasG ? pg[p] : splat(0.0f);
+        if constexpr (kInc) inc_2str2(t, w0, g0, qt[p], qw[p], qg[p]);
         const f2 alb = pa[p], src = ps[p];
         f2 Rdif, Tdif, Sdn = kRc ? splat(0.0f) : pd[p], Fdir = kRc ? splat(0.0f) : pf[p];
         load(p, lay_of_down(min(j + kPF, nlay - 1)));
-        // branchless: padding steps only come after the last layer, and their ring rows are never flushed
-        if (kBl || j < nlay) {
+        if (j < nlay) {
           if constexpr (kRc) {
             // pass 2's coefficients from the same inputs (same bits), the beam from pass 1's recurrence
             const SwCoef2 cf = sw_two_stream2<!kHasG && !kInc>(t, w0, g0, mu0, mu0_inv, Fd3, etab);
@@ -367,9 +279,6 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
             Sdn = cf.Sdn;
             Fd3 = cf.Tnoscat * Fd3;
             Fdir = Fd3;
-          } else if constexpr (kSw2StoreDif) {
-            Rdif = t;
-            Tdif = w0;
           } else {
             const SwDif2 d = sw_dif2(t, w0, g0, etab);
             Rdif = d.Rdif;
@@ -386,12 +295,8 @@ __global__ void __launch_bounds__(512, RRTMGPNN_SW2_WAVES)
   }
 }
 
-// layer planes (ngpt x nlay x ncol floats) the x2 kernel needs after its 4 level planes
-size_t sw_2stream_x2_layer_planes(bool inc)
-{
-  const size_t extra = (kSw2StoreDif ? 2 : 0) + (kSw2StoreTns ? 1 : 0);
-  return (inc || extra ? (size_t)kSw2Park : 0) + extra;  // the extra planes sit after the park planes
-}
+// layer planes (ngpt x nlay x ncol floats) the x2 kernel needs after its 4 level planes: none
+size_t sw_2stream_x2_layer_planes(bool) { return 0; }
 
 // ngpt even and <= 256; workspace: 4 level planes + sw_2stream_x2_layer_planes(inc) layer planes
 int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
@@ -402,18 +307,15 @@ int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
 {
   // Columns per block: 2 (224 g-points: 224 lanes in 4 waves, 32 idle, a 32 KB ring).  Four columns fill 7 waves
   // exactly and were 5 % faster alone at C4, but in the overlapped step the smaller blocks share the CUs better with
-  // the LW chain: whole step C3 -1.7 %, C4 -3.5 % (tools/ab_env.sh RRTMGPNN_LIB).  0: columns_per_block (fewest idle).
-#ifndef RRTMGPNN_SW_NCB
-#define RRTMGPNN_SW_NCB 2
-#endif
-  const int ncb = RRTMGPNN_SW_NCB > 0 && RRTMGPNN_SW_NCB * (ngpt / 2) <= 512 ? RRTMGPNN_SW_NCB : columns_per_block(ngpt / 2);
+  // the LW chain: whole step C3 -1.7 %, C4 -3.5 % (tools/ab_env.sh RRTMGPNN_LIB).
+  const int ncb = 2 * (ngpt / 2) <= 512 ? 2 : columns_per_block(ngpt / 2);
   const int threads = (ncb * (ngpt / 2) + 63) / 64 * 64;
   const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * kSw2Ring * ngpt);
   if (lds > 160 * 1024) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: LDS ring exceeds 160 KiB");
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
   const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
-  constexpr int PF = RRTMGPNN_SW2_PF, PFN = RRTMGPNN_SW2_PF_NOG, PFI = RRTMGPNN_SW2_PF_INC;
+  constexpr int PF = kSw2Pf, PFN = kSw2PfNoG, PFI = kSw2PfInc;
   auto go = [&](auto kern, const float *tb, const float *sb, const float *gb) -> int {
     // rings past 64 KiB (4 columns of 224 g-points: 64.5 KiB) need the dynamic-LDS limit raised (per device)
     if (lds > 64 * 1024)

@@ -30,19 +30,8 @@ __device__ __forceinline__ float pow8(float t)
   return t4 * t4;
 }
 
-#ifndef RRTMGPNN_MLP_FASTDIV
-#define RRTMGPNN_MLP_FASTDIV 1
-#endif
-
-// softsign (neural/mod_activation.F90:107-128).  FASTDIV: libm_ref.hpp div_softsign (reciprocal and two residual
-// corrections), equal to the IEEE quotient for every |x| < 2^126, checked exhaustively on the GPU
-__device__ __forceinline__ float softsign(float x)
-{
-#if RRTMGPNN_MLP_FASTDIV
-  return div_softsign(x, fabsf(x) + 1.0f);
-#else
-  return x / (fabsf(x) + 1.0f);
-#endif
-}
+// softsign (neural/mod_activation.F90:107-128) with libm_ref.hpp div_softsign (reciprocal and two residual
+// corrections), equal to the IEEE quotient x / (|x| + 1) for every |x| < 2^126, checked exhaustively on the GPU
+__device__ __forceinline__ float softsign(float x) { return div_softsign(x, fabsf(x) + 1.0f); }
 
 }  // namespace rrtmgpnn

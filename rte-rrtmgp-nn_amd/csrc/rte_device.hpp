@@ -22,20 +22,9 @@ __device__ __forceinline__ int band_of(const BandArgs &b, int g)
 
 static constexpr int kExpTabOff = 0, kExpTabFloats = 64;  // exp table (32 x u64) at the front of LDS
 
-// RRTMGPNN_FASTOPS (default 1; 0 for tools/solver_variants.sh A/B runs): the solvers' divisions whose operands stay
-// in the normal range use div_rn_normal, and their exps of non-positive arguments ref_expf_neg (libm_ref.hpp).
-// Same bits either way; fewer instructions per layer step.
-#ifndef RRTMGPNN_FASTOPS
-#define RRTMGPNN_FASTOPS 1
-#endif
-__device__ __forceinline__ float solver_div(float a, float b)
-{
-#if RRTMGPNN_FASTOPS
-  return div_rn_normal(a, b);
-#else
-  return a / b;
-#endif
-}
+// The solvers' divisions whose operands stay in the normal range use div_rn_normal, and their exps of non-positive
+// arguments ref_expf_neg (libm_ref.hpp): the bits of a / b and of glibc's expf, in fewer instructions.
+__device__ __forceinline__ float solver_div(float a, float b) { return div_rn_normal(a, b); }
 // RRTMGPNN_FAST_LIBM (opt-in tolerance build, librrtmgpnn_fastlibm.so; never the default): the solvers' exps of
 // non-positive arguments use the hardware exponential (v_exp_f32, a few ulp) instead of glibc's algorithm
 // evaluated in double.  Fluxes then differ from the reference's in the last bits; tests/test_gpu_tolerance.py holds
@@ -46,14 +35,7 @@ __device__ __forceinline__ float solver_div(float a, float b)
 // The direct-beam transmittance exp(-tau/mu0) multiplies down every layer of a column, so its rounding errors compound:
 // it keeps glibc's algorithm in the tolerance build too (with the hardware exp there, C3 SW down-flux errors reached
 // 1.0e-3 W/m2 RMS, the north star's bar itself).
-__device__ __forceinline__ float solver_exp_beam(float x, const uint64_t *tab)
-{
-#if RRTMGPNN_FASTOPS || RRTMGPNN_FAST_LIBM
-  return ref_expf_neg(x, tab);
-#else
-  return ref_expf_nb(x, tab);
-#endif
-}
+__device__ __forceinline__ float solver_exp_beam(float x, const uint64_t *tab) { return ref_expf_neg(x, tab); }
 __device__ __forceinline__ float solver_exp_neg(float x, const uint64_t *tab)
 {
 #if RRTMGPNN_FAST_LIBM
@@ -67,10 +49,8 @@ __device__ __forceinline__ float solver_exp_neg(float x, const uint64_t *tab)
   e = fmaf(x, L_lo, e);
   const float r = __builtin_amdgcn_exp2f(t);
   return (x < -0x1.9fe368p6f) ? 0.0f : fmaf(r, e * LN2, r);
-#elif RRTMGPNN_FASTOPS
-  return ref_expf_neg(x, tab);
 #else
-  return ref_expf_nb(x, tab);
+  return ref_expf_neg(x, tab);
 #endif
 }
 
@@ -124,11 +104,7 @@ __device__ __forceinline__ void ring_flush(const float *ring, float *part, int n
 {
   __syncthreads();
   const int t = threadIdx.x;
-#ifdef RRTMGPNN_ABL_NO_REDUCE
-  if (false) {
-#else
   if (t < nq * n) {
-#endif
     const int q = t / n, c = t - q * n;
     const float *r = ring + ((size_t)q * R + c) * ngpt;
     const float *r2 = ring + ((size_t)2 * R + c) * ngpt;
@@ -196,16 +172,10 @@ __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n,
                                               int icol0, int ncol, float *o_up, float *o_dn, float *o_dir,
                                               int stride = 0, int slot0 = 0)
 {
-#ifndef RRTMGPNN_ABL_FLUSH_NOBAR  // ablation builds only (timing; results are not produced)
   __syncthreads();
-#endif
   const int t = threadIdx.x;
   const int rs = stride ? stride : ngpt;
-#ifdef RRTMGPNN_ABL_FLUSH_NOWORK
-  if (false) {
-#else
   if (t < 3 * ncb * n) {
-#endif
     const int c = t / (3 * n), rem = t - c * 3 * n, q = rem / n, s = rem - q * n;
     const float *rc = ring + (size_t)c * 3 * R * rs;
     const float *r = rc + ((size_t)q * R + slot0 + s) * rs;
@@ -238,9 +208,7 @@ __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n,
       o[lev0 + s * dl + (size_t)nlev * icol] = ((s0 + s1) + s2) + s3;
     }
   }
-#ifndef RRTMGPNN_ABL_FLUSH_NOBAR
   __syncthreads();
-#endif
 }
 
 // The same sums with one lane per partial (ngpt % 4 == 0): lane (q, c, s, j) walks partial j of quantity q, column c,

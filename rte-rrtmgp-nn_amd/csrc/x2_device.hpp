@@ -52,15 +52,11 @@ __device__ __forceinline__ f2 rcp2(f2 b)
 // solver_div (rte_device.hpp) with the Newton fmas paired
 __device__ __forceinline__ f2 div2(f2 a, f2 b)
 {
-#if RRTMGPNN_FASTOPS
   f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
   r = vfma(vfma(-b, r, splat(1.0f)), r, r);
   f2 q = a * r;
   q = vfma(vfma(-b, q, a), r, q);
   return vfma(vfma(-b, q, a), r, q);
-#else
-  return a / b;
-#endif
 }
 
 // The same helpers for one g-point per lane: the scalar functions they pair (same bits element by element)
@@ -75,7 +71,7 @@ __device__ __forceinline__ float div2(float a, float b) { return solver_div(a, b
 template <int N, class V>
 __device__ __forceinline__ void exp_neg_batch(const V (&x)[N], V (&y)[N], const uint64_t *etab)
 {
-#if RRTMGPNN_FASTOPS && !RRTMGPNN_FAST_LIBM
+#if !RRTMGPNN_FAST_LIBM
   constexpr int L = sizeof(V) / sizeof(float);
   float xs[N * L], ys[N * L];
 #pragma unroll
@@ -91,7 +87,6 @@ __device__ __forceinline__ void exp_neg_batch(const V (&x)[N], V (&y)[N], const 
 template <int N, class V>
 __device__ __forceinline__ void exp_beam_batch(const V (&x)[N], V (&y)[N], const uint64_t *etab)
 {
-#if RRTMGPNN_FASTOPS || RRTMGPNN_FAST_LIBM
   constexpr int L = sizeof(V) / sizeof(float);
   float xs[N * L], ys[N * L];
 #pragma unroll
@@ -99,10 +94,6 @@ __device__ __forceinline__ void exp_beam_batch(const V (&x)[N], V (&y)[N], const
   ref_expf_neg_batch<N * L>(xs, ys, etab);
 #pragma unroll
   for (int i = 0; i < N; i++) __builtin_memcpy(&y[i], &ys[i * L], sizeof(V));
-#else
-#pragma unroll
-  for (int i = 0; i < N; i++) y[i] = exp2v_beam(x[i], etab);
-#endif
 }
 
 // 8-byte column-local loads and stores (g-point pair at byte offset voff, layer at soff)

@@ -61,8 +61,13 @@ def spawn_ranks(n, script, argv, visible_devices):
     if visible_devices < n:
         env.setdefault("RRTMGPNN_DIST_BACKEND", "gloo")
     env["RRTMGPNN_VISIBLE_DEVICES"] = str(visible_devices)
-    r = subprocess.run(launch_command(n, script, argv, free_port()), env=env)
-    return r.returncode
+    # the ranks' stdout is filtered: JSON lines (rank 0's result line) pass to stdout, everything else (gloo and
+    # launcher chatter) goes to stderr, so the caller still reads one JSON line
+    p = subprocess.Popen(launch_command(n, script, argv, free_port()), env=env, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
 
 
 def slab_checksum(x):

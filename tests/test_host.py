@@ -172,8 +172,9 @@ def test_bench_rejects_gpus_world_mismatch():
     assert r.returncode == 2 and "disagrees" in r.stderr
 
 
-def test_spawn_ranks_starts_n_processes(tmp_path):
-    """spawn_ranks runs the script as N torch.distributed.run ranks (no GPU: the script only reports its env)."""
+def test_spawn_ranks_starts_n_processes(tmp_path, capsys):
+    """spawn_ranks runs the script as N torch.distributed.run ranks (no GPU: the script only reports its env); of the
+    ranks' stdout only JSON lines reach stdout (rank 0's result line), the rest goes to stderr."""
     from rrtmgpnn import shard
     out = tmp_path / "ranks"
     out.mkdir()
@@ -181,7 +182,9 @@ def test_spawn_ranks_starts_n_processes(tmp_path):
     script.write_text("import os, sys\n"
                       "open(os.path.join(sys.argv[1], os.environ['RANK']), 'w').write("
                       "'%s %s %s %s' % (os.environ['WORLD_SIZE'], os.environ['LOCAL_RANK'], "
-                      "os.environ.get('RRTMGPNN_DIST_BACKEND'), sys.argv[2]))\n")
+                      "os.environ.get('RRTMGPNN_DIST_BACKEND'), sys.argv[2]))\n"
+                      "print('[chatter] rank', os.environ['RANK'], flush=True)\n"
+                      "if os.environ['RANK'] == '0': print('{\"rank\": 0}', flush=True)\n")
     env_backup = os.environ.pop("RRTMGPNN_DIST_BACKEND", None)
     try:
         rc = shard.spawn_ranks(2, str(script), [str(out), "--gpus"], visible_devices=1)
@@ -191,6 +194,9 @@ def test_spawn_ranks_starts_n_processes(tmp_path):
     assert rc == 0
     got = sorted((p.name, p.read_text()) for p in out.iterdir())
     assert got == [("0", "2 0 gloo --gpus"), ("1", "2 1 gloo --gpus")]
+    cap = capsys.readouterr()
+    assert cap.out.strip() == '{"rank": 0}'
+    assert "[chatter] rank 0" in cap.err and "[chatter] rank 1" in cap.err
 
 
 def test_synthetic_problem_column_ranges_are_slices_of_the_whole():
