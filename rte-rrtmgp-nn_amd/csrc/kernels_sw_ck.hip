@@ -52,8 +52,15 @@ __device__ __forceinline__ void ck_two_stream_k(const V (&tau)[K], const V (&w0)
   V gamma1[K], gamma2[K], k[K], arg[K], emk[K];
 #pragma unroll
   for (int p = 0; p < K; p++) {
-    gamma1[p] = (8.0f - w0[p] * (5.0f + 3.0f * g[p])) * .25f;
-    gamma2[p] = 3.0f * (w0[p] * (1.0f - g[p])) * .25f;
+    if constexpr (kG0) {
+      // g = 0: one rounding of the value the reference rounds at 4x and scales back exactly -- the same bits for
+      // every |ssa| < 6.8e37 (tools/check_sw_identities.py walks all of those floats), two operations fewer
+      gamma1[p] = 2.0f - w0[p] * 1.25f;
+      gamma2[p] = w0[p] * .75f;
+    } else {
+      gamma1[p] = (8.0f - w0[p] * (5.0f + 3.0f * g[p])) * .25f;
+      gamma2[p] = 3.0f * (w0[p] * (1.0f - g[p])) * .25f;
+    }
     k[p] = sqrt2(vmax((gamma1[p] - gamma2[p]) * (gamma1[p] + gamma2[p]), (V)k_min));
     arg[p] = -tau[p] * k[p];
   }
@@ -75,8 +82,10 @@ __device__ __forceinline__ void ck_two_stream_k(const V (&tau)[K], const V (&w0)
     c[p].Tdif = RTd * 2.0f * k[p] * emk[p];
     const V gamma3 = kG0 ? (V)0.5f : (2.0f - 3.0f * mu0 * g[p]) * .25f;
     const V gamma4 = 1.0f - gamma3;
-    const V alpha1 = gamma1[p] * gamma4 + gamma2[p] * gamma3;
-    const V alpha2 = gamma1[p] * gamma3 + gamma2[p] * gamma4;
+    // g = 0 (gamma3 = gamma4 = 1/2): alpha1 = alpha2 = (gamma1 + gamma2) / 2, the sum k's radicand already formed
+    // (same bits, tools/check_sw_identities.py)
+    const V alpha1 = kG0 ? (gamma1[p] + gamma2[p]) * .5f : gamma1[p] * gamma4 + gamma2[p] * gamma3;
+    const V alpha2 = kG0 ? alpha1 : gamma1[p] * gamma3 + gamma2[p] * gamma4;
     const V k2e = 2.0f * k[p] * emk[p];
     const V k_mu = k[p] * mu0, k_mu2 = k_mu * k_mu, k_g3 = k[p] * gamma3, k_g4 = k[p] * gamma4;
     const V dd = ck_eps_guard(1.0f - k_mu2, eps);
@@ -127,16 +136,19 @@ constexpr int kCkWavesNN = 4;
 
 // kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
 // broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
-// Small grids (the clear-sky instance when the grid fits in one round of resident waves, e.g. C3): K = 4 layers per
-// chunk at 2 waves per SIMD (more independent layers per wave where there are too few waves to hide the exps'
-// latency), ring of 8 levels.  Whole-step A/B at C3 (one box, alternating): +1.3 %, SW solver -2.4 %; a ring of 4 was
+// Small grids (the clear-sky instance when the grid fits in one round of resident waves, e.g. C3): 2 waves per SIMD
+// as the register floor (more independent layers per wave where there are too few waves to hide the exps' latency);
+// chunk length and ring below.  Whole-step A/B at C3 (one box, alternating): +1.3 %, SW solver -2.4 %; a ring of 4 was
 // 3 % slower, K = 2 at 4 waves +0.5 %.  With many columns (C4, C5) K = 3 at 3-4 waves stays (K = 4 was 13 % slower).
 // The small-grid instance also keeps pass 1's beam transmittances exp(-tau/mu0) in a workspace plane that passes 2 and
 // 3 read instead of evaluating the exp again, and pass 2's exp(-tau k) in a second plane that pass 3 reads (C3: SW
 // solver -3.7 %, step -3.7 %, alternating A/B on one box).  One g-point per lane (twice the waves to hide latency with;
 // packed fp32 issues at the same cost per element as scalar fp32 on gfx950, tools/valu_rates.hip) measured slower than
 // two, and so did the transmittance plane in the all-sky (fused-increment) instances.
-constexpr int kCkKSmall = 4, kCkRingSmall = 8, kCkWavesSmall = 2;
+// Round 4 (alone, alternating, bitwise; with the fence-free walk): K = 3 with a ring of 9 levels (three chunks per
+// flush, 7 flushes per column instead of 8) -2.3 % against K = 4 / ring 8; K = 3 / ring 6 +3 %, K = 2 / ring 6 +5 %,
+// K = 5 / ring 10 equal; a 3-wave floor equal.  A ring of 12 levels would not leave room for three blocks per CU.
+constexpr int kCkKSmall = 3, kCkRingSmall = 9, kCkWavesSmall = 2;
 constexpr bool kCkTnSmall = true, kCkEmkSmall = true;
 using VSmall = f2;
 
@@ -257,15 +269,15 @@ __global__ void __launch_bounds__(512, WAVES)
   // buffer while this one is computed, so no copy waits for them at the end of the step.  body(buf, ck, valid)
   // computes chunk ck; idx(i) is the pass's i-th chunk.  With an odd count the last step's second body runs on the
   // last chunk again with valid = false (no state change, no stores), so that no branch separates a prefetch from its
-  // use (the compiler sinks loads past such a branch); the scheduling fences keep each prefetch ahead of the compute.
+  // use (the compiler sinks loads past such a branch).  No scheduling fences between the loads and the bodies: the
+  // scheduler may then start a chunk's independent coefficient algebra under the previous chunk's recurrence (round
+  // 4: C3 SW solver -0.6 to -2.5 %, C4 -1.1 %, tools/kernel_ab.py).
   auto walk = [&](auto &&load, auto &&body, int count, auto &&idx, auto &A, auto &B) {
     load(A, idx(0));
     for (int i = 0; i < count; i += 2) {
       load(B, idx(min(i + 1, count - 1)));
-      __builtin_amdgcn_sched_barrier(0);
       body(A, idx(i), true);
       load(A, idx(min(i + 2, count - 1)));
-      __builtin_amdgcn_sched_barrier(0);
       body(B, idx(min(i + 1, count - 1)), i + 1 < count);
     }
   };
@@ -382,8 +394,12 @@ __global__ void __launch_bounds__(512, WAVES)
       ring_flush_sw<R, kGpt>(smem + kExpTabFloats, ncb, n, lev0, dl, ngpt, nlev, icol0, ncol, flux_up, flux_dn,
                              flux_dir, rs, slot0);
   };
-  // the ring holds M = R / K chunks; the block flushes it when it is full (a barrier, the ordered sums, a barrier)
+  // the ring holds M = R / K chunks; the block flushes it when it is full (a barrier, the ordered sums, a barrier).
+  // Flush phases are staggered between blocks: block b's first fill starts at chunk slot b % M, so the blocks that
+  // share a CU (dispatched 256 apart) flush at different chunks and one's latency-bound ordered sums run beside the
+  // others' layer arithmetic, instead of every block of the chip flushing at once.
   constexpr int M = R / K;
+  const int phase = (int)(blockIdx.x % (unsigned)M);
   V Fdn = inc_dif ? ld_col(inc_dif) : (V)0.0f;
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top, true);
   flush(1, top, 1);
@@ -434,7 +450,7 @@ __global__ void __launch_bounds__(512, WAVES)
         }
       }
       // fluxes down the chunk (adding :1583-1591, Eqs 12-13)
-      const int rbase = (ck % M) * K;
+      const int rbase = ((ck + phase) % M) * K;
 #pragma unroll
       for (int p = 0; p < K; p++) {
         const V fdn = (cf[p].Tdif * Fdn + cf[p].Rdif * S[p] + cf[p].Sdn) * D[p];
@@ -442,8 +458,9 @@ __global__ void __launch_bounds__(512, WAVES)
         put(fdn * Al[p] + S[p], fdn, Fdir[p], rbase + p, top + dl_dn * (ck * K + p + 1), p < n);
       }
       if (valid && (rbase + K == R || ck == nck - 1)) {
-        const int j0 = ck * K - rbase;  // first layer of this ring's levels
-        flush(min(R, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
+        const int s0 = ck < M - phase ? phase * K : 0;  // the first fill starts at the block's phase
+        const int j0 = ck * K - (rbase - s0);           // first layer of this fill's levels
+        flush(min(rbase + K - s0, nlay - j0), top + dl_dn * (j0 + 1), dl_dn, s0);
       }
     };
     walk(load3, body3, nck, [](int i) { return i; }, A, B);

@@ -98,16 +98,17 @@ struct LwAngles {
 // the float4 at m is g = 4m + k, so the 4 interleaved partials advance together, each in g order.
 // dn_mode (SW): quantity 1 is accumulated as (s + ring1) + ring2, i.e. sums_dn + radn_dn + radn_dir.
 // ngpt % 4 != 0, or seq: the reference uses sum(radn, 1) instead (one sequential sum, kept in partial 0).
+// slot0: the first staged slot (the levels sit in slots slot0 .. slot0 + n - 1)
 template <int R>
 __device__ __forceinline__ void ring_flush(const float *ring, float *part, int nq, int n, int lev0, int dl, int ngpt,
-                                           int nlev, bool dn_mode, bool seq = false)
+                                           int nlev, bool dn_mode, bool seq = false, int slot0 = 0)
 {
   __syncthreads();
   const int t = threadIdx.x;
   if (t < nq * n) {
     const int q = t / n, c = t - q * n;
-    const float *r = ring + ((size_t)q * R + c) * ngpt;
-    const float *r2 = ring + ((size_t)2 * R + c) * ngpt;
+    const float *r = ring + ((size_t)q * R + slot0 + c) * ngpt;
+    const float *r2 = ring + ((size_t)2 * R + slot0 + c) * ngpt;
     const bool dn = dn_mode && q == 1;
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
     if ((ngpt & 3) == 0 && !seq) {
@@ -140,14 +141,15 @@ __device__ __forceinline__ void ring_flush(const float *ring, float *part, int n
 // partial j of slot s (ring rows `stride` floats apart) and stores it to part[lev][j] -- the same partial sums as
 // ring_flush's float4 walk, in the same order, with a quarter of its instructions on the flushing wave.  With rows
 // padded to stride = ngpt + 4 the lanes' rows start in different LDS banks.
+// slot0: the first staged slot (the levels sit in slots slot0 .. slot0 + n - 1)
 __device__ __forceinline__ void ring_flush_lanes(const float *ring, int stride, float *part, int n, int lev0, int dl,
-                                                 int ngpt)
+                                                 int ngpt, int slot0 = 0)
 {
   __syncthreads();
   const int t = threadIdx.x;
   if (t < 4 * n) {
     const int sl = t >> 2, j = t & 3;
-    const float *r = ring + (size_t)sl * stride + j;
+    const float *r = ring + (size_t)(slot0 + sl) * stride + j;
     const int n4 = ngpt >> 2;
     float sum = 0.0f;
 #pragma unroll 8

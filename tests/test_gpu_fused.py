@@ -25,7 +25,8 @@ def dev():
 
 
 def T(a, dev):
-    return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
+    # a copy: a flipped (n, 1) array counts as contiguous to numpy but keeps its negative stride, which torch refuses
+    return torch.as_tensor(np.array(a, dtype=np.float32, order="C", copy=True), device=dev)
 
 
 def _flip(prob):
@@ -277,3 +278,41 @@ def test_fused_gas_optics_special_pressures(dev, rfmip, mlp_kernel):
         assert np.isnan(a).any() == np.isnan(b).any(), k
         np.testing.assert_array_equal(a.view(np.uint32)[~np.isnan(a)], b.view(np.uint32)[~np.isnan(b)], err_msg=str(k))
         np.testing.assert_array_equal(np.isnan(a), np.isnan(b), err_msg=str(k))
+
+
+@pytest.mark.parametrize("nlay", [1, 7, 37, 64, 65, 71, 137])
+@pytest.mark.parametrize("top_at_1", [True, False])
+@pytest.mark.parametrize("lw_ds", [False, True])
+def test_fused_lw_any_nlay(dev, orc, nlay, top_at_1, lw_ds):
+    """The one-angle fused LW solver on synthetic columns of 1 to 137 layers (odd and even, shorter and longer than
+    its ring of 8 levels and its prefetch depth, the C5 depth) in both orientations, with and without rte_lw's lw_Ds,
+    against the oracle."""
+    from rrtmgpnn import _lib, data
+    from rrtmgpnn._lib import check, float_array, int_array
+    from rrtmgpnn.api import GAUSS_DS, GAUSS_WTS, context
+    prob = data.synthetic_problem(23, nlay, seed=11)
+    if not top_at_1:
+        prob = _flip(prob)
+    kd = data.load_kdist("lw")
+    go = orc.lw_gas_optics(prob, [data.load_model("lw_abs"), data.load_model("lw_pfrac")], kd)
+    ncol, _, ngpt = go["tau"].shape
+    emis = np.repeat(np.asarray(prob["sfc_emis"], np.float32)[:, None], ngpt, axis=1)
+    ds = (np.random.default_rng(nlay).uniform(1.0, 2.5, size=ngpt * ncol).astype(np.float32) if lw_ds else None)
+    up_o, dn_o = orc.lw_solver(go["tau"], go["lay_source"], go["lev_source"], emis, go["sfc_source"], top_at_1, 1,
+                               lw_Ds=ds)
+    sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
+    up, dn = torch.full((ncol, nlay + 1), float("nan"), device=dev), torch.full((ncol, nlay + 1), float("nan"),
+                                                                               device=dev)
+    args = [T(go["tau"], dev), T(go["pfrac"], dev), T(prob["tlay"], dev), T(prob["tlev"], dev), T(prob["tsfc"], dev),
+            T(kd["totplnk"], dev), T(emis, dev)]
+    dsd = T(ds, dev) if lw_ds else None
+    check(_lib.lib().rrtmgpnn_lw_solver_noscat_planck_gpt(
+        context(0).h, ngpt, nlay, ncol, int(top_at_1), 1, float_array(GAUSS_DS[1]), float_array(GAUSS_WTS[1]),
+        dsd.data_ptr() if lw_ds else None, None, args[0].data_ptr(), args[1].data_ptr(), kd["nband"],
+        kd["nPlanckTemp"], args[2].data_ptr(), args[3].data_ptr(), args[4].data_ptr(), sfc_lay,
+        int_array(kd["band_lims_gpt"].ravel()), float(kd["temp_ref_min"][0]), float(kd["totplnk_delta"]),
+        args[5].data_ptr(), 0, args[6].data_ptr(), up.data_ptr(), dn.data_ptr(), None, None),
+        "lw_solver_noscat_planck_gpt")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(up.cpu().numpy(), up_o)
+    np.testing.assert_array_equal(dn.cpu().numpy(), dn_o)

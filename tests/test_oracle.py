@@ -193,3 +193,21 @@ def test_gpt_fluxes_and_lw_ds_bitwise_vs_reference(orc, rfmip, models, top_at_1)
     got = orc.sw_solver(t2, w2, g2, mu0, toa, alb, alb, top_at_1, gpt=True)
     for a, b, what in zip(got, want, ("up", "dn", "dir", "gpt_up", "gpt_dn", "gpt_dir")):
         np.testing.assert_array_equal(a, b, err_msg="sw " + what)
+
+
+def test_sw_g0_identities_sampled():
+    """The exact g = 0 rewrites of sw_two_stream's gamma1, gamma2 and alpha1 = alpha2 in the checkpointed SW kernel
+    (kernels_sw_ck.hip): every subnormal and every 13th float of [0, 4] against the reference expressions
+    (tools/check_sw_identities.py walks every float with |ssa| < 6.8e37)."""
+    import numpy as np
+    f = np.float32
+    hi = int(np.float32(4).view(np.uint32))
+    bits = np.concatenate([np.arange(0, 1 << 23, dtype=np.uint32), np.arange(1 << 23, hi, 13, dtype=np.uint32)])
+    w = bits.view(np.float32)
+    g1_ref = (f(8) - w * (f(5) + f(3) * f(0))) * f(.25)
+    g2_ref = f(3) * (w * (f(1) - f(0))) * f(.25)
+    a_ref = g1_ref * f(.5) + g2_ref * f(.5)
+    g1, g2 = f(2) - w * f(1.25), w * f(.75)
+    np.testing.assert_array_equal(g1.view(np.uint32), g1_ref.view(np.uint32))
+    np.testing.assert_array_equal(g2.view(np.uint32), g2_ref.view(np.uint32))
+    np.testing.assert_array_equal(((g1 + g2) * f(.5)).view(np.uint32), a_ref.view(np.uint32))

@@ -30,9 +30,55 @@ ABLATIONS = {
                        "  // ablation mlp32_nostore\n", "replace")],
 }
 
+# Variants that keep the bits (tools/kernel_ab.py checks them bitwise against the default library): A/B candidates
+ABLATIONS.update({
+    # SW checkpointed solver: scheduling fences between a pass's chunk bodies and their prefetches (rounds 2-3)
+    "swck_fence": [("kernels_sw_ck.hip", """      load(B, idx(min(i + 1, count - 1)));
+      body(A, idx(i), true);
+      load(A, idx(min(i + 2, count - 1)));
+""", """      load(B, idx(min(i + 1, count - 1)));
+      __builtin_amdgcn_sched_barrier(0);
+      body(A, idx(i), true);
+      load(A, idx(min(i + 2, count - 1)));
+      __builtin_amdgcn_sched_barrier(0);
+""", "replace")],
+    # SW checkpointed solver: every block flushes its ring at the same chunks (no staggered phases)
+    "swck_nostagger": [("kernels_sw_ck.hip", "const int phase = (int)(blockIdx.x % (unsigned)M);",
+                        "const int phase = 0;", "replace")],
+    # LW no-scattering solver: every block flushes its ring at the same layers (no staggered phases)
+    "lw_nostagger": [("kernels_rte.hip", "const int phase = kMulti ? 0 : kPF * (int)(blockIdx.x % (unsigned)(kRing / kPF));",
+                      "const int phase = 0;", "replace")],
+})
+
+
+def parametric(name):
+    """swck_small:K:R:W -- the small-grid SW instance's chunk length, ring levels and wave floor;
+    swck_planes:T:E -- its beam-transmittance (T) and exp(-k tau) (E) workspace planes on (1) or off (0)."""
+    f = name.split(":")
+    if f[0] == "swck_small" and len(f) == 4:
+        return [("kernels_sw_ck.hip", None, "constexpr int kCkKSmall = %s, kCkRingSmall = %s, kCkWavesSmall = %s;"
+                 % tuple(f[1:]), r"constexpr int kCkKSmall = \d+, kCkRingSmall = \d+, kCkWavesSmall = \d+;")]
+    if f[0] == "swck_planes" and len(f) == 3:
+        t, e = ("true" if v == "1" else "false" for v in f[1:])
+        return [("kernels_sw_ck.hip", None, "constexpr bool kCkTnSmall = %s, kCkEmkSmall = %s;" % (t, e),
+                 r"constexpr bool kCkTnSmall = \w+, kCkEmkSmall = \w+;")]
+    return None
+
 
 def apply(csrc, name):
-    for fname, anchor, text, where in ABLATIONS[name]:
+    edits = ABLATIONS.get(name) or parametric(name)
+    for fname, anchor, text, where in edits:
+        if anchor is None:  # parametric: `where` is a regex matching exactly one line
+            import re
+            path = os.path.join(csrc, fname)
+            with open(path) as f:
+                src = f.read()
+            new, n = re.subn(where, text, src)
+            if n != 1:
+                raise SystemExit("ablation %s: pattern matched %d times in %s" % (name, n, fname))
+            with open(path, "w") as f:
+                f.write(new)
+            continue
         path = os.path.join(csrc, fname)
         with open(path) as f:
             src = f.read()
@@ -45,7 +91,7 @@ def apply(csrc, name):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) < 3 or any(n not in ABLATIONS for n in sys.argv[2:]):
+    if len(sys.argv) < 3 or any(n not in ABLATIONS and parametric(n) is None for n in sys.argv[2:]):
         raise SystemExit("usage: ablations.py <csrc_dir> <name>...; names: %s" % ", ".join(sorted(ABLATIONS)))
     for n in sys.argv[2:]:
         apply(sys.argv[1], n)
