@@ -201,18 +201,14 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
       ring[(size_t)r * rs + g] = v;
     }
   };
-  auto flush = [&](float *pq, int n, int lev0, int dl, int slot0 = 0) {
+  auto flush = [&](float *pq, int n, int lev0, int dl) {
     if constexpr (!kMulti) {
       if (rs != ngpt)
-        ring_flush_lanes(ring, rs, pq, n, lev0, dl, ngpt, slot0);
+        ring_flush_lanes(ring, rs, pq, n, lev0, dl, ngpt);
       else
-        ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false, false, slot0);
+        ring_flush<kRing>(ring, pq, 1, n, lev0, dl, ngpt, nlev, false);
     }
   };
-  // Flush phases are staggered between blocks (a multiple of the prefetch depth, so every layer keeps its prefetch
-  // slot): block b's layer walks start kPF * (b % (kRing / kPF)) virtual layers early, so the blocks that share a CU
-  // flush their rings at different layers and one's latency-bound ordered sums run beside the others' arithmetic.
-  const int phase = kMulti ? 0 : kPF * (int)(blockIdx.x % (unsigned)(kRing / kPF));
   // layer source and the level source on the side given by `li` (lev index, 0..nlay)
   auto lay_src = [&](float y, int l) { return kFused ? y * bl[l] : y; };
   auto lev_src = [&](float v, int li) { return kFused ? v * bl[nlay + li] : v; };
@@ -246,14 +242,14 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
       // the last chunk's steps past nlay is skipped, by a uniform branch holding no memory access, so the
       // compiler's vmcnt waits see the same loads on every path and keep the prefetch distance.
       auto step = [&](int j, int r) {
-        const int p = r % kPF, l = lay_dn(min(max(j, 0), nlay - 1));
+        const int p = r % kPF, l = lay_dn(min(j, nlay - 1));
         const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
         {
-          const int ln = lay_dn(min(max(j + kPF, 0), nlay - 1));
+          const int ln = lay_dn(min(j + kPF, nlay - 1));
           pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
           pi[p] = ld_inc(ln);
         }
-        if (j >= 0 && j < nlay) {
+        if (j < nlay) {
           const float T = solver_exp_neg(-t, etab);
           const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
           const float S = (1.0f - T) * lvdn + 2.0f * fact * (ly - lvdn);
@@ -261,11 +257,10 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
           put(fac * I, I, r, 0, top_at_1 ? l + 1 : l, acc);
         }
       };
-      for (int j0 = -phase; j0 < nlay; j0 += kRing) {
+      for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
         for (int r = 0; r < kRing; r++) step(j0 + r, r);
-        const int jf = max(j0, 0);  // the chunk's first real layer
-        flush(pdn, min(j0 + kRing, nlay) - jf, top + dl_dn * (jf + 1), dl_dn, jf - j0);
+        flush(pdn, min(kRing, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     }
     // surface reflection and emission (:269)
@@ -283,16 +278,16 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
         if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * l);
       }
       auto step = [&](int j, int r) {
-        const int p = r % kPF, l = lay_up(min(max(j, 0), nlay - 1));
+        const int p = r % kPF, l = lay_up(min(j, nlay - 1));
         // fused: lev(l) = pfrac(l) * B(tlev(l)) (l < nlay), from the layer's own pfrac
         const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l);
         const float lvup = lev_src(kFused ? py[p] : pv[p], l);
         {
-          const int ln = lay_up(min(max(j + kPF, 0), nlay - 1));
+          const int ln = lay_up(min(j + kPF, nlay - 1));
           pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pi[p] = ld_inc(ln);
           if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * ln);
         }
-        if (j >= 0 && j < nlay) {
+        if (j < nlay) {
           const float T = solver_exp_neg(-t, etab);
           const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
           const float S = (1.0f - T) * lvup + 2.0f * fact * (ly - lvup);
@@ -300,11 +295,10 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
           put(fac * U, U, r, 1, top_at_1 ? l : l + 1, acc);
         }
       };
-      for (int j0 = -phase; j0 < nlay; j0 += kRing) {
+      for (int j0 = 0; j0 < nlay; j0 += kRing) {
 #pragma unroll
         for (int r = 0; r < kRing; r++) step(j0 + r, r);
-        const int jf = max(j0, 0);
-        flush(pup, min(j0 + kRing, nlay) - jf, sfcl - dl_dn * (jf + 1), -dl_dn, jf - j0);
+        flush(pup, min(kRing, nlay - j0), sfcl - dl_dn * (j0 + 1), -dl_dn);
       }
     }
   }

@@ -395,11 +395,9 @@ __global__ void __launch_bounds__(512, WAVES)
                              flux_dir, rs, slot0);
   };
   // the ring holds M = R / K chunks; the block flushes it when it is full (a barrier, the ordered sums, a barrier).
-  // Flush phases are staggered between blocks: block b's first fill starts at chunk slot b % M, so the blocks that
-  // share a CU (dispatched 256 apart) flush at different chunks and one's latency-bound ordered sums run beside the
-  // others' layer arithmetic, instead of every block of the chip flushing at once.
+  // (Staggering the blocks' flush phases, so that blocks sharing a CU flush at different chunks, measured equal, round
+  // 4: the flush's cost is its own latency inside each block, not the whole chip flushing at once.)
   constexpr int M = R / K;
-  const int phase = (int)(blockIdx.x % (unsigned)M);
   V Fdn = inc_dif ? ld_col(inc_dif) : (V)0.0f;
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top, true);
   flush(1, top, 1);
@@ -450,7 +448,7 @@ __global__ void __launch_bounds__(512, WAVES)
         }
       }
       // fluxes down the chunk (adding :1583-1591, Eqs 12-13)
-      const int rbase = ((ck + phase) % M) * K;
+      const int rbase = (ck % M) * K;
 #pragma unroll
       for (int p = 0; p < K; p++) {
         const V fdn = (cf[p].Tdif * Fdn + cf[p].Rdif * S[p] + cf[p].Sdn) * D[p];
@@ -458,9 +456,8 @@ __global__ void __launch_bounds__(512, WAVES)
         put(fdn * Al[p] + S[p], fdn, Fdir[p], rbase + p, top + dl_dn * (ck * K + p + 1), p < n);
       }
       if (valid && (rbase + K == R || ck == nck - 1)) {
-        const int s0 = ck < M - phase ? phase * K : 0;  // the first fill starts at the block's phase
-        const int j0 = ck * K - (rbase - s0);           // first layer of this fill's levels
-        flush(min(rbase + K - s0, nlay - j0), top + dl_dn * (j0 + 1), dl_dn, s0);
+        const int j0 = ck * K - rbase;  // first layer of this ring's levels
+        flush(min(R, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     };
     walk(load3, body3, nck, [](int i) { return i; }, A, B);

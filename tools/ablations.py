@@ -42,22 +42,20 @@ ABLATIONS.update({
       load(A, idx(min(i + 2, count - 1)));
       __builtin_amdgcn_sched_barrier(0);
 """, "replace")],
-    # SW checkpointed solver: every block flushes its ring at the same chunks (no staggered phases)
-    "swck_nostagger": [("kernels_sw_ck.hip", "const int phase = (int)(blockIdx.x % (unsigned)M);",
-                        "const int phase = 0;", "replace")],
-    # LW no-scattering solver: every block flushes its ring at the same layers (no staggered phases)
-    "lw_nostagger": [("kernels_rte.hip", "const int phase = kMulti ? 0 : kPF * (int)(blockIdx.x % (unsigned)(kRing / kPF));",
-                      "const int phase = 0;", "replace")],
 })
 
 
 def parametric(name):
     """swck_small:K:R:W -- the small-grid SW instance's chunk length, ring levels and wave floor;
-    swck_planes:T:E -- its beam-transmittance (T) and exp(-k tau) (E) workspace planes on (1) or off (0)."""
+    swck_planes:T:E -- its beam-transmittance (T) and exp(-k tau) (E) workspace planes on (1) or off (0);
+    mlp_sw:NT:W -- the SW network's threads per block and waves-per-SIMD floor (kernels_nn32.hip)."""
     f = name.split(":")
     if f[0] == "swck_small" and len(f) == 4:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkKSmall = %s, kCkRingSmall = %s, kCkWavesSmall = %s;"
                  % tuple(f[1:]), r"constexpr int kCkKSmall = \d+, kCkRingSmall = \d+, kCkWavesSmall = \d+;")]
+    if f[0] == "mlp_sw" and len(f) == 3:
+        return [("kernels_nn32.hip", None, "constexpr int kMlp32Threads = 512, kSwNT = %s, kSwWPE = %s;" % tuple(f[1:]),
+                 r"constexpr int kMlp32Threads = 512, kSwNT = \d+, kSwWPE = \d+;")]
     if f[0] == "swck_planes" and len(f) == 3:
         t, e = ("true" if v == "1" else "false" for v in f[1:])
         return [("kernels_sw_ck.hip", None, "constexpr bool kCkTnSmall = %s, kCkEmkSmall = %s;" % (t, e),
