@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="launch eagerly instead of replaying a hipGraph")
     ap.add_argument("--no-overlap", action="store_true", help="issue the SW chain on the same stream as LW")
     ap.add_argument("--lw-after", default="", help="start the LW chain after this SW-chain call (e.g. predict_nn_sw; none: chains start together; default: the library pipeline's choice)")
+    ap.add_argument("--sw-after", default="", help="the SW solver waits for this LW-chain call (predict_nn_lw: both "
+                    "networks first, then the solvers side by side; none: no wait; default: the library pipeline's "
+                    "choice)")
+    ap.add_argument("--sw-priority", type=int, default=0, help="priority of the SW chain's stream (-1: high)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
@@ -246,6 +250,7 @@ def main():
         from rrtmgpnn import api
         api.set_sw_kernel_default(args.sw_kernel)
     lw_after = None if not args.lw_after else ("" if args.lw_after == "none" else args.lw_after)
+    sw_after = None if not args.sw_after else ("" if args.sw_after == "none" else args.sw_after)
     use_graph = not args.no_graph
     # the rank's columns in chunks of at most one block (pipeline.ChunkedRank): with more than one chunk every chunk's
     # inputs are resident in HBM and copied into the step's buffers before its replay, its fluxes copied into the
@@ -253,7 +258,8 @@ def main():
     rank_run = ChunkedRank(lo, hi, block, problem,
                            lambda p, c: ClearSkyStep(p, device=local, fused=not args.unfused, clouds=c,
                                                      overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
-                                                     lw_after=lw_after),
+                                                     lw_after=lw_after, sw_after=sw_after,
+                                                     sw_priority=args.sw_priority),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first
@@ -472,7 +478,9 @@ def main():
                        "parallelism": "column-sharded (shard.column_range), 1 process per GPU",
                        "launch": ("hipGraph replay" if use_graph else "eager") +
                                  (", LW and SW chains on two streams" if step.overlap else "") +
-                                 (", the LW chain after %s" % step.lw_after if step.lw_after else ""),
+                                 (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
+                                 (", the SW solver after %s" % step.sw_after if step.sw_after else "") +
+                                 (", SW stream priority %d" % step.sw_priority if step.sw_priority else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
                                    "fused Planck-in-LW-solver, g=0 elided" +
                                    (", cloud increments fused into both solvers" if step.allsky else ""))},

@@ -236,17 +236,26 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
         const int l = lay_dn(min(p, nlay - 1));
-        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pv[p] = lev_ld(l + 1); pi[p] = ld_inc(l);
+        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
+        if constexpr (!kFused) pv[p] = lev_ld(l + 1);
       }
+      // fused: lev(l+1)'s Planck fraction pfrac(min(l+1, nlay-1)) is a neighbour's in walk order, already loaded --
+      // the next layer's (top_at_1: in the other prefetch slot) or the previous one's (bottom first) -- and the
+      // layer's own at the clamped end; kept here instead of loaded a second time
+      float py_prev = 0.0f;
       // Every step issues its prefetch loads unconditionally (clamped to the last layer); only the arithmetic of
       // the last chunk's steps past nlay is skipped, by a uniform branch holding no memory access, so the
       // compiler's vmcnt waits see the same loads on every path and keep the prefetch distance.
       auto step = [&](int j, int r) {
         const int p = r % kPF, l = lay_dn(min(j, nlay - 1));
-        const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(py[p], l), lvdn = lev_src(pv[p], l + 1);
+        const float y_next = py[(r + 1) % kPF], y_own = py[p];
+        const float v = kFused ? (top_at_1 ? y_next : (j == 0 ? y_own : py_prev)) : pv[p];
+        const float t = tau_of(pt[p], pi[p]) * D, ly = lay_src(y_own, l), lvdn = lev_src(v, l + 1);
+        py_prev = y_own;
         {
           const int ln = lay_dn(min(j + kPF, nlay - 1));
-          pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln); pv[p] = lev_ld(ln + 1);
+          pt[p] = Ttau.ld(vg, row * ln); py[p] = Tlay.ld(vg, row * ln);
+          if constexpr (!kFused) pv[p] = lev_ld(ln + 1);
           pi[p] = ld_inc(ln);
         }
         if (j < nlay) {

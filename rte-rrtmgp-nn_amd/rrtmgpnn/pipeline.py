@@ -50,7 +50,7 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
@@ -237,9 +237,10 @@ class ClearSkyStep:
                  (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw),
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
-        self._finish(overlap, lw_after)
+        self.sw_priority = sw_priority
+        self._finish(overlap, lw_after, sw_after)
 
-    def _finish(self, overlap, lw_after=None):
+    def _finish(self, overlap, lw_after=None, sw_after=None):
         if self.fused:
             # the small kernels that do not depend on a network's output go first in their chain, ahead of the big
             # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW
@@ -252,17 +253,20 @@ class ClearSkyStep:
         # network and the LW solver instead of running after them
         self.overlap = overlap
         # The LW chain may start once a call of the SW chain has finished (issued first, the SW network then has the
-        # chip to itself).  Default: after the SW network when the SW solver's grid fits in one round of resident
-        # waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane, against 16 per CU): the solver is then
-        # latency-bound and its start is the step's critical path (C3: step -3 %); with more columns it is VALU-bound
-        # and the chains are better started together (C4: gating was 2.3 % slower).  Making the SW chain wait for
-        # the LW network instead, or both networks first, measured slower at C3.
+        # chip to itself), and the SW solver may wait for a call of the LW chain (sw_after).  Default, when the SW
+        # solver's grid fits in one round of resident waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane,
+        # against 16 per CU; C3): both networks first, side by side, then the two solvers side by side -- the SW solver
+        # waits for the LW network (round 4, alternating whole steps at C3: 0.436-0.439 ms against 0.447-0.451 for the
+        # LW chain after the SW network, the rounds-2/3 default, and 0.483 for the chains started together; with a
+        # high-priority SW stream 0.57).  With more columns the solvers are VALU-bound and the chains start together.
         names = [n for n, _, _ in self.calls]
-        gate = ""
-        if overlap and self.fused and "predict_nn_sw" in names:
+        gate, sw_gate = "", ""
+        if overlap and self.fused and "predict_nn_sw" in names and "predict_nn_lw" in names:
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
             if self.ncol * self.ng_sw <= 2048 * cus:
-                gate = "predict_nn_sw"
+                sw_gate = "predict_nn_lw"
+        if sw_after is None:
+            sw_after = sw_gate
         self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
         if self.lw_after:
             names = [n for n, _, _ in self.calls]
@@ -272,6 +276,17 @@ class ClearSkyStep:
             head = [c for i, c in enumerate(self.calls) if c[0] in SW_CHAIN and i <= cut]
             self.calls = head + [c for c in self.calls if c not in head]
             self._gate = torch.cuda.Event()
+        # sw_after: an LW-chain call the SW solver waits for (the two networks first, then the two solvers side by side)
+        self.sw_after = sw_after if overlap else ""
+        if self.sw_after:
+            names = [n for n, _, _ in self.calls]
+            if self.sw_after not in names or self.sw_after in SW_CHAIN or "sw_solver" not in names:
+                raise ValueError("sw_after: %r is not a call of this fused step's LW chain" % self.sw_after)
+            sol = next(c for c in self.calls if c[0] == "sw_solver")
+            rest = [c for c in self.calls if c is not sol]
+            cut = [n for n, _, _ in rest].index(self.sw_after)
+            self.calls = rest[:cut + 1] + [sol] + rest[cut + 1:]  # issued right after the call it waits for
+            self._gate2 = torch.cuda.Event()
         self.ctx2 = None
         if overlap:
             self.ctx2 = Context(self.dev.index, self._sw_stream())
@@ -282,7 +297,9 @@ class ClearSkyStep:
     def _sw_stream(self):
         # default priority: a high-priority SW stream (critical path) was measured 25 % slower at C3 -- it takes every
         # CU first and the chains stop overlapping (tools/ab_prio.sh)
-        return torch.cuda.Stream(self.dev)
+        # sw_priority < 0: a higher-priority stream (the two-solvers-side-by-side schedule, so the SW solver's blocks are
+        # dispatched ahead of the LW solver's when both are ready)
+        return torch.cuda.Stream(self.dev, priority=getattr(self, "sw_priority", 0))
 
     def stream_for(self, name):
         """The torch stream a call of `self.calls` is issued on."""
@@ -328,6 +345,9 @@ class ClearSkyStep:
             if self.overlap and name == self.lw_after:
                 self._gate.record(self.ctx2.stream)
                 self.ctx.stream.wait_event(self._gate)
+            if self.sw_after and name == self.sw_after:
+                self._gate2.record(self.ctx.stream)
+                self.ctx2.stream.wait_event(self._gate2)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)
