@@ -255,18 +255,18 @@ class ClearSkyStep:
         # The LW chain may start once a call of the SW chain has finished (issued first, the SW network then has the
         # chip to itself), and the SW solver may wait for a call of the LW chain (sw_after).  Default, when the SW
         # solver's grid fits in one round of resident waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane,
-        # against 16 per CU; C3): both networks first, side by side, then the two solvers side by side -- the SW solver
-        # waits for the LW network (round 4, alternating whole steps at C3: 0.436-0.439 ms against 0.447-0.451 for the
-        # LW chain after the SW network, the rounds-2/3 default, and 0.483 for the chains started together; with a
-        # high-priority SW stream 0.57).  With more columns the solvers are VALU-bound and the chains start together.
+        # against 16 per CU; C3): the LW chain after the SW network.  Round 4, alternating whole steps at C3 (3 triples,
+        # one box): 0.435-0.439 ms, against 0.470-0.473 for both networks first and then the two solvers side by side
+        # (the SW solver waiting for both networks) and 0.469-0.476 for the chains started together.  At C4 the three
+        # are within the run-to-run band (2.70-2.77 ms); with more columns the chains start together.
         names = [n for n, _, _ in self.calls]
-        gate, sw_gate = "", ""
+        gate = ""
         if overlap and self.fused and "predict_nn_sw" in names and "predict_nn_lw" in names:
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
             if self.ncol * self.ng_sw <= 2048 * cus:
-                sw_gate = "predict_nn_lw"
+                gate = "predict_nn_sw"
         if sw_after is None:
-            sw_after = sw_gate
+            sw_after = ""
         self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
         if self.lw_after:
             names = [n for n, _, _ in self.calls]
@@ -282,10 +282,11 @@ class ClearSkyStep:
             names = [n for n, _, _ in self.calls]
             if self.sw_after not in names or self.sw_after in SW_CHAIN or "sw_solver" not in names:
                 raise ValueError("sw_after: %r is not a call of this fused step's LW chain" % self.sw_after)
-            sol = next(c for c in self.calls if c[0] == "sw_solver")
-            rest = [c for c in self.calls if c is not sol]
-            cut = [n for n, _, _ in rest].index(self.sw_after)
-            self.calls = rest[:cut + 1] + [sol] + rest[cut + 1:]  # issued right after the call it waits for
+            names = [n for n, _, _ in self.calls]
+            if names.index(self.sw_after) > names.index("sw_solver"):
+                raise ValueError("sw_after: %r is issued after the SW solver" % self.sw_after)
+            # the event is recorded on the LW stream right after that call is issued, and the SW stream waits for it
+            # right before the SW solver -- the SW network, issued in between, does not wait
             self._gate2 = torch.cuda.Event()
         self.ctx2 = None
         if overlap:
@@ -329,6 +330,8 @@ class ClearSkyStep:
             self._fork.record(self.ctx.stream)
             self.ctx2.stream.wait_event(self._fork)
         for name, fn, args in self.calls:
+            if self.sw_after and name == "sw_solver":
+                self.ctx2.stream.wait_event(self._gate2)
             if timing is not None:
                 s = self.stream_for(name)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -347,7 +350,6 @@ class ClearSkyStep:
                 self.ctx.stream.wait_event(self._gate)
             if self.sw_after and name == self.sw_after:
                 self._gate2.record(self.ctx.stream)
-                self.ctx2.stream.wait_event(self._gate2)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)

@@ -162,7 +162,7 @@ def test_fused_gas_optics_equals_separate_calls(dev, rfmip, ncol, mlp_kernel):
 def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky, lw_after):
     """LW and SW chains on two streams (forked at the start, joined at the end; the LW chain started after the SW
     network by default at this size, with both started together, or after the SW solver; or both networks first and
-    the SW solver after the LW network, on a high-priority stream), eager and as one hipGraph, give the
+    the SW solver after both networks, on a high-priority stream), eager and as one hipGraph, give the
     single-stream step's fluxes bit for bit."""
     from rrtmgpnn import data
     from rrtmgpnn.pipeline import ClearSkyStep
@@ -174,9 +174,9 @@ def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky, lw_after):
                        lw_after={"": None, "none": "", "sw_solver": "sw_solver", "nets_first": ""}[lw_after],
                        sw_after={"": None, "nets_first": "predict_nn_lw"}.get(lw_after, ""),
                        sw_priority=-1 if nets_first else 0)
-    # default at this size (450 columns): both networks first, then the solvers side by side
-    assert two.lw_after == {"": "", "none": "", "sw_solver": "sw_solver", "nets_first": ""}[lw_after]
-    assert two.sw_after == ("predict_nn_lw" if lw_after in ("", "nets_first") else "")
+    # default at this size (450 columns): the LW chain after the SW network
+    assert two.lw_after == {"": "predict_nn_sw", "none": "", "sw_solver": "sw_solver", "nets_first": ""}[lw_after]
+    assert two.sw_after == ("predict_nn_lw" if nets_first else "")
     one.step()
     two.step()
     torch.cuda.synchronize()
