@@ -606,9 +606,21 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=7, bind="non
         sweep[str(threads)] = round(value, 1)
         nproc = int(res["nproc"])
         per_thread = value / threads
+        # the CPUs the job may use: its cgroup quota (cpu.max "quota period") caps it below the affinity mask on the
+        # GPU box (16 of 256), so the per-GPU share of nproc / 8 = 32 threads cannot be measured there
+        quota = None
+        try:
+            q, per = allot.get("cgroup_cpu_max", "").split()
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+        except ValueError:
+            pass
+        ss = sorted(secs)
         return {"value": round(value, 1), "unit": "columns/s", "cores": threads, "kind": "reference",
                 "nproc": nproc, "runs_s": [round(t, 4) for t in secs],
                 "spread": round((max(secs) - min(secs)) / med, 4),
+                # without the fastest and the slowest run (other tenants' load on the host shows up as single outliers)
+                "spread_trimmed": round((ss[-2] - ss[1]) / med, 4) if len(ss) >= 5 else None,
+                "quota_cpus": quota,
                 "thread_sweep": sweep, "cpu_allotment": allot,
                 "extrapolated": {
                     "node_share_per_gpu": {"threads": max(1, nproc // 8),
@@ -616,7 +628,8 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=7, bind="non
                     "node": {"threads": nproc, "value": round(per_thread * nproc, 1)},
                     "note": "not measured: linear in threads from the %d-thread value (an upper bound, the blocks are "
                             "independent), to nproc/8 and nproc logical CPUs; the measured %d threads are the CPU "
-                            "share the GPU box allots this job (OMP_NUM_THREADS)" % (threads, threads)},
+                            "share the GPU box allots this job (OMP_NUM_THREADS%s)"
+                            % (threads, threads, ", cgroup quota %s CPUs" % quota if quota else "")},
                 "sample": ("%d columns per run (blocks of %d cycling through %d columns of the workload), %s, median "
                            "of %d runs: the reference's Fortran rte_lw/rte_sw + network_type sgemm MLP (MKL, "
                            "sequential)%s compiled from its sources, OpenMP over blocks on %d threads (%s) "

@@ -17,8 +17,8 @@
 // Per launch this reads tau three times and ssa twice (as before) but moves 3/K planes of checkpoints instead of 6
 // planes of workspace.  The VALU work per element is pass 2's and 3's sw_two_stream plus one more adding step in pass
 // 3; the K layers of a chunk are independent until the recurrences, which gives the scheduler K-wide ILP.
-// Workspace: (ngpt, nck, ncol) beam checkpoints, then (ngpt, nck+1, ncol) albedo and source checkpoints, nck =
-// ceil(nlay / K); index c holds level c*K counted from the top, index nck the surface.
+// Workspace: (ngpt, 3 nck + 2, ncol) checkpoints, per column nck beam rows, then nck+1 albedo and nck+1 source rows,
+// nck = ceil(nlay / K); row c of each holds level c*K counted from the top, albedo / source row nck the surface.
 #include "x2_device.hpp"
 
 #include <algorithm>
@@ -125,14 +125,16 @@ __host__ __device__ constexpr int ck_ring_stride(int ngpt) { return ngpt + 4; }
 // K: layers per chunk (checkpoint spacing); kCkRing: levels staged for the ordered broadband sums (a multiple of K).
 // K = 3 layers per chunk under a 3-waves-per-SIMD register budget (132 VGPRs, no spill; at 4 waves K = 3 spilled and
 // K = 2 fit): C3 step -3 %, C4 -1 % against K = 2 or the two-per-lane workspace kernel; K = 4 (148 VGPRs) was best
-// alone at C3 but 13 % slower at C4, K = 6 spilled (tools/gpu_ab.sh, round 2)
-constexpr int kCkK = 3, kCkRing = 6, kCkWaves = 3;
+// alone at C3 but 13 % slower at C4, K = 6 spilled (tools/gpu_ab.sh, round 2).  Round 4 (the SW solver alone,
+// alternating, bitwise; tools/kernel_ab.py): a ring of 9 levels (7 flushes per 60-layer column instead of 10) C4 -2.7 %;
+// a 2-wave floor (no VGPR spill) +7 % with K = 3, +5 % with K = 4 / ring 8.
+constexpr int kCkK = 3, kCkRing = 9, kCkWaves = 3;
 // pass 1 loads kCkP1 chunks of optical depths per step (and the next step's while it computes)
 constexpr int kCkP1 = 2;
-// Waves per SIMD of the clear-sky NN instance (g = NULL, no increment), which needs fewer registers: at 4 (128 VGPRs,
-// 2 spilled) the C3 grid (900 blocks of 4 waves) is resident at once instead of 768 + a second round of 132; SW solver
-// -2.5 % at C3, step -0.7 %, C5 shard equal (tools/gpu_ab.sh, round 2)
-constexpr int kCkWavesNN = 4;
+// Waves per SIMD of the large-grid clear-sky NN instance (g = NULL, no increment; C5).  Round 2 chose 4 (128 VGPRs)
+// when it also ran C3; since the small-grid instance took C3 over, the register floor spilled 19-21 VGPRs for no
+// residency gain: at 3 (no spill) the C5 shard's SW solver runs 10 % faster alone, 12 % with the ring of 9 (round 4).
+constexpr int kCkWavesNN = 3;
 
 // kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
 // broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
@@ -192,19 +194,20 @@ __global__ void __launch_bounds__(512, WAVES)
   const size_t cl = (size_t)ngpt * nlay * icol0;
   const uint32_t bL = (uint32_t)nc * row * nlay;
   const CA_ Ttau(tau, cl, bL), Tssa(ssa, cl, bL), Tg(kHasG ? gg : tau, cl, bL);
-  // checkpoints: beam (ngpt, nck, ncol), albedo and source (ngpt, nck+1, ncol)
-  const size_t pB = (size_t)ngpt * nck * ncol, pA = (size_t)ngpt * (nck + 1) * ncol;
-  const uint32_t vB = 4u * (uint32_t)gc + (uint32_t)c * row * nck, vA = 4u * (uint32_t)gc + (uint32_t)c * row * (nck + 1);
-  const CA_ CB(ws, (size_t)ngpt * nck * icol0, (uint32_t)nc * row * nck);
-  const CA_ CA(ws + pB, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
-  const CA_ CS(ws + pB + pA, (size_t)ngpt * (nck + 1) * icol0, (uint32_t)nc * row * (nck + 1));
+  // checkpoints, column by column: (ngpt, 3 nck + 2, ncol) -- rows [0, nck) the beam, [nck, 2 nck + 1) the albedo,
+  // [2 nck + 1, 3 nck + 2) the source; one buffer descriptor for the three (the layer offset in the SGPR offset)
+  const int nrw = 3 * nck + 2;
+  const size_t pW = (size_t)ngpt * nrw * ncol;
+  const uint32_t vW = 4u * (uint32_t)gc + (uint32_t)c * row * nrw;
+  const CA_ CW(ws, (size_t)ngpt * nrw * icol0, (uint32_t)nc * row * nrw);
+  const uint32_t sA0 = row * (uint32_t)nck, sS0 = row * (uint32_t)(2 * nck + 1);
   // kTn: the beam transmittances (ngpt, nlay, ncol), addressed as tau.  kEmk: pass 2's exp(-tau k) in the plane after
   // it, which pass 3 reads instead of evaluating the exp again.  (Keeping all four coefficients R_dif, T_dif, S_up, S_dn
   // instead, so that pass 3 forms none, was 23 % slower at C3: four planes written and read cost more than they save.)
   const size_t plane = (size_t)ngpt * nlay * ncol;
-  const CA_ CT(kTn ? ws + pB + 2 * pA : ws, kTn ? cl : 0, kTn ? bL : 0u);
-  const CA_ CE(kEmk ? ws + pB + 2 * pA + (kTn ? plane : 0) : ws, kEmk ? cl : 0, kEmk ? bL : 0u);
-  const uint32_t vBs = on ? vB : kBufOOB, vAs = on ? vA : kBufOOB;
+  const CA_ CT(kTn ? ws + pW : ws, kTn ? cl : 0, kTn ? bL : 0u);
+  const CA_ CE(kEmk ? ws + pW + (kTn ? plane : 0) : ws, kEmk ? cl : 0, kEmk ? bL : 0u);
+  const uint32_t vWs = on ? vW : kBufOOB;
   // band-resolved increments: one band offset per g-point of the lane
   const size_t cb = (size_t)bands.nbnd * nlay * icol0;
   const uint32_t brow = 4u * (uint32_t)bands.nbnd, vbc = (uint32_t)c * brow * nlay;
@@ -251,11 +254,11 @@ __global__ void __launch_bounds__(512, WAVES)
       }
     }
     if (pass == 2) {
-      ch.fb = CB.ldv(vB, row * (uint32_t)ck);
+      ch.fb = CW.ldv(vW, row * (uint32_t)ck);
     } else {
       const uint32_t sE = row * (uint32_t)min(ck + 1, nck);
-      ch.ae = CA.ldv(vA, sE);
-      ch.se = CS.ldv(vA, sE);
+      ch.ae = CW.ldv(vW, sA0 + sE);
+      ch.se = CW.ldv(vW, sS0 + sE);
     }
   };
   // the (incremented) properties of layer p of a chunk
@@ -311,7 +314,7 @@ __global__ void __launch_bounds__(512, WAVES)
       }
 #pragma unroll
       for (int p = 0; p < P1; p++) {
-        if (p % K == 0) CB.stv(Fd, (p < n) ? vBs : kBufOOB, row * (uint32_t)(c1 * kCkP1 + p / K));
+        if (p % K == 0) CW.stv(Fd, (p < n) ? vWs : kBufOOB, row * (uint32_t)(c1 * kCkP1 + p / K));
         Fd = (p < n) ? Tn[p] * Fd : Fd;
       }
     };
@@ -320,8 +323,8 @@ __global__ void __launch_bounds__(512, WAVES)
   // ---- pass 2: bottom -> top adding; albedo / source checkpoint at every chunk top and at the surface ----
   V alb_b = ld_col(alb_dif);
   V src_b = Fd * ld_col(alb_dir);
-  CA.stv(alb_b, vAs, row * (uint32_t)nck);
-  CS.stv(src_b, vAs, row * (uint32_t)nck);
+  CW.stv(alb_b, vWs, sA0 + row * (uint32_t)nck);
+  CW.stv(src_b, vWs, sS0 + row * (uint32_t)nck);
   {
     Chunk A, B;
     auto load2 = [&](Chunk &ch, int ck) { load_chunk(ch, ck, 2); };
@@ -362,8 +365,8 @@ __global__ void __launch_bounds__(512, WAVES)
         alb_b = (p < n) ? alb : alb_b;
         src_b = (p < n) ? src : src_b;
       }
-      CA.stv(alb_b, valid && ck > 0 ? vAs : kBufOOB, row * (uint32_t)ck);
-      CS.stv(src_b, valid && ck > 0 ? vAs : kBufOOB, row * (uint32_t)ck);
+      CW.stv(alb_b, valid && ck > 0 ? vWs : kBufOOB, sA0 + row * (uint32_t)ck);
+      CW.stv(src_b, valid && ck > 0 ? vWs : kBufOOB, sS0 + row * (uint32_t)ck);
     };
     walk(load2, body2, nck, [&](int i) { return nck - 1 - i; }, A, B);
   }

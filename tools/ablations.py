@@ -48,11 +48,19 @@ ABLATIONS.update({
 def parametric(name):
     """swck_small:K:R:W -- the small-grid SW instance's chunk length, ring levels and wave floor;
     swck_planes:T:E -- its beam-transmittance (T) and exp(-k tau) (E) workspace planes on (1) or off (0);
+    swck_big:K:R:W -- the large-grid instances' chunk length, ring levels and wave floor (the all-sky ones; C4);
+    swck_nnw:W -- the large-grid clear-sky (NN) instance's wave floor (C5);
     mlp_sw:NT:W -- the SW network's threads per block and waves-per-SIMD floor (kernels_nn32.hip)."""
     f = name.split(":")
     if f[0] == "swck_small" and len(f) == 4:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkKSmall = %s, kCkRingSmall = %s, kCkWavesSmall = %s;"
                  % tuple(f[1:]), r"constexpr int kCkKSmall = \d+, kCkRingSmall = \d+, kCkWavesSmall = \d+;")]
+    if f[0] == "swck_big" and len(f) == 4:
+        return [("kernels_sw_ck.hip", None, "constexpr int kCkK = %s, kCkRing = %s, kCkWaves = %s;" % tuple(f[1:]),
+                 r"constexpr int kCkK = \d+, kCkRing = \d+, kCkWaves = \d+;")]
+    if f[0] == "swck_nnw" and len(f) == 2:
+        return [("kernels_sw_ck.hip", None, "constexpr int kCkWavesNN = %s;" % f[1],
+                 r"constexpr int kCkWavesNN = \d+;")]
     if f[0] == "mlp_sw" and len(f) == 3:
         return [("kernels_nn32.hip", None, "constexpr int kMlp32Threads = 512, kSwNT = %s, kSwWPE = %s;" % tuple(f[1:]),
                  r"constexpr int kMlp32Threads = 512, kSwNT = \d+, kSwWPE = \d+;")]
