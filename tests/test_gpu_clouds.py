@@ -307,9 +307,16 @@ def test_fused_increment_solvers_match_increment_then_solve(dev, rfmip, top_at_1
     mu0 = t(rng.uniform(0.1, 1, ncol))
     inc = t(rng.uniform(0, 5, (ncol, ng)))
     alb = t(rng.uniform(0, 1, (ncol, ng)))
-    lims = int_array(ks["band_lims_gpt"].ravel())
+    # the k-distribution's bands (16 g-points each: both g-points of a lane in one band, the kernel's band-pair
+    # instance) and a layout with odd band starts (the general instance)
+    bl = np.array(ks["band_lims_gpt"], dtype=np.int64).reshape(-1, 2)
+    odd = bl.copy()
+    odd[0, 1] -= 1
+    odd[1, 0] -= 1
+    assert (odd[1, 0] - 1) % 2 == 1
     outs = [[f(ncol, nlay + 1) for _ in range(3)] for _ in range(2)]
-    for with_g in (True, False):
+    for band_lims, with_g in ((b, w) for b in (bl, odd) for w in (True, False)):
+        lims = int_array(band_lims.ravel())
         g_in = gg if with_g else None
         saved = [a.clone() for a in (tau, ssa, gg)]
         _lib.check(L.rrtmgpnn_sw_solver_2stream_inc(
@@ -327,4 +334,4 @@ def test_fused_increment_solvers_match_increment_then_solve(dev, rfmip, top_at_1
                                                 alb.data_ptr(), alb.data_ptr(), *[o.data_ptr() for o in outs[1]]))
         torch.cuda.synchronize()
         for a, b in zip(*outs):
-            assert torch.equal(a, b), "with_g=%s" % with_g
+            assert torch.equal(a, b), "with_g=%s bands=%s" % (with_g, band_lims[:2].tolist())
