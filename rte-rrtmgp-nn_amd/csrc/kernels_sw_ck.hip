@@ -154,10 +154,12 @@ constexpr int kCkKSmall = 3, kCkRingSmall = 9, kCkWavesSmall = 2;
 constexpr bool kCkTnSmall = true, kCkEmkSmall = true;
 using VSmall = f2;
 
-// V: f2 (two g-points per lane) or float (one per lane)
+// V: f2 (two g-points per lane) or float (one per lane).  kBandPair (fused increment, two g-points per lane): every
+// band starts at an even g-point, so both g-points of a lane lie in one band and its band values are one load each
+// (the RRTMGP g-point sets: 16 per band)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? kCkWavesNN : kCkWaves, bool kTn = false,
-          class V = f2, bool kEmk = false>
+          class V = f2, bool kEmk = false, bool kBandPair = false>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -218,7 +220,10 @@ __global__ void __launch_bounds__(512, WAVES)
       Bg(kInc ? g_bnd : tau, kInc ? cb : 0, bB);
   auto ld_bnd = [&](const CA_ &a, int l) -> V {
     if constexpr (!kInc) return (V)0.0f;
-    else if constexpr (NPL == 2) return (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)};
+    else if constexpr (NPL == 2 && kBandPair) {
+      const float v = a.ld1(vb0, brow * (uint32_t)l);
+      return (f2){v, v};
+    } else if constexpr (NPL == 2) return (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)};
     else return a.ld1(vb0, brow * (uint32_t)l);
   };
   const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
@@ -517,8 +522,18 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     if (g) return go(sw_2stream_ck_kernel<true, false, kCkK, true>, nullptr, nullptr, nullptr);
     return go(sw_2stream_ck_kernel<false, false, kCkK, true>, nullptr, nullptr, nullptr);
   }
-  if (bands && g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
-  if (bands) return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
+  if (bands) {
+    bool pair = true;  // every band starts at an even (0-based) g-point
+    for (int i = 0; i < b.nbnd; i++) pair = pair && ((b.lims[2 * i] - 1) % 2 == 0);
+    constexpr int W = kCkWaves;
+    if (pair && g)
+      return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W, false, f2, false, true>, tau_bnd, ssa_bnd, g_bnd);
+    if (pair)
+      return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, W, false, f2, false, true>, tau_bnd, ssa_bnd,
+                g_bnd);
+    if (g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
+    return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
+  }
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
