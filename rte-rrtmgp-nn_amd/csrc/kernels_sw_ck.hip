@@ -156,7 +156,7 @@ using VSmall = f2;
 
 // V: f2 (two g-points per lane) or float (one per lane).  kBandPair (fused increment, two g-points per lane): every
 // band starts at an even g-point, so both g-points of a lane lie in one band and its band values are one load each
-// (the RRTMGP g-point sets: 16 per band)
+// (the RRTMGP g-point sets: 16 per band).  Round 4, C4: SW solver -1.7 % alone, steps -0.8 % (3 alternating pairs)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? kCkWavesNN : kCkWaves, bool kTn = false,
           class V = f2, bool kEmk = false, bool kBandPair = false>
