@@ -43,6 +43,25 @@ FUSED_ORDER = ["get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", 
                "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver"]
 
 
+def issue_order(calls, fused, lw_after=""):
+    """The step's issue order of `calls` ((name, fn, args) tuples): fused steps sort by FUSED_ORDER (stable; names
+    not listed keep their place at the end); lw_after (an SW-chain call) moves the SW-chain calls up to and including
+    it ahead of the rest, so the LW chain can be gated on it.  Each chain keeps its own relative order (a chain is
+    issued on one stream, in this order)."""
+    calls = list(calls)
+    if fused:
+        order = {n: i for i, n in enumerate(FUSED_ORDER)}
+        calls.sort(key=lambda c: order.get(c[0], len(order)))
+    if lw_after:
+        names = [n for n, _, _ in calls]
+        if lw_after not in names or lw_after not in SW_CHAIN or "get_col_dry" in names:
+            raise ValueError("lw_after: %r is not a call of this fused step's SW chain" % lw_after)
+        cut = names.index(lw_after)
+        head = [c for i, c in enumerate(calls) if c[0] in SW_CHAIN and i <= cut]
+        calls = head + [c for c in calls if c not in head]
+    return calls
+
+
 def _t(a, dev):
     return torch.as_tensor(np.ascontiguousarray(a, dtype=np.float32), device=dev)
 
@@ -241,12 +260,10 @@ class ClearSkyStep:
         self._finish(overlap, lw_after, sw_after)
 
     def _finish(self, overlap, lw_after=None, sw_after=None):
-        if self.fused:
-            # the small kernels that do not depend on a network's output go first in their chain, ahead of the big
-            # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW
-            # solver held while the LW solver, which needs it, could not start
-            order = {n: i for i, n in enumerate(FUSED_ORDER)}
-            self.calls.sort(key=lambda c: order.get(c[0], len(order)))
+        # fused: the small kernels that do not depend on a network's output go first in their chain, ahead of the big
+        # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW solver
+        # held while the LW solver, which needs it, could not start
+        self.calls = issue_order(self.calls, self.fused)
         # overlap: the SW chain runs on a second context/stream, forked after col_dry (which both streams read; the
         # fused step, whose chains form col_dry each in their network kernel, forks at its start)
         # and joined at the end of the step -- the VALU-bound SW solver shares the CUs with the MFMA-bound LW
@@ -269,12 +286,7 @@ class ClearSkyStep:
             sw_after = ""
         self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
         if self.lw_after:
-            names = [n for n, _, _ in self.calls]
-            if self.lw_after not in names or self.lw_after not in SW_CHAIN or "get_col_dry" in names:
-                raise ValueError("lw_after: %r is not a call of this fused step's SW chain" % self.lw_after)
-            cut = names.index(self.lw_after)
-            head = [c for i, c in enumerate(self.calls) if c[0] in SW_CHAIN and i <= cut]
-            self.calls = head + [c for c in self.calls if c not in head]
+            self.calls = issue_order(self.calls, self.fused, self.lw_after)
             self._gate = torch.cuda.Event()
         # sw_after: an LW-chain call the SW solver waits for (the two networks first, then the two solvers side by side)
         self.sw_after = sw_after if overlap else ""

@@ -218,3 +218,30 @@ def test_synthetic_problem_column_ranges_are_slices_of_the_whole():
     r = data.rfmip_columns(3500, 200)
     full = data.rfmip_problem()
     np.testing.assert_array_equal(r["tlay"], full["tlay"][(3500 + np.arange(200)) % 1800])
+
+
+@pytest.mark.parametrize("allsky", [False, True])
+@pytest.mark.parametrize("lw_after", ["", "predict_nn_sw", "sw_solver", "cloud_optics_sw"])
+def test_issue_order_keeps_each_chain_in_order(allsky, lw_after):
+    """The step's issue order (pipeline.issue_order) keeps every chain in FUSED_ORDER's relative order -- each chain
+    runs on one stream in issue order, so a call issued ahead of its producer would read the previous step's data --
+    and with an LW gate the SW-chain calls up to the gate come first."""
+    from rrtmgpnn.pipeline import FUSED_ORDER, SW_CHAIN, issue_order
+    names = ["predict_nn_lw", "lw_solver", "predict_nn_sw", "sw_solver"]
+    if allsky:
+        names = ["cloud_optics_lw"] + names[:2] + ["cloud_optics_sw", "delta_scale_sw"] + names[2:]
+    elif lw_after == "cloud_optics_sw":
+        with pytest.raises(ValueError):
+            issue_order([(n, None, ()) for n in names], True, lw_after)
+        return
+    calls = [(n, None, ()) for n in reversed(names)]  # any construction order
+    out = [n for n, _, _ in issue_order(calls, True, lw_after)]
+    assert sorted(out) == sorted(names)
+    for chain in (SW_CHAIN, set(names) - SW_CHAIN):
+        got = [n for n in out if n in chain]
+        assert got == sorted(got, key=FUSED_ORDER.index)
+    if lw_after:
+        cut = out.index(lw_after)
+        assert all(n in SW_CHAIN for n in out[:cut + 1])
+        assert [n for n in out[:cut + 1]] == [n for n in sorted(names, key=FUSED_ORDER.index)
+                                              if n in SW_CHAIN][:cut + 1]
