@@ -270,18 +270,17 @@ class ClearSkyStep:
         # network and the LW solver instead of running after them
         self.overlap = overlap
         # The LW chain may start once a call of the SW chain has finished (issued first, the SW network then has the
-        # chip to itself), and the SW solver may wait for a call of the LW chain (sw_after).  Default, when the SW
-        # solver's grid fits in one round of resident waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane,
-        # against 16 per CU; C3): the LW chain after the SW network.  Round 4, alternating whole steps at C3 (3 triples,
-        # one box): 0.435-0.439 ms, against 0.470-0.473 for both networks first and then the two solvers side by side
-        # (the SW solver waiting for both networks) and 0.469-0.476 for the chains started together.  At C4 the three
-        # are within the run-to-run band (2.70-2.77 ms); with more columns the chains start together.
+        # chip to itself), and the SW solver may wait for a call of the LW chain (sw_after).  Default: the LW chain
+        # after the SW network -- the SW chain is the critical path at every size.  Round 4, alternating whole steps on
+        # one box: C3 0.435-0.439 ms, against 0.470-0.473 for both networks first and then the two solvers side by
+        # side (the SW solver waiting for both networks) and 0.469-0.476 for the chains started together; C4 2.613-2.618
+        # against 2.649-2.670 started together (3 pairs), C5 shard 62.96-63.03 against 63.64-63.65 (2 pairs).  Started
+        # together at C4, the SW network ran beside the LW network and solver for 775 us (239 alone) and the SW solver
+        # started 1.1 ms into the step.
         names = [n for n, _, _ in self.calls]
         gate = ""
         if overlap and self.fused and "predict_nn_sw" in names and "predict_nn_lw" in names:
-            cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
-            if self.ncol * self.ng_sw <= 2048 * cus:
-                gate = "predict_nn_sw"
+            gate = "predict_nn_sw"
         if sw_after is None:
             sw_after = ""
         self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
