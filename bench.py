@@ -61,6 +61,9 @@ def parse():
                     "networks first, then the solvers side by side; none: no wait; default: the library pipeline's "
                     "choice)")
     ap.add_argument("--sw-priority", type=int, default=0, help="priority of the SW chain's stream (-1: high)")
+    ap.add_argument("--lw-net-cus", type=int, default=None,
+                    help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
+                         "choice, 3/4 of the CUs when the LW chain follows the SW network)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
@@ -202,6 +205,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from rrtmgpnn import data
+    from rrtmgpnn import _lib
     from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
 
     # ---- the global problem and this rank's part of it (shard.column_range) ----
@@ -259,7 +263,7 @@ def main():
                            lambda p, c: ClearSkyStep(p, device=local, fused=not args.unfused, clouds=c,
                                                      overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
                                                      lw_after=lw_after, sw_after=sw_after,
-                                                     sw_priority=args.sw_priority),
+                                                     sw_priority=args.sw_priority, lw_net_cus=args.lw_net_cus),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first
@@ -338,6 +342,10 @@ def main():
     reps = max(3, min(20, args.steps))
 
     def time_stages(serial):
+        # serialised: every kernel on the whole chip, the LW network's CU cap (rrtmgpnn_context_set_mlp_max_cus, an
+        # overlap measure) lifted for the measurement
+        if serial and step.lw_net_cus:
+            _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx.h, 0), "context_set_mlp_max_cus")
         step.step()  # warm the eager path
         torch.cuda.synchronize(dev)
         timing = {}
@@ -357,6 +365,8 @@ def main():
             else:
                 step.step(timing)
         torch.cuda.synchronize(dev)
+        if serial and step.lw_net_cus:
+            _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx.h, step.lw_net_cus), "context_set_mlp_max_cus")
         return {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
 
     stages = time_stages(True)
@@ -479,6 +489,7 @@ def main():
                        "launch": ("hipGraph replay" if use_graph else "eager") +
                                  (", LW and SW chains on two streams" if step.overlap else "") +
                                  (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
+                                 (" (LW network on %d CUs)" % step.lw_net_cus if step.lw_net_cus else "") +
                                  (", the SW solver after %s" % step.sw_after if step.sw_after else "") +
                                  (", SW stream priority %d" % step.sw_priority if step.sw_priority else ""),
                        "kernels": ("class-layer sequence" if not step.fused else

@@ -63,6 +63,11 @@ int rrtmgpnn_context_set_sw_kernel(rrtmgpnn_context *ctx, int mode);
  * otherwise.  1: 16x16x4 tiles.
  * Bit-identical outputs either way.  ctx == NULL sets the default of every context not set itself. */
 int rrtmgpnn_context_set_mlp_kernel(rrtmgpnn_context *ctx, int mode);
+/* MI355X tuning, no reference counterpart: the gas-optics networks launched on this context use at most `cus` CUs'
+ * worth of resident blocks (0, the default: every CU).  For a host that runs the LW and SW chains side by side on two
+ * streams: an LW network confined to part of the chip leaves the other CUs to the SW solver from its start (each LW
+ * network block holds a whole CU's LDS).  Bit-identical outputs. */
+int rrtmgpnn_context_set_mlp_max_cus(rrtmgpnn_context *ctx, int cus);
 void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_synchronize(rrtmgpnn_context *ctx);
 /* The context's device workspace grows on demand.  A call issued while the context's stream is captured into a

@@ -203,6 +203,14 @@ int rrtmgpnn_context_set_mlp_kernel(rrtmgpnn_context *ctx, int mode)
   return RRTMGPNN_OK;
 }
 
+int rrtmgpnn_context_set_mlp_max_cus(rrtmgpnn_context *ctx, int cus)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (cus < 0) return fail(RRTMGPNN_ERR_ARGUMENT, "mlp max cus must be >= 0");
+  ctx->mlp_max_cus = cus;
+  return RRTMGPNN_OK;
+}
+
 int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream)
 {
   if (int rc = check_ctx(ctx)) return rc;

@@ -54,6 +54,7 @@ struct rrtmgpnn_context {
   bool own_stream = false;
   int num_cus = 256;
   int sw_kernel = -1;  // SW two-stream kernel: 0 by ngpt, 1 / 2 g-points per lane, -1 the library default
+  int mlp_max_cus = 0;  // rrtmgpnn_context_set_mlp_max_cus: CUs' worth of network blocks, 0 = all
   int mlp_kernel = -1;  // LW network tiling: 0 32x32x2 where instantiated, 1 16x16x4, -1 the library default
   // Per-call solver extras, set by the *_gpt entry points for the duration of one call (rte_lw's lw_Ds and
   // ty_fluxes_flexible's g-point outputs, (ngpt, nlay+1, ncol) each); the other entries leave them null.

@@ -572,7 +572,8 @@ static int launch_mlp_acts(rrtmgpnn_context *ctx, MlpArgs &a)
   int per_cu = std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1)));
   per_cu = std::min(per_cu, 2048 / kThreads);
   long long want = (ntiles + wpb - 1) / wpb;
-  long long grid = std::min<long long>(want, (long long)ctx->num_cus * per_cu);
+  const int cus = ctx->mlp_max_cus > 0 ? std::min(ctx->mlp_max_cus, ctx->num_cus) : ctx->num_cus;
+  long long grid = std::min<long long>(want, (long long)cus * per_cu);
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kThreads), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp_pair_kernel");

@@ -485,7 +485,9 @@ static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
     }
   }
   if (occ > 0 && want <= 2LL * occ * ctx->num_cus) per_cu = std::min(per_cu, occ);
-  const long long grid = std::max<long long>(1, std::min<long long>(want, (long long)ctx->num_cus * per_cu));
+  // rrtmgpnn_context_set_mlp_max_cus: at most that many CUs' worth of blocks (the waves stride the tiles)
+  const int cus = ctx->mlp_max_cus > 0 ? std::min(ctx->mlp_max_cus, ctx->num_cus) : ctx->num_cus;
+  const long long grid = std::max<long long>(1, std::min<long long>(want, (long long)cus * per_cu));
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), lds, ctx->stream, a);
   RRTMGPNN_LAUNCH_CHECK("mlp32_kernel");
   return RRTMGPNN_OK;

@@ -69,7 +69,7 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None, sw_after=None, sw_priority=0):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
@@ -257,9 +257,9 @@ class ClearSkyStep:
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
         self.sw_priority = sw_priority
-        self._finish(overlap, lw_after, sw_after)
+        self._finish(overlap, lw_after, sw_after, lw_net_cus)
 
-    def _finish(self, overlap, lw_after=None, sw_after=None):
+    def _finish(self, overlap, lw_after=None, sw_after=None, lw_net_cus=None):
         # fused: the small kernels that do not depend on a network's output go first in their chain, ahead of the big
         # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW solver
         # held while the LW solver, which needs it, could not start
@@ -287,6 +287,17 @@ class ClearSkyStep:
         if self.lw_after:
             self.calls = issue_order(self.calls, self.fused, self.lw_after)
             self._gate = torch.cuda.Event()
+        # lw_net_cus: the LW network's blocks on at most that many CUs (rrtmgpnn_context_set_mlp_max_cus; 0: all).
+        # Default with the LW chain gated on the SW network: 3/4 of the CUs.  Each LW network block holds a whole CU's
+        # LDS (117 KB), so on the full chip it kept the SW solver, launched beside it, off every CU for its first 75 us
+        # at C3; on 3/4 of them the SW solver starts at once on the rest.  Round 4, C3 whole steps (3 alternating
+        # triples): 0.4370-0.4409 ms on 192 CUs, 0.4374-0.4393 on 128, 0.4473-0.4504 on all 256.
+        if lw_net_cus is None:
+            lw_net_cus = 0
+            if self.overlap and self.lw_after:
+                lw_net_cus = 3 * torch.cuda.get_device_properties(self.dev).multi_processor_count // 4
+        self.lw_net_cus = int(lw_net_cus)
+        check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx.h, self.lw_net_cus), "context_set_mlp_max_cus")
         # sw_after: an LW-chain call the SW solver waits for (the two networks first, then the two solvers side by side)
         self.sw_after = sw_after if overlap else ""
         if self.sw_after:

@@ -98,6 +98,7 @@ def test_c_abi_errors_are_reported_not_crashed():
     assert b"null context" in L.rrtmgpnn_last_error()
     assert L.rrtmgpnn_context_set_sw_kernel(None, 4) != 0 and b"sw kernel mode" in L.rrtmgpnn_last_error()
     assert L.rrtmgpnn_context_set_sw_kernel(None, 0) == 0
+    assert L.rrtmgpnn_context_set_mlp_max_cus(None, 192) != 0 and b"null context" in L.rrtmgpnn_last_error()
 
 
 def _shard_worker(rank, world, port, q):
