@@ -288,14 +288,18 @@ class ClearSkyStep:
             self.calls = issue_order(self.calls, self.fused, self.lw_after)
             self._gate = torch.cuda.Event()
         # lw_net_cus: the LW network's blocks on at most that many CUs (rrtmgpnn_context_set_mlp_max_cus; 0: all).
-        # Default with the LW chain gated on the SW network: 3/4 of the CUs.  Each LW network block holds a whole CU's
-        # LDS (117 KB), so on the full chip it kept the SW solver, launched beside it, off every CU for its first 75 us
-        # at C3; on 3/4 of them the SW solver starts at once on the rest.  Round 4, C3 whole steps (3 alternating
-        # triples): 0.4370-0.4409 ms on 192 CUs, 0.4374-0.4393 on 128, 0.4473-0.4504 on all 256.
+        # Default with the LW chain gated on the SW network and an SW solver grid that fits in one round of resident
+        # waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane, against 16 per CU; C3): 5/8 of the CUs.
+        # Each LW network block holds a whole CU's LDS (117 KB), so on the full chip it kept the SW solver, launched
+        # beside it, off every CU for its first 75 us at C3; confined, it leaves the SW solver the other CUs from the
+        # start.  Round 4, C3 whole steps (3 alternating rounds, one box): 0.4350-0.4368 ms on 160 CUs, 0.4374-0.4379
+        # on 192, 0.4417-0.4434 on 224, 0.4456-0.4462 on all 256.  With more columns (C4) the cap costs 2 % (the SW
+        # solver is throughput-bound there; 2.705-2.726 on 192 against 2.651-2.664 ms); C5 equal.
         if lw_net_cus is None:
             lw_net_cus = 0
-            if self.overlap and self.lw_after:
-                lw_net_cus = 3 * torch.cuda.get_device_properties(self.dev).multi_processor_count // 4
+            cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
+            if self.overlap and self.lw_after and self.ncol * self.ng_sw <= 2048 * cus:
+                lw_net_cus = 5 * cus // 8
         self.lw_net_cus = int(lw_net_cus)
         check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx.h, self.lw_net_cus), "context_set_mlp_max_cus")
         # sw_after: an LW-chain call the SW solver waits for (the two networks first, then the two solvers side by side)
