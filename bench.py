@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--sw-priority", type=int, default=0, help="priority of the SW chain's stream (-1: high)")
     ap.add_argument("--lw-net-cus", type=int, default=None,
                     help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
-                         "choice, 3/4 of the CUs when the LW chain follows the SW network)")
+                         "choice: 5/8 of the CUs at small grids, where the LW chain follows the SW network)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
