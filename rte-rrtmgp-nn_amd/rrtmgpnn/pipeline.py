@@ -76,6 +76,7 @@ class ClearSkyStep:
         self.dev = torch.device("cuda", device)
         self.allsky = clouds is not None
         self.fused = fused
+        self._own_ctx = ctx is None  # a caller's context keeps its settings (the LW network's CU cap below)
         self.ctx = ctx or Context(device)
         L = self.L = _lib.lib()
         self.kd_lw, self.kd_sw = data.load_kdist("lw"), data.load_kdist("sw")
@@ -295,13 +296,16 @@ class ClearSkyStep:
         # start.  Round 4, C3 whole steps (3 alternating rounds, one box): 0.4350-0.4368 ms on 160 CUs, 0.4374-0.4379
         # on 192, 0.4417-0.4434 on 224, 0.4456-0.4462 on all 256.  With more columns (C4) the cap costs 2 % (the SW
         # solver is throughput-bound there; 2.705-2.726 on 192 against 2.651-2.664 ms); C5 equal.
+        # A caller's context is left as it is unless lw_net_cus is given.
+        explicit = lw_net_cus is not None
         if lw_net_cus is None:
             lw_net_cus = 0
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
-            if self.overlap and self.lw_after and self.ncol * self.ng_sw <= 2048 * cus:
+            if self._own_ctx and self.overlap and self.lw_after and self.ncol * self.ng_sw <= 2048 * cus:
                 lw_net_cus = 5 * cus // 8
         self.lw_net_cus = int(lw_net_cus)
-        check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx.h, self.lw_net_cus), "context_set_mlp_max_cus")
+        if self._own_ctx or explicit:
+            check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx.h, self.lw_net_cus), "context_set_mlp_max_cus")
         # sw_after: an LW-chain call the SW solver waits for (the two networks first, then the two solvers side by side)
         self.sw_after = sw_after if overlap else ""
         if self.sw_after:
