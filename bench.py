@@ -61,6 +61,7 @@ def parse():
                     "networks first, then the solvers side by side; none: no wait; default: the library pipeline's "
                     "choice)")
     ap.add_argument("--sw-priority", type=int, default=0, help="priority of the SW chain's stream (-1: high)")
+    ap.add_argument("--sw-net-cus", type=int, default=0, help="the SW network's blocks on at most this many CUs (0: all)")
     ap.add_argument("--lw-net-cus", type=int, default=None,
                     help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
                          "choice: 5/8 of the CUs at small grids, where the LW chain follows the SW network)")
@@ -263,7 +264,8 @@ def main():
                            lambda p, c: ClearSkyStep(p, device=local, fused=not args.unfused, clouds=c,
                                                      overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
                                                      lw_after=lw_after, sw_after=sw_after,
-                                                     sw_priority=args.sw_priority, lw_net_cus=args.lw_net_cus),
+                                                     sw_priority=args.sw_priority, lw_net_cus=args.lw_net_cus,
+                                                     sw_net_cus=args.sw_net_cus),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first
@@ -346,6 +348,8 @@ def main():
         # overlap measure) lifted for the measurement
         if serial and step.lw_net_cus:
             _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx.h, 0), "context_set_mlp_max_cus")
+        if serial and getattr(step, "sw_net_cus", 0):
+            _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx2.h, 0), "context_set_mlp_max_cus")
         step.step()  # warm the eager path
         torch.cuda.synchronize(dev)
         timing = {}
@@ -367,6 +371,8 @@ def main():
         torch.cuda.synchronize(dev)
         if serial and step.lw_net_cus:
             _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx.h, step.lw_net_cus), "context_set_mlp_max_cus")
+        if serial and getattr(step, "sw_net_cus", 0):
+            _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx2.h, step.sw_net_cus), "context_set_mlp_max_cus")
         return {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
 
     stages = time_stages(True)

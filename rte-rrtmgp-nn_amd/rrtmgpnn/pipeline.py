@@ -69,7 +69,7 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
@@ -258,9 +258,9 @@ class ClearSkyStep:
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
         self.sw_priority = sw_priority
-        self._finish(overlap, lw_after, sw_after, lw_net_cus)
+        self._finish(overlap, lw_after, sw_after, lw_net_cus, sw_net_cus)
 
-    def _finish(self, overlap, lw_after=None, sw_after=None, lw_net_cus=None):
+    def _finish(self, overlap, lw_after=None, sw_after=None, lw_net_cus=None, sw_net_cus=0):
         # fused: the small kernels that do not depend on a network's output go first in their chain, ahead of the big
         # ones: issued after the LW network (class-layer order), expand_emis waited ~75 us at C3 for CUs the SW solver
         # held while the LW solver, which needs it, could not start
@@ -321,6 +321,10 @@ class ClearSkyStep:
         self.ctx2 = None
         if overlap:
             self.ctx2 = Context(self.dev.index, self._sw_stream())
+            # sw_net_cus: the SW network's blocks on at most that many CUs (0: all; an A/B knob, not a default)
+            self.sw_net_cus = int(sw_net_cus or 0)
+            if self.sw_net_cus:
+                check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx2.h, self.sw_net_cus), "context_set_mlp_max_cus")
             self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
