@@ -75,6 +75,10 @@ def parse():
                          "(host arrays in and out, as a reference driver calls it)")
     ap.add_argument("--fortran-block", type=int, default=1800, help="--fortran: columns per block")
     ap.add_argument("--fortran-threads", type=int, default=1, help="--fortran: OpenMP threads over blocks")
+    ap.add_argument("--c5-steps", type=int, default=3,
+                    help="timed steps of the c5_global block every line carries (BASELINE configs[4]: 1e6 synthetic "
+                         "columns x 137 layers split over the ranks, streamed in 125 000-column chunks); 0: skip it")
+    ap.add_argument("--c5-warmup", type=int, default=1, help="untimed steps of the c5_global block")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline work")
     ap.add_argument("--cpu-kind", default="auto", choices=["auto", "reference", "port"],
@@ -472,6 +476,14 @@ def main():
         end_to_end = {"value": round(total_cols / (elapsed + gather_ms * 1e-3), 1), "unit": "columns/s",
                       "note": "all ranks' columns over the timed steps plus one final flux all-gather"}
 
+    # ---- BASELINE configs[4] as stated: 1e6 x 137 columns over the ranks (strong scaling), in every line ----
+    c5g = None
+    if args.config == "c5" and scaling == "strong" and global_cols == C5_GLOBAL_COLS:
+        c5g = {"same_as_main": True, "note": "this line's own workload is configs[4]: see value / ms_per_step / "
+                                             "gather_ms / gather_check"}
+    elif args.c5_steps > 0:
+        c5g = c5_global(args, world, rank, dev)
+
     # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -511,6 +523,7 @@ def main():
             "gather_check": gather_check,
             "end_to_end": end_to_end,
             "host_resident": pcie,
+            "c5_global": c5g,
         }
         if world > 1:
             out["ranks"] = {"launcher": ("bench.py --gpus %d (torch.distributed.run child)" % world
@@ -520,8 +533,94 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-        if not gather_check["ok"]:
+        if not gather_check["ok"] or (c5g and c5g.get("gather_check") and not c5g["gather_check"]["ok"]):
             sys.exit(1)
+
+
+C5_GLOBAL_COLS, C5_CHUNK, C5_NLAY = 1000000, 125000, 137
+
+
+def c5_global(args, world, rank, dev):
+    """BASELINE.json configs[4] exactly as stated -- 1e6 synthetic columns x 137 layers, clear-sky LW+SW, column-sharded
+    over the ranks -- measured beside the line's own workload, so that the driver's `--gpus N` runs (N = 1, 2, 4, 8)
+    record it: each rank takes its shard.column_range of the 1e6 columns and streams it through one step in chunks of
+    at most 125 000 columns (pipeline.ChunkedRank: 8 chunks at N = 1, one at N = 8; every chunk's inputs resident in
+    HBM, copied into the step's buffers inside the timed region).  The reference's own decomposition is the OpenMP
+    loop over column blocks of examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:364-446; the ranks replace the threads.
+    `--c5-warmup` untimed steps, then `--c5-steps` steps bracketed by barrier + synchronize, max over ranks; then the
+    final broadband flux all-gather (2.76 GB of (ncol, 5, 138) slabs) over RCCL, timed and checked as the main line's.
+    Synthetic columns: data.synthetic_problem (PCG64 streams seeded by (20251015, column block)), generated on host
+    threads, chunk by chunk."""
+    import torch
+    import torch.distributed as dist
+    from concurrent.futures import ThreadPoolExecutor
+    from rrtmgpnn import data, shard
+    from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
+    G, CH, NL = C5_GLOBAL_COLS, C5_CHUNK, C5_NLAY
+    lo, hi = shard.column_range(G, rank, world)
+    chunks = [(c, min(c + CH, hi)) for c in range(lo, hi, CH)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max(1, min(8, len(chunks)))) as ex:
+        futs = {c: ex.submit(data.synthetic_problem, c[1] - c[0], NL, seed=20251015, col0=c[0]) for c in chunks}
+        rr = ChunkedRank(lo, hi, CH, lambda c0, c1: (futs.pop((c0, c1)).result(), None),
+                         lambda p, c: ClearSkyStep(p, device=dev.index), use_graph=not args.no_graph)
+    rr.first = None  # the first chunk's host arrays are not needed here
+    setup_s = time.perf_counter() - t0
+    for _ in range(args.c5_warmup):
+        rr.run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.c5_steps):
+        rr.run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    slab = torch.stack(list(rr.flux), dim=1)  # (ncol, 5, nlev): lw_up, lw_dn, sw_up, sw_dn, sw_dir
+    finite = bool(torch.isfinite(slab).all().item())
+    gather_ms, check = None, {"ok": finite, "finite": finite,
+                              "note": "one rank: its slab is the global array, no exchange"}
+    if world > 1:
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        full = shard.gather_columns(slab, G, world)
+        torch.cuda.synchronize(dev)
+        gather_ms = (time.perf_counter() - g0) * 1e3
+        t = torch.tensor([gather_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gather_ms = float(t.item())
+        chk = shard.verify_gather(full, slab, G, rank, world)
+        ok = torch.tensor([1 if chk["ok"] else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        check = dict(chk, ok=bool(ok.item()), ranks_checked=world, gathered_bytes=full.numel() * 4,
+                     note="rank 0's view; ok is the minimum over ranks")
+        del full
+        if not check["ok"]:
+            sys.stderr.write("bench.py: c5_global flux all-gather check failed on some rank: %s\n" % chk)
+    steps = args.c5_steps
+    res = {"workload": "C5 (BASELINE configs[4]): 1e6 synthetic columns x 137 layers, clear-sky LW+SW, column-sharded "
+                       "over the ranks (shard.column_range), each rank streaming its range in chunks of <= 125000",
+           "global_columns": G, "nlay": NL, "n_gpus": world, "ncol_per_rank": hi - lo, "chunks_per_rank": len(chunks),
+           "chunk_columns": CH, "steps": steps, "warmup": args.c5_warmup, "scaling": "strong",
+           "ms_per_step": round(el / steps * 1e3, 3), "value": round(G * steps / el, 1), "unit": "columns/s",
+           "column_layers_per_s": round(G * steps / el * NL, 1),
+           "gather_ms": None if gather_ms is None else round(gather_ms, 3), "gather_check": check,
+           "end_to_end": {"value": round(G * steps / (el + (gather_ms or 0.0) * 1e-3), 1), "unit": "columns/s",
+                          "note": "the timed steps plus one final flux all-gather"},
+           "setup_s": round(setup_s, 1),
+           "data": "synthetic columns interpolated from RFMIP profiles (PCG64 streams seeded by (20251015, column "
+                   "block)), generated per chunk on host threads (setup_s, outside the timed region)"}
+    del rr, slab
+    torch.cuda.empty_cache()
+    return res
 
 
 def _subset(prob, idx):

@@ -68,6 +68,8 @@ int rrtmgpnn_context_set_mlp_kernel(rrtmgpnn_context *ctx, int mode);
  * streams: an LW network confined to part of the chip leaves the other CUs to the SW solver from its start (each LW
  * network block holds a whole CU's LDS).  Bit-identical outputs. */
 int rrtmgpnn_context_set_mlp_max_cus(rrtmgpnn_context *ctx, int cus);
+/* The cap rrtmgpnn_context_set_mlp_max_cus left in force on this context (0: every CU). */
+int rrtmgpnn_context_get_mlp_max_cus(rrtmgpnn_context *ctx, int *cus);
 void *rrtmgpnn_context_stream(rrtmgpnn_context *ctx);
 int rrtmgpnn_context_synchronize(rrtmgpnn_context *ctx);
 /* The context's device workspace grows on demand.  A call issued while the context's stream is captured into a

@@ -211,6 +211,14 @@ int rrtmgpnn_context_set_mlp_max_cus(rrtmgpnn_context *ctx, int cus)
   return RRTMGPNN_OK;
 }
 
+int rrtmgpnn_context_get_mlp_max_cus(rrtmgpnn_context *ctx, int *cus)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!cus) return fail(RRTMGPNN_ERR_ARGUMENT, "null cus");
+  *cus = ctx->mlp_max_cus;
+  return RRTMGPNN_OK;
+}
+
 int rrtmgpnn_context_set_stream(rrtmgpnn_context *ctx, void *hip_stream)
 {
   if (int rc = check_ctx(ctx)) return rc;

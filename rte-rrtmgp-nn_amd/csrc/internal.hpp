@@ -214,7 +214,7 @@ int launch_sw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
 // kernels_sw_ck.hip (checkpointed passes; called by launch_sw_2stream for even ngpt in mode 3)
 // the checkpointed SW kernel's small-grid instance applies (clear sky, g = 0, no g-point outputs, the grid in one round)
 bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bool inc, bool gpt);
-size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc);
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn);
 int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,

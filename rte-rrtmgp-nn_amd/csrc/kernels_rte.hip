@@ -131,6 +131,9 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
                                            float *__restrict__ flux_up, float *__restrict__ flux_dn)
 {
   static_assert(kRing % kPF == 0, "prefetch depth must divide the ring");
+  // the fused down pass takes lev(l+1)'s Planck fraction from the neighbouring prefetch slot, py[(r+1) % kPF]: with
+  // one slot that would be the layer's own pfrac
+  static_assert(!kFused || kPF >= 2, "the fused down pass needs at least two prefetch slots");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int icol = blockIdx.x, g = threadIdx.x;
   const bool on = g < ngpt;
@@ -740,7 +743,8 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   const bool x2 = !ck && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc ? 3 : 0);
-  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), inc)
+  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), inc,
+                                                     !g && !inc && !gpt)
                         : 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
   int rc = ctx->workspace(sizeof(float) * nws, &ws);
   if (rc) return rc;

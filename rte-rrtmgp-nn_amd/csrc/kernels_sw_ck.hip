@@ -135,6 +135,10 @@ constexpr int kCkP1 = 2;
 // when it also ran C3; since the small-grid instance took C3 over, the register floor spilled 19-21 VGPRs for no
 // residency gain: at 3 (no spill) the C5 shard's SW solver runs 10 % faster alone, 12 % with the ring of 9 (round 4).
 constexpr int kCkWavesNN = 3;
+// Workspace planes of the large-grid instances (as the small-grid instance's kCkTnSmall / kCkEmkSmall): the clear-sky
+// NN instance (C5) and the all-sky ones (C4).  A/B knobs (tools/ablations.py swck_nnplanes / swck_incplanes).
+constexpr bool kCkTnNN = false, kCkEmkNN = false;
+constexpr bool kCkTnInc = false, kCkEmkInc = false;
 
 // kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
 // broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
@@ -479,11 +483,15 @@ bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bo
 }
 
 // workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either
-// instance; small: plus the small-grid instance's plane of beam transmittances)
-size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc)
+// instance) plus the planes of the instance that runs: small-grid clear sky, large-grid clear sky (NN: g = NULL, no
+// increment, no g-point outputs) or all sky (inc)
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn)
 {
-  const size_t tn = (small && kCkTnSmall ? (size_t)ngpt * nlay * ncol : 0) +
-                    (small && kCkEmkSmall ? (size_t)ngpt * nlay * ncol : 0);
+  const int np = small ? (int)kCkTnSmall + (int)kCkEmkSmall
+                 : nn  ? (int)kCkTnNN + (int)kCkEmkNN
+                 : inc ? (int)kCkTnInc + (int)kCkEmkInc
+                       : 0;
+  const size_t tn = (size_t)np * ngpt * nlay * ncol;
   const int k = std::min(kCkK, kCkKSmall);
   const size_t nck = (size_t)(nlay + k - 1) / k;
   return (size_t)ngpt * ncol * (nck + 2 * (nck + 1)) + tn;
@@ -526,13 +534,13 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     bool pair = true;  // every band starts at an even (0-based) g-point
     for (int i = 0; i < b.nbnd; i++) pair = pair && ((b.lims[2 * i] - 1) % 2 == 0);
     constexpr int W = kCkWaves;
+    constexpr bool T = kCkTnInc, E = kCkEmkInc;
     if (pair && g)
-      return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W, false, f2, false, true>, tau_bnd, ssa_bnd, g_bnd);
+      return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W, T, f2, E, true>, tau_bnd, ssa_bnd, g_bnd);
     if (pair)
-      return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, W, false, f2, false, true>, tau_bnd, ssa_bnd,
-                g_bnd);
-    if (g) return go(sw_2stream_ck_kernel<true, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
-    return go(sw_2stream_ck_kernel<false, true, kCkK>, tau_bnd, ssa_bnd, g_bnd);
+      return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, W, T, f2, E, true>, tau_bnd, ssa_bnd, g_bnd);
+    if (g) return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W, T, f2, E>, tau_bnd, ssa_bnd, g_bnd);
+    return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, W, T, f2, E>, tau_bnd, ssa_bnd, g_bnd);
   }
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
@@ -541,7 +549,8 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
                                    kCkEmkSmall>,
               nullptr, nullptr, nullptr, kCkRingSmall, 2);
-  return go(sw_2stream_ck_kernel<false, false, kCkK>, nullptr, nullptr, nullptr);
+  return go(sw_2stream_ck_kernel<false, false, kCkK, false, kCkRing, kCkWavesNN, kCkTnNN, f2, kCkEmkNN>, nullptr,
+            nullptr, nullptr);
 }
 
 }  // namespace rrtmgpnn

@@ -24,6 +24,7 @@ SIGNATURES = {
     "rrtmgpnn_context_set_sw_kernel": (c_int, [c_vp, c_int]),
     "rrtmgpnn_context_set_mlp_kernel": (c_int, [c_vp, c_int]),
     "rrtmgpnn_context_set_mlp_max_cus": (c_int, [c_vp, c_int]),
+    "rrtmgpnn_context_get_mlp_max_cus": (c_int, [c_vp, ctypes.POINTER(c_int)]),
     "rrtmgpnn_context_unpin_workspace": (c_int, [c_vp]),
     "rrtmgpnn_sw_solver_noscat": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_context_stream": (c_vp, [c_vp]),

@@ -19,6 +19,8 @@ Layout: torch tensors in C order with the Fortran shape reversed (reference tau(
 tensor (ncol, nlay, ngpt) here): the bytes are identical, so the kernels see the reference layout.
 All compute runs in HIP kernels of librrtmgpnn.so; there is no torch/CPU compute path.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -62,6 +64,16 @@ class Context:
     def set_sw_kernel(self, mode):
         """0: SW two-stream kernel by ngpt (two g-points per lane when even; default); 1 / 2: one / two (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_sw_kernel(self.h, int(mode)), "context_set_sw_kernel")
+
+    def set_mlp_max_cus(self, cus):
+        """The gas-optics networks launched on this context on at most `cus` CUs (0: all; bit-identical)."""
+        check(_lib.lib().rrtmgpnn_context_set_mlp_max_cus(self.h, int(cus)), "context_set_mlp_max_cus")
+
+    def mlp_max_cus(self):
+        """The network CU cap in force on this context (0: every CU)."""
+        v = ctypes.c_int(0)
+        check(_lib.lib().rrtmgpnn_context_get_mlp_max_cus(self.h, ctypes.byref(v)), "context_get_mlp_max_cus")
+        return v.value
 
     def set_mlp_kernel(self, mode):
         """0: the gas-optics networks on 32x32x2 MFMA tiles where instantiated (default); 1: 16x16x4 (bit-identical)."""

@@ -9,6 +9,7 @@ reference's column-major arrays:  Fortran p_lay(nlay, ncol) <-> numpy (ncol, nla
 column = site + 100*expt as read_and_block_* reshape them, mo_rfmip_io.F90:74-680).
 `synthetic_problem()` builds the larger synthetic configurations (C4, C5 of BASELINE.json).
 """
+import functools
 import os
 
 import numpy as np
@@ -179,6 +180,16 @@ def _interp_base(base, nlay, pmin):
     return prof, gases
 
 
+@functools.lru_cache(maxsize=4)
+def _synthetic_base(nlay):
+    """(RFMIP base problem, its profiles on nlay layers, their gases, press_ref_min): the same for every column range
+    of one synthetic problem, so computed once per nlay (read only by synthetic_problem)."""
+    base = rfmip_problem()
+    pmin = np.float32(load_kdist("lw")["press_ref_min"][0])
+    prof, bgas = _interp_base(base, nlay, pmin)
+    return base, prof, bgas, pmin
+
+
 def synthetic_problem(ncol, nlay=60, seed=20251015, t_sigma=2.0, h2o_sigma=0.2, col0=0):
     """Columns [col0, col0 + ncol) of the synthetic clear-sky problem of BASELINE configs C4/C5.
 
@@ -189,10 +200,7 @@ def synthetic_problem(ncol, nlay=60, seed=20251015, t_sigma=2.0, h2o_sigma=0.2, 
     press_ref_min.  T += N(0, t_sigma K) clipped to the NN training range [160, 320.5] K; h2o *= lognormal(0,
     h2o_sigma) clipped to the NN range [xmin^4, xmax^4]; tsfc += N(0, t_sigma K).
     """
-    base = rfmip_problem()
-    kd = load_kdist("lw")
-    pmin = np.float32(kd["press_ref_min"][0])
-    prof, bgas = _interp_base(base, nlay, pmin)
+    base, prof, bgas, pmin = _synthetic_base(nlay)
     b0, b1 = col0 // SYN_BLOCK, (col0 + ncol + SYN_BLOCK - 1) // SYN_BLOCK
     pick, tn_lay, tn_lev, hf, tn_sfc = [], [], [], [], []
     for b in range(b0, b1):

@@ -296,16 +296,21 @@ class ClearSkyStep:
         # start.  Round 4, C3 whole steps (3 alternating rounds, one box): 0.4350-0.4368 ms on 160 CUs, 0.4374-0.4379
         # on 192, 0.4417-0.4434 on 224, 0.4456-0.4462 on all 256.  With more columns (C4) the cap costs 2 % (the SW
         # solver is throughput-bound there; 2.705-2.726 on 192 against 2.651-2.664 ms); C5 equal.
-        # A caller's context is left as it is unless lw_net_cus is given.
+        # A caller's context is left as it is unless lw_net_cus is given.  The caps are overlap measures: without a
+        # second stream both networks run on self.ctx, so a cap would confine the SW network too -- refused.
         explicit = lw_net_cus is not None
+        if not overlap and (lw_net_cus or sw_net_cus):
+            raise ValueError("lw_net_cus / sw_net_cus cap the networks of overlapped chains; overlap is off")
         if lw_net_cus is None:
             lw_net_cus = 0
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
             if self._own_ctx and self.overlap and self.lw_after and self.ncol * self.ng_sw <= 2048 * cus:
                 lw_net_cus = 5 * cus // 8
-        self.lw_net_cus = int(lw_net_cus)
         if self._own_ctx or explicit:
-            check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx.h, self.lw_net_cus), "context_set_mlp_max_cus")
+            self.ctx.set_mlp_max_cus(int(lw_net_cus))
+        # the cap in force on the LW context (a caller's context may carry its own), which bench.py's serialised stage
+        # timings lift and restore
+        self.lw_net_cus = self.ctx.mlp_max_cus()
         # sw_after: an LW-chain call the SW solver waits for (the two networks first, then the two solvers side by side)
         self.sw_after = sw_after if overlap else ""
         if self.sw_after:

@@ -83,3 +83,54 @@ def test_c5_shard_full_size_step_sampled_vs_oracle(dev, orc):
     lu, ld, _ = orc.clear_sky_lw(ps, [m["lw_abs"], m["lw_pfrac"]], data.load_kdist("lw"))
     su, sd, sr, _ = orc.clear_sky_sw(ps, [m["sw_abs"], m["sw_ray"]], data.load_kdist("sw"))
     _check(got, idx, ps, (lu, ld), (su, sd, sr))
+
+
+def test_c5_global_rank_chunked_full_size_sampled_vs_oracle(dev, orc):
+    """BASELINE configs[4] as bench.py runs it (--global, and every line's c5_global block): the 1e6 x 137 problem
+    split over 3 ranks, rank 1's range [333334, 666667) streamed through pipeline.ChunkedRank in 125 000-column chunks
+    -- two full chunks through one captured step and a short last one (83 333 columns) through a second -- run twice
+    (the slab refilled with nans in between), then a strided sample of the slab that includes every chunk's first and
+    last column compared bit for bit with the oracle on those columns."""
+    from concurrent.futures import ThreadPoolExecutor
+    from rrtmgpnn import data, shard
+    from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
+    G, CH, NL = 1000000, 125000, 137
+    lo, hi = shard.column_range(G, 1, 3)
+    chunks = [(c, min(c + CH, hi)) for c in range(lo, hi, CH)]
+    assert len(chunks) == 3 and chunks[-1][1] - chunks[-1][0] < CH
+    with ThreadPoolExecutor(3) as ex:
+        futs = {c: ex.submit(data.synthetic_problem, c[1] - c[0], NL, seed=20251015, col0=c[0]) for c in chunks}
+        rank = ChunkedRank(lo, hi, CH, lambda c0, c1: (futs.pop((c0, c1)).result(), None),
+                           lambda p, c: ClearSkyStep(p, device=0), use_graph=True)
+    rank.first = None
+    assert len(rank.steps) == 2
+    for rep in range(2):
+        for t in rank.flux:
+            t.fill_(float("nan"))
+        rank.run()
+        torch.cuda.synchronize()
+    got = dict(zip(("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir"), (t.cpu().numpy() for t in rank.flux)))
+    del rank
+    torch.cuda.empty_cache()
+    for v in got.values():
+        assert np.isfinite(v).all()
+    edges = [c - lo for c0, c1 in chunks for c in (c0, c1 - 1)]
+    idx = np.unique(np.concatenate([_sample(hi - lo, 300), edges]))
+    # the sampled global columns, generated alone (synthetic_problem is column-addressable)
+    parts = [data.synthetic_problem(1, NL, seed=20251015, col0=lo + int(i)) for i in idx]
+    ps = _concat(parts)
+    m = {k: data.load_model(k) for k in ("lw_abs", "lw_pfrac", "sw_abs", "sw_ray")}
+    lu, ld, _ = orc.clear_sky_lw(ps, [m["lw_abs"], m["lw_pfrac"]], data.load_kdist("lw"))
+    su, sd, sr, _ = orc.clear_sky_sw(ps, [m["sw_abs"], m["sw_ray"]], data.load_kdist("sw"))
+    _check(got, idx, ps, (lu, ld), (su, sd, sr))
+
+
+def _concat(parts):
+    """One problem dict of single-column problems, in order."""
+    out = dict(parts[0])
+    for k, v in parts[0].items():
+        if isinstance(v, np.ndarray) and v.ndim >= 1 and v.shape[0] == 1:
+            out[k] = np.concatenate([p[k] for p in parts])
+    out["gases"] = {k: np.concatenate([p["gases"][k] for p in parts]) for k in parts[0]["gases"]}
+    out["ncol"] = len(parts)
+    return out

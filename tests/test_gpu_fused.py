@@ -177,6 +177,10 @@ def test_two_stream_overlap_is_bitwise_identical(dev, rfmip, allsky, lw_after):
     # default at this size (450 columns): the LW chain after the SW network
     assert two.lw_after == {"": "predict_nn_sw", "none": "", "sw_solver": "sw_solver", "nets_first": ""}[lw_after]
     assert two.sw_after == ("predict_nn_lw" if nets_first else "")
+    # the LW network's CU cap is on whenever the LW chain is gated at this size (the default), off when the chains
+    # start together, and the step records the cap the context actually holds
+    assert (two.lw_net_cus > 0) == bool(two.lw_after)
+    assert two.lw_net_cus == two.ctx.mlp_max_cus()
     one.step()
     two.step()
     torch.cuda.synchronize()
@@ -322,3 +326,67 @@ def test_fused_lw_any_nlay(dev, orc, nlay, top_at_1, lw_ds):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(up.cpu().numpy(), up_o)
     np.testing.assert_array_equal(dn.cpu().numpy(), dn_o)
+
+
+@pytest.mark.parametrize("cap", ["1", "eighth"])
+def test_network_cu_cap_is_bitwise(dev, rfmip, cap, mlp_kernel):
+    """rrtmgpnn_context_set_mlp_max_cus: the fused gas-optics networks (LW pair, SW pair) on one CU's worth of blocks
+    (every wave strides many tiles) or an eighth of the chip give the uncapped outputs bit for bit, for both MFMA
+    tilings."""
+    from rrtmgpnn import _lib
+    from rrtmgpnn._lib import check
+    from rrtmgpnn.pipeline import ClearSkyStep
+    prob = subset(rfmip, np.arange(0, 1800, 4))
+    st = ClearSkyStep(prob, device=0, overlap=False)
+    assert st.lw_net_cus == 0 and st.ctx.mlp_max_cus() == 0
+    calls = [(n, f, a) for n, f, a in st.calls if n in ("predict_nn_lw", "predict_nn_sw")]
+    outs = (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)
+
+    def run():
+        for t in outs:
+            t.fill_(float("nan"))
+        for n, f, a in calls:
+            check(f(*a), n)
+        torch.cuda.synchronize()
+        return [t.cpu().numpy().copy() for t in outs]
+
+    ref = run()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 1 if cap == "1" else max(1, cus // 8)
+    st.ctx.set_mlp_max_cus(n)
+    assert st.ctx.mlp_max_cus() == n
+    got = run()
+    st.ctx.set_mlp_max_cus(0)
+    for k, (a, b) in enumerate(zip(ref, got)):
+        assert np.isfinite(a).all()
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=str(k))
+    with pytest.raises(ValueError):
+        ClearSkyStep(prob, device=0, overlap=False, lw_net_cus=64)
+
+
+def test_set_stream_inside_a_global_capture(dev, rfmip):
+    """rrtmgpnn_context_set_stream called while the NEW stream is being captured into a hipGraph (global capture mode):
+    the context's old stream is idle and not capturing, so set_stream synchronises it; the call must succeed, the
+    kernel issued next must be captured, and the replay must give the eager result bit for bit."""
+    from rrtmgpnn.pipeline import ClearSkyStep
+    prob = subset(rfmip, np.arange(1, 1800, 9))
+    st = ClearSkyStep(prob, device=0, overlap=False)
+    st.step()
+    torch.cuda.synchronize()
+    ref = st.fluxes()
+    old = st.ctx.stream
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="global"):
+            st.ctx.use_stream(s)  # inside the capture
+            st.step()
+    st.ctx.use_stream(old)
+    for t in (st.lw_up, st.lw_dn, st.sw_up, st.sw_dn, st.sw_dir):
+        t.fill_(float("nan"))
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    got = st.fluxes()
+    for k in ref:
+        np.testing.assert_array_equal(ref[k], got[k], err_msg=k)

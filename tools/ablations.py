@@ -50,8 +50,10 @@ def parametric(name):
     swck_planes:T:E -- its beam-transmittance (T) and exp(-k tau) (E) workspace planes on (1) or off (0);
     swck_big:K:R:W -- the large-grid instances' chunk length, ring levels and wave floor (the all-sky ones; C4);
     swck_nnw:W -- the large-grid clear-sky (NN) instance's wave floor (C5);
-    mlp_sw:NT:W -- the SW network's threads per block and waves-per-SIMD floor (kernels_nn32.hip);
-    mlp_lwgrid:N -- the LW network's grid capped at N blocks."""
+    swck_nnplanes:T:E / swck_incplanes:T:E -- the same planes in the large-grid clear-sky (C5) / all-sky (C4)
+    instances;
+    mlp_sw:NT:W -- the SW network's threads per block and waves-per-SIMD floor (kernels_nn32.hip).
+    (The LW network's grid cap is a library call now, rrtmgpnn_context_set_mlp_max_cus / bench.py --lw-net-cus.)"""
     f = name.split(":")
     if f[0] == "swck_small" and len(f) == 4:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkKSmall = %s, kCkRingSmall = %s, kCkWavesSmall = %s;"
@@ -62,11 +64,11 @@ def parametric(name):
     if f[0] == "swck_nnw" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkWavesNN = %s;" % f[1],
                  r"constexpr int kCkWavesNN = \d+;")]
-    if f[0] == "mlp_lwgrid" and len(f) == 2:  # the LW pair's grid capped at N blocks (the rest of the CUs free)
-        return [("kernels_nn32.hip", None,
-                 "const long long grid = std::max<long long>(1, std::min<long long>(std::min<long long>(want, "
-                 "MODE == MLP_LW_PAIR ? %s : want), (long long)ctx->num_cus * per_cu));" % f[1],
-                 r"const long long grid = std::max<long long>\(1, std::min<long long>\(want, \(long long\)ctx->num_cus \* per_cu\)\);")]
+    if f[0] in ("swck_nnplanes", "swck_incplanes") and len(f) == 3:
+        t, e = ("true" if v == "1" else "false" for v in f[1:])
+        suf = "NN" if f[0] == "swck_nnplanes" else "Inc"
+        return [("kernels_sw_ck.hip", None, "constexpr bool kCkTn%s = %s, kCkEmk%s = %s;" % (suf, t, suf, e),
+                 r"constexpr bool kCkTn%s = \w+, kCkEmk%s = \w+;" % (suf, suf))]
     if f[0] == "mlp_sw" and len(f) == 3:
         return [("kernels_nn32.hip", None, "constexpr int kMlp32Threads = 512, kSwNT = %s, kSwWPE = %s;" % tuple(f[1:]),
                  r"constexpr int kMlp32Threads = 512, kSwNT = \d+, kSwWPE = \d+;")]
