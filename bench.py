@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--lw-net-cus", type=int, default=None,
                     help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
                          "choice: 5/8 of the CUs at small grids, where the LW chain follows the SW network)")
+    ap.add_argument("--lw-tail", type=float, default=0.0,
+                    help="fraction of the columns whose LW solver runs as a second launch after the SW solver "
+                         "(pipeline.ClearSkyStep lw_tail; 0: one LW solver launch)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
@@ -269,7 +272,7 @@ def main():
                                                      overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
                                                      lw_after=lw_after, sw_after=sw_after,
                                                      sw_priority=args.sw_priority, lw_net_cus=args.lw_net_cus,
-                                                     sw_net_cus=args.sw_net_cus),
+                                                     sw_net_cus=args.sw_net_cus, lw_tail=args.lw_tail),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first
@@ -377,7 +380,10 @@ def main():
             _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx.h, step.lw_net_cus), "context_set_mlp_max_cus")
         if serial and getattr(step, "sw_net_cus", 0):
             _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx2.h, step.sw_net_cus), "context_set_mlp_max_cus")
-        return {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
+        res = {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
+        if "lw_solver_tail" in res:  # the LW solver's two launches (lw_tail) are one stage
+            res["lw_solver"] += res.pop("lw_solver_tail")
+        return res
 
     stages = time_stages(True)
     stages_ov = time_stages(False) if step.overlap else None
@@ -509,7 +515,9 @@ def main():
                                  (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
                                  (" (LW network on %d CUs)" % step.lw_net_cus if step.lw_net_cus else "") +
                                  (", the SW solver after %s" % step.sw_after if step.sw_after else "") +
-                                 (", SW stream priority %d" % step.sw_priority if step.sw_priority else ""),
+                                 (", SW stream priority %d" % step.sw_priority if step.sw_priority else "") +
+                                 (", the LW solver of the last %d columns after the SW solver" % step.lw_tail_cols
+                                  if getattr(step, "lw_tail_cols", 0) else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
                                    "fused Planck-in-LW-solver, g=0 elided" +
                                    (", cloud increments fused into both solvers" if step.allsky else ""))},
@@ -708,7 +716,9 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=7, bind="non
                 return run(nthr, n, nreps)
 
             try:
+                load0, wall0 = os.getloadavg(), time.time()
                 res = measure(threads, target_s, reps)
+                load1 = os.getloadavg()
                 sweep = {}
                 for t in sorted({1, min(8, threads)} - {threads}):
                     r = measure(t, max(2.0, target_s / 5), 3)
@@ -733,6 +743,11 @@ def cpu_baseline(prob, clouds, target_s, kind="auto", sw=True, reps=7, bind="non
         ss = sorted(secs)
         return {"value": round(value, 1), "unit": "columns/s", "cores": threads, "kind": "reference",
                 "nproc": nproc, "runs_s": [round(t, 4) for t in secs],
+                # each run's start (s after the first timed run's) and the host's load averages around the
+                # measurement, so a slow run can be tied to other tenants' load on the box
+                "runs_start_s": [round(t, 3) for t in res.get("starts", [])],
+                "host_loadavg": {"before": [round(x, 2) for x in load0], "after": [round(x, 2) for x in load1],
+                                 "wall_start_unix": round(wall0, 1)},
                 "spread": round((max(secs) - min(secs)) / med, 4),
                 # without the fastest and the slowest run (other tenants' load on the host shows up as single outliers)
                 "spread_trimmed": round((ss[-2] - ss[1]) / med, 4) if len(ss) >= 5 else None,

@@ -108,8 +108,8 @@ program rrtmgp_cpu_bench
   real(wp) :: tmin_lw, tdelta_lw, def_tsi
   type(ty_cloud_optics) :: co_lw, co_sw
   logical :: top_at_1, allsky
-  real(8), allocatable :: secs(:)
-  real(8) :: t0
+  real(8), allocatable :: secs(:), starts(:)
+  real(8) :: t0, tfirst
   character(len=128) :: e
   character(len=512) :: ofile
   character(len=32) :: num
@@ -186,7 +186,7 @@ program rrtmgp_cpu_bench
     call load_clouds(trim(ddir) // "/cloud_optics_sw.rbin", wvn_sw, co_sw)
   end if
 
-  allocate(secs(nreps))
+  allocate(secs(nreps), starts(nreps))
   keep = .false.
   ! one untimed pass first (thread creation, MKL initialisation, first touch of every array)
   rep = nblocks
@@ -201,6 +201,8 @@ program rrtmgp_cpu_bench
       o_lwu = 0._wp; o_lwd = 0._wp; o_swu = 0._wp; o_swd = 0._wp; o_swr = 0._wp
     end if
     t0 = omp_get_wtime()
+    if (rep == 1) tfirst = t0
+    starts(rep) = t0 - tfirst
     call run_blocks()
     secs(rep) = omp_get_wtime() - t0
   end do
@@ -223,6 +225,14 @@ program rrtmgp_cpu_bench
   line = line // ', "columns": ' // trim(num) // ', "seconds": ['
   do rep = 1, nreps
     write(num, '(f0.6)') secs(rep)
+    if (num(1:1) == '.') num = '0' // num
+    line = line // trim(num)
+    if (rep < nreps) line = line // ', '
+  end do
+  ! each run's start, seconds after the first timed run's (a slow run can then be tied to the host's load over time)
+  line = line // '], "starts": ['
+  do rep = 1, nreps
+    write(num, '(f0.6)') starts(rep)
     if (num(1:1) == '.') num = '0' // num
     line = line // trim(num)
     if (rep < nreps) line = line // ', '

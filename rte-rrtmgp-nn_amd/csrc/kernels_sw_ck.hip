@@ -136,9 +136,14 @@ constexpr int kCkP1 = 2;
 // residency gain: at 3 (no spill) the C5 shard's SW solver runs 10 % faster alone, 12 % with the ring of 9 (round 4).
 constexpr int kCkWavesNN = 3;
 // Workspace planes of the large-grid instances (as the small-grid instance's kCkTnSmall / kCkEmkSmall): the clear-sky
-// NN instance (C5) and the all-sky ones (C4).  A/B knobs (tools/ablations.py swck_nnplanes / swck_incplanes).
-constexpr bool kCkTnNN = false, kCkEmkNN = false;
-constexpr bool kCkTnInc = false, kCkEmkInc = false;
+// NN instance (C5) and the all-sky ones (C4).  Round 5 (tools/kernel_ab.py alone, tools/gpu_ab.sh whole steps;
+// bitwise): the C5 shard's SW solver 32.68 -> 31.64 ms with both planes (the transmittances alone 32.24, exp(-k tau)
+// alone 33.23: with both, pass 3 reads no tau), whole steps 66.63 -> 64.77 ms (2 alternating pairs); the large grid is
+// then at HBM (199 GB per launch at 6.3 TB/s) where it was at its VALU floor (valu_busy 0.99, 3.35 TB/s).  C4 all sky:
+// the transmittance plane 1.480 -> 1.458 ms alone (1.50 -> 1.435 in steps), steps within noise (-0.5 %); exp(-k tau)
+// +1.3 %.  A/B knobs: tools/ablations.py swck_nnplanes / swck_incplanes.
+constexpr bool kCkTnNN = true, kCkEmkNN = true;
+constexpr bool kCkTnInc = true, kCkEmkInc = false;
 
 // kGpt: also store the g-point fluxes (ty_fluxes_flexible: up, total down, direct; (ngpt, nlay+1, ncol)) and sum the
 // broadband down flux from the total as sw_solver_2stream does when it saves them (:572-588, :660-684)
@@ -157,13 +162,16 @@ constexpr bool kCkTnInc = false, kCkEmkInc = false;
 constexpr int kCkKSmall = 3, kCkRingSmall = 9, kCkWavesSmall = 2;
 constexpr bool kCkTnSmall = true, kCkEmkSmall = true;
 using VSmall = f2;
+// pass-1 chunks per load step of the small-grid instance (its pass 1 is latency-bound at C3: 10 dependent load steps
+// of 6 layers per 60-layer column with the default)
+constexpr int kCkP1Small = 2;
 
 // V: f2 (two g-points per lane) or float (one per lane).  kBandPair (fused increment, two g-points per lane): every
 // band starts at an even g-point, so both g-points of a lane lie in one band and its band values are one load each
 // (the RRTMGP g-point sets: 16 per band).  Round 4, C4: SW solver -1.7 % alone, steps -0.8 % (3 alternating pairs)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? kCkWavesNN : kCkWaves, bool kTn = false,
-          class V = f2, bool kEmk = false, bool kBandPair = false>
+          class V = f2, bool kEmk = false, bool kBandPair = false, int P1C = kCkP1>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -298,7 +306,7 @@ __global__ void __launch_bounds__(512, WAVES)
   // Steps of P1 = kCkP1 * K layers: pass 1 has little arithmetic per layer, so it needs many loads in flight.
   V Fd = Ftop;
   {
-    constexpr int P1 = kCkP1 * K;
+    constexpr int P1 = P1C * K;
     const int np1 = (nlay + P1 - 1) / P1;
     struct Buf1 {
       V t[P1];
@@ -323,7 +331,7 @@ __global__ void __launch_bounds__(512, WAVES)
       }
 #pragma unroll
       for (int p = 0; p < P1; p++) {
-        if (p % K == 0) CW.stv(Fd, (p < n) ? vWs : kBufOOB, row * (uint32_t)(c1 * kCkP1 + p / K));
+        if (p % K == 0) CW.stv(Fd, (p < n) ? vWs : kBufOOB, row * (uint32_t)(c1 * P1C + p / K));
         Fd = (p < n) ? Tn[p] * Fd : Fd;
       }
     };
@@ -547,8 +555,8 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   // waves per CU)
   if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
     return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
-                                   kCkEmkSmall>,
-              nullptr, nullptr, nullptr, kCkRingSmall, 2);
+                                   kCkEmkSmall, false, kCkP1Small>,
+              nullptr, nullptr, nullptr, kCkRingSmall, (int)(sizeof(VSmall) / sizeof(float)));
   return go(sw_2stream_ck_kernel<false, false, kCkK, false, kCkRing, kCkWavesNN, kCkTnNN, f2, kCkEmkNN>, nullptr,
             nullptr, nullptr);
 }

@@ -40,7 +40,7 @@ SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw"
 
 # issue order of the fused step (stable sort; names not listed keep their place at the end)
 FUSED_ORDER = ["get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", "predict_nn_lw", "lw_solver",
-               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver"]
+               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver", "lw_solver_tail"]
 
 
 def issue_order(calls, fused, lw_after=""):
@@ -69,7 +69,7 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0, lw_tail=0.0):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
@@ -207,6 +207,26 @@ class ClearSkyStep:
                      (c, ncol, nlay, self.ng_lw, self.nb_lw, self._lims_lw, p(self.tau_lw), None, None,
                       p(self.cld_tau_lw), None, None)),
                 ]
+        # lw_tail: the last fraction of the columns' LW solver runs as a second launch ("lw_solver_tail") that waits for
+        # the SW solver (overlapped fused steps): the SW solver, the critical path, shares the chip with less LW work,
+        # and the tail runs on the chip it leaves (same kernel on a column range: same bits)
+        ntail = int(round(float(lw_tail) * ncol)) if (fused and sw and overlap) else 0
+        self.lw_tail_cols = ntail = min(max(ntail, 0), ncol - 1)
+        if ntail:
+            n1 = ncol - ntail
+            (nm, fn, a), = lw_calls
+            a = list(a)
+            head, tail = list(a), list(a)
+            head[3], tail[3] = n1, ntail
+            G, b = self.ng_lw, 4  # float bytes
+            off = {9: n1 * nlay * G * b, 10: n1 * nlay * G * b, 13: n1 * nlay * b, 14: n1 * (nlay + 1) * b,
+                   15: n1 * b, 22: n1 * self.nb_lw * b, 23: n1 * (nlay + 1) * b, 24: n1 * (nlay + 1) * b}
+            if self.allsky:  # the cloud optical depth by band sits after tau: every later index moves by one
+                off = {(k if k < 10 else k + 1): v for k, v in off.items()}
+                off[10] = n1 * nlay * self.nb_lw * b
+            for k, v in off.items():
+                tail[k] = tail[k] + v
+            lw_calls = [(nm, fn, tuple(head)), ("lw_solver_tail", fn, tuple(tail))]
         self.calls += lw_calls
         if not sw:
             self.calls = [c for c in self.calls if c[0] != "cloud_optics_sw"]
@@ -259,6 +279,8 @@ class ClearSkyStep:
             ]
         self.sw_priority = sw_priority
         self._finish(overlap, lw_after, sw_after, lw_net_cus, sw_net_cus)
+        if self.lw_tail_cols:
+            self._tail_gate = torch.cuda.Event()
 
     def _finish(self, overlap, lw_after=None, sw_after=None, lw_net_cus=None, sw_net_cus=0):
         # fused: the small kernels that do not depend on a network's output go first in their chain, ahead of the big
@@ -371,6 +393,8 @@ class ClearSkyStep:
         for name, fn, args in self.calls:
             if self.sw_after and name == "sw_solver":
                 self.ctx2.stream.wait_event(self._gate2)
+            if name == "lw_solver_tail":
+                self.ctx.stream.wait_event(self._tail_gate)
             if timing is not None:
                 s = self.stream_for(name)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -389,6 +413,8 @@ class ClearSkyStep:
                 self.ctx.stream.wait_event(self._gate)
             if self.sw_after and name == self.sw_after:
                 self._gate2.record(self.ctx.stream)
+            if name == "sw_solver" and getattr(self, "lw_tail_cols", 0):
+                self._tail_gate.record(self.ctx2.stream)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)

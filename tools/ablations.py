@@ -30,6 +30,39 @@ ABLATIONS = {
                        "  // ablation mlp32_nostore\n", "replace")],
 }
 
+ABLATIONS.update({
+    # SW pair (32x32x2 kernel): stores dropped unless a value is a nan (the write path's share of the kernel)
+    "mlp32_sw_nostore": [("kernels_nn32.hip", """          const uint32_t off = vo[r] + 128u * go;
+          o0.st(tot, off);
+          o1.st(ssa, off);""", """          const uint32_t off = (tot != tot || ssa != ssa) ? vo[r] + 128u * go : kOOB;  // ablation mlp32_sw_nostore
+          o0.st(tot, off);
+          o1.st(ssa, off);""", "replace")],
+    # SW pair: the same bytes as 16-byte stores (lane (c, h) writes 16 bytes of row 8b + 4h + (c >> 3) at g-point
+    # 32go + 4(c & 7): 4 dwordx4 per array and g-tile instead of 16 dwords) -- values scrambled, addresses and widths
+    # those of a transposed epilogue (the store width's share of the kernel)
+    "mlp32_sw_st4": [("kernels_nn32.hip", """          const uint32_t off = vo[r] + 128u * go;
+          o0.st(tot, off);
+          o1.st(ssa, off);
+        }""", """          tots[r] = tot;
+          ssas[r] = ssa;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++) {  // ablation mlp32_sw_st4
+          const uint32_t R = 8u * b + 4u * h + ((uint32_t)j >> 3);
+          const uint32_t off = R < nvalid ? 4u * (R * (uint32_t)ngpt) + 128u * go + 16u * ((uint32_t)j & 7u) : kOOB;
+          o0.st4((floatx4){tots[4 * b], tots[4 * b + 1], tots[4 * b + 2], tots[4 * b + 3]}, off);
+          o1.st4((floatx4){ssas[4 * b], ssas[4 * b + 1], ssas[4 * b + 2], ssas[4 * b + 3]}, off);
+        }""", "replace"),
+                     ("kernels_nn32.hip", """        const float bB = iB[LB.b3 + g], sdB = iB[LB.sd + g], mnB = iB[LB.mn + g];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          float ta""", """        const float bB = iB[LB.b3 + g], sdB = iB[LB.sd + g], mnB = iB[LB.mn + g];
+        float tots[16], ssas[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          float ta""", "replace")],
+})
+
 # Variants that keep the bits (tools/kernel_ab.py checks them bitwise against the default library): A/B candidates
 ABLATIONS.update({
     # SW checkpointed solver: scheduling fences between a pass's chunk bodies and their prefetches (rounds 2-3)
@@ -64,6 +97,10 @@ def parametric(name):
     if f[0] == "swck_nnw" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkWavesNN = %s;" % f[1],
                  r"constexpr int kCkWavesNN = \d+;")]
+    if f[0] == "swck_p1small" and len(f) == 2:
+        return [("kernels_sw_ck.hip", None, "constexpr int kCkP1Small = %s;" % f[1], r"constexpr int kCkP1Small = \d+;")]
+    if f[0] == "swck_vsmall" and len(f) == 2:
+        return [("kernels_sw_ck.hip", None, "using VSmall = %s;" % f[1], r"using VSmall = \w+;")]
     if f[0] in ("swck_nnplanes", "swck_incplanes") and len(f) == 3:
         t, e = ("true" if v == "1" else "false" for v in f[1:])
         suf = "NN" if f[0] == "swck_nnplanes" else "Inc"

@@ -11,12 +11,12 @@ timeout -k 10 ${PYTEST_TIMEOUT:-600} python -m pytest tests -m gpu -q ${PYTEST_A
 rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
 ok $rc || exit $rc
 echo "== bench"
-timeout -k 10 300 python bench.py --steps $STEPS --warmup 5 ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
+timeout -k 10 300 python bench.py --steps $STEPS --warmup 5 ${BENCH_ARGS:-} --c5-steps 0 > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err
 ok $rc || exit $rc
 if [ "${PROFILE:-1}" = "1" ]; then
   echo "== rocprofv3 kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} --c5-steps 0 > gpurun_out/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.log
   [ $rc -eq 0 ] || exit $rc
   find gpurun_out/prof -name "*stats*" | head
@@ -25,7 +25,7 @@ if [ "${PMC:-0}" = "1" ]; then
   # HBM bytes per launch: FETCH_SIZE and WRITE_SIZE in separate passes (MI355X_MICROARCH.md, HBM section)
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== rocprofv3 --pmc $c"
-    timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} > gpurun_out/pmc_$c.log 2>&1
+    timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-graph ${BENCH_ARGS:-} --c5-steps 0 > gpurun_out/pmc_$c.log 2>&1
     rc=$?; echo "pmc $c rc=$rc"; tail -2 gpurun_out/pmc_$c.log
     [ $rc -eq 0 ] || exit $rc
   done

@@ -16,18 +16,18 @@ for cfg in ${CONFIGS:-c3 c4}; do
   o=gpurun_out/$cfg
   mkdir -p $o
   echo "== $cfg rocprofv3 kernel trace"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof_iso -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --no-overlap ${BENCH_ARGS:-} > $o/prof_iso.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --c5-steps 0 ${BENCH_ARGS:-} > $o/prof.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/prof_iso -o run --output-format csv -- python3 bench.py --config $cfg --steps $STEPS --warmup 5 --no-cpu-baseline --c5-steps 0 --no-overlap ${BENCH_ARGS:-} > $o/prof_iso.log 2>&1 || exit $?
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "== $cfg rocprofv3 --pmc $c"
-    timeout -k 10 300 rocprofv3 --pmc $c -d $o/pmc_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph --settle-s 0 ${BENCH_ARGS:-} > $o/pmc_$c.log 2>&1 || exit $?
+    timeout -k 10 300 rocprofv3 --pmc $c -d $o/pmc_$c -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --c5-steps 0 --no-graph --settle-s 0 ${BENCH_ARGS:-} > $o/pmc_$c.log 2>&1 || exit $?
   done
   python3 tools/pmc_traffic.py $o/pmc_FETCH_SIZE $o/pmc_WRITE_SIZE $cfg gpurun_out/pmc_traffic.json > $o/pmc_traffic.txt || exit $?
   echo "== $cfg rocprofv3 --pmc SQ counters"
-  timeout -k 10 300 rocprofv3 --pmc $SQ -d $o/pmc_SQ -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph --settle-s 0 ${BENCH_ARGS:-} > $o/pmc_SQ.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $SQ -d $o/pmc_SQ -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --c5-steps 0 --no-graph --settle-s 0 ${BENCH_ARGS:-} > $o/pmc_SQ.log 2>&1 || exit $?
   python3 tools/pmc_counters.py $o/pmc_SQ gpurun_out/pmc_sq.json $cfg > $o/pmc_sq.txt || exit $?
   echo "== $cfg rocprofv3 --pmc MFMA counters"
-  timeout -k 10 300 rocprofv3 --pmc $MFMA -d $o/pmc_MFMA -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --no-graph --settle-s 0 ${BENCH_ARGS:-} > $o/pmc_MFMA.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $MFMA -d $o/pmc_MFMA -o run --output-format csv -- python3 bench.py --config $cfg --steps 5 --warmup 2 --no-cpu-baseline --c5-steps 0 --no-graph --settle-s 0 ${BENCH_ARGS:-} > $o/pmc_MFMA.log 2>&1 || exit $?
   python3 tools/pmc_counters.py $o/pmc_MFMA gpurun_out/pmc_sq.json $cfg > $o/pmc_mfma.txt || exit $?
   # the bench line last, so its roofline carries this build's PMC traffic and SQ figures
   echo "== $cfg bench"
