@@ -566,6 +566,8 @@ def c5_global(args, world, rank, dev):
     from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
     G, CH, NL = C5_GLOBAL_COLS, C5_CHUNK, C5_NLAY
     lo, hi = shard.column_range(G, rank, world)
+    torch.cuda.synchronize(dev)
+    free0 = torch.cuda.mem_get_info(dev)[0]
     chunks = [(c, min(c + CH, hi)) for c in range(lo, hi, CH)]
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max(1, min(8, len(chunks)))) as ex:
@@ -591,8 +593,10 @@ def c5_global(args, world, rank, dev):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    free1 = torch.cuda.mem_get_info(dev)[0]  # steps, workspaces and chunk inputs in place
     slab = torch.stack(list(rr.flux), dim=1)  # (ncol, 5, nlev): lw_up, lw_dn, sw_up, sw_dn, sw_dir
     finite = bool(torch.isfinite(slab).all().item())
+    slab_bytes = slab.numel() * 4
     gather_ms, check = None, {"ok": finite, "finite": finite,
                               "note": "one rank: its slab is the global array, no exchange"}
     if world > 1:
@@ -624,6 +628,13 @@ def c5_global(args, world, rank, dev):
            "end_to_end": {"value": round(G * steps / (el + (gather_ms or 0.0) * 1e-3), 1), "unit": "columns/s",
                           "note": "the timed steps plus one final flux all-gather"},
            "setup_s": round(setup_s, 1),
+           # this block's device memory on the rank: torch's allocator peak (steps, chunk inputs, flux slab, gathered
+           # array) plus the library's own buffers (network images, workspaces: rrtmgpnn_context_workspace_bytes)
+           "hbm_gb_per_rank": {"steps_and_inputs": round((free0 - free1) / 1e9, 2),
+                               "flux_slab": round(slab_bytes / 1e9, 3),
+                               "note": "device memory this block held on the rank after its steps ran (hipMemGetInfo "
+                                       "before and after: the steps' arrays, the library's workspaces, every chunk's "
+                                       "resident inputs); plus the flux slab and, at N > 1, the gathered array"},
            "data": "synthetic columns interpolated from RFMIP profiles (PCG64 streams seeded by (20251015, column "
                    "block)), generated per chunk on host threads (setup_s, outside the timed region)"}
     del rr, slab

@@ -177,7 +177,14 @@ struct Mlp32Args {
   // per input k (host-made, so the device offsets need no branch): byte offset of sample s, layer ilay =
   // s * gsm[k] + ilay * glm[k] (2-D: 4, 0; 1-D: 0, 4; scalar: 0, 0); grec[k] = the array's bytes (0: absent or k >= nx)
   uint32_t gsm[kMaxInputs], glm[kMaxInputs], grec[kMaxInputs];
+  // the same per input as a 2-bit code (0 absent, 1 scalar, 2 1-D, 3 2-D), 16 inputs per word (kMlpPackedIn)
+  uint32_t gcode[(kMaxInputs + 15) / 16];
 };
+
+// In-kernel inputs: per-input multipliers and ranges from the packed codes (a few scalar ops per tile) and the gas
+// pointers re-read per tile, instead of 3 x 18 words and 18 buffer descriptors held across the tile loop (the LW pair
+// spilled 163 SGPRs into VGPR lanes, reloaded by 83 v_readlane per tile).  A/B knob (tools/ablations.py mlp_packin).
+constexpr bool kMlpPackedIn = false;
 
 __device__ __forceinline__ floatx16 mfma32(float a, float b, const floatx16 &c)
 {
@@ -297,12 +304,31 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
         return h ? v1 : v0;
       };
       xv[0] = pair(0, a.tlay, nb4, o2, a.play, nb4, o2);
-      if constexpr (KS > 1) xv[1] = pair(2, a.gas.p[2], a.grec[2], o2, a.gas.p[3], a.grec[3], o2);
+      if constexpr (kMlpPackedIn) {
+        // code c of input k: records (c == 3 ? batch : c == 2 ? layers : c) x 4 bytes; offset s*4 (2-D) or ilay*4
+        auto gp = [&](int k) {
+          const float *p = a.gas.p[k];
+          asm volatile("" : "+s"(p));  // loaded where it is used, not held across the tile loop
+          return p;
+        };
+        auto code = [&](int k) { return (a.gcode[k >> 4] >> (2 * (k & 15))) & 3u; };
+        auto rec = [&](uint32_t c) { return c == 3u ? nb4 : (c == 2u ? 4u * nlay : 4u * c); };
+        auto off = [&](uint32_t c) { return c == 3u ? 4u * s : (c == 2u ? 4u * ilay : 0u); };
+        if constexpr (KS > 1) xv[1] = pair(2, gp(2), rec(code(2)), o2, gp(3), rec(code(3)), o2);
 #pragma unroll
-      for (int t = 2; t < KS; t++) {
-        const int k0 = 2 * t, k1 = 2 * t + 1;
-        xv[t] = pair(k0, a.gas.p[k0], a.grec[k0], s * a.gsm[k0] + ilay * a.glm[k0], a.gas.p[k1], a.grec[k1],
-                     s * a.gsm[k1] + ilay * a.glm[k1]);
+        for (int t = 2; t < KS; t++) {
+          const int k0 = 2 * t, k1 = 2 * t + 1;
+          const uint32_t c0 = code(k0), c1 = code(k1);
+          xv[t] = pair(k0, gp(k0), rec(c0), off(c0), gp(k1), rec(c1), off(c1));
+        }
+      } else {
+        if constexpr (KS > 1) xv[1] = pair(2, a.gas.p[2], a.grec[2], o2, a.gas.p[3], a.grec[3], o2);
+#pragma unroll
+        for (int t = 2; t < KS; t++) {
+          const int k0 = 2 * t, k1 = 2 * t + 1;
+          xv[t] = pair(k0, a.gas.p[k0], a.grec[k0], s * a.gsm[k0] + ilay * a.glm[k0], a.gas.p[k1], a.grec[k1],
+                       s * a.gsm[k1] + ilay * a.glm[k1]);
+        }
       }
       const Buf bh(a.h2o, nb4), bl(a.plev, 4u * (nlay + 1u) * (uint32_t)a.ncol);
       const uint32_t pl = 4u * (icol * (nlay + 1u) + ilay);
@@ -548,6 +574,8 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
       a.gsm[k] = nd == 2 ? 4u : 0u;
       a.glm[k] = nd == 1 ? 4u : 0u;
       a.grec[k] = !on ? 0u : (nd == 2 ? 4u * (uint32_t)nbatch : (nd == 1 ? 4u * (uint32_t)in->nlay : 4u));
+      const uint32_t code = !on ? 0u : (nd == 2 ? 3u : (nd == 1 ? 2u : 1u));
+      a.gcode[k >> 4] |= code << (2 * (k & 15));
     }
   if (mode == MLP_LW_PAIR && shape32(A, 9, 2, 29, 2, 29, 8) && shape32(B, 9, 1, 8, 1, 8, 8)) {
     // the shipped g256 pair: absorption 18-58-58-256, Planck fraction 18-16-16-256
