@@ -181,10 +181,12 @@ struct Mlp32Args {
   uint32_t gcode[(kMaxInputs + 15) / 16];
 };
 
-// In-kernel inputs: per-input multipliers and ranges from the packed codes (a few scalar ops per tile) and the gas
-// pointers re-read per tile, instead of 3 x 18 words and 18 buffer descriptors held across the tile loop (the LW pair
-// spilled 163 SGPRs into VGPR lanes, reloaded by 83 v_readlane per tile).  A/B knob (tools/ablations.py mlp_packin).
-constexpr bool kMlpPackedIn = false;
+// In-kernel inputs of the LW pair: per-input multipliers and ranges from the packed codes (a few scalar ops per tile)
+// and the gas pointers re-read per tile, instead of 3 x 18 words and 18 buffer descriptors held across the tile loop
+// (163 SGPRs spilled into VGPR lanes, reloaded by 83 v_readlane per tile; now 16).  Round 5, alone, alternating,
+// bitwise: C3 LW network 76.0 -> 74.8 us, C4 362.9 -> 357.3 us; serialised in-step 81.8 -> 79.4 us.  The SW pair (no
+// spills) keeps the held form: the packed one made it 3 % slower.  A/B knob: tools/ablations.py mlp_packin.
+constexpr bool kMlpPackedIn = true;
 
 __device__ __forceinline__ floatx16 mfma32(float a, float b, const floatx16 &c)
 {
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
         return h ? v1 : v0;
       };
       xv[0] = pair(0, a.tlay, nb4, o2, a.play, nb4, o2);
-      if constexpr (kMlpPackedIn) {
+      if constexpr (kMlpPackedIn && MODE == MLP_LW_PAIR) {
         // code c of input k: records (c == 3 ? batch : c == 2 ? layers : c) x 4 bytes; offset s*4 (2-D) or ilay*4
         auto gp = [&](int k) {
           const float *p = a.gas.p[k];

@@ -165,13 +165,17 @@ using VSmall = f2;
 // pass-1 chunks per load step of the small-grid instance (its pass 1 is latency-bound at C3: 10 dependent load steps
 // of 6 layers per 60-layer column with the default)
 constexpr int kCkP1Small = 2;
+// passes 2 and 3 of the small-grid instance prefetch this many chunks ahead (three register buffers for 2): at C3
+// each pass streams at 4.8-5.2 TB/s where the same 8-byte loads reach 6.3 TB/s at 3 waves per SIMD with 4 per lane in
+// flight (tools/bw_width.hip), i.e. a chunk's loads are not always back when its body starts
+constexpr int kCkAheadSmall = 1;
 
 // V: f2 (two g-points per lane) or float (one per lane).  kBandPair (fused increment, two g-points per lane): every
 // band starts at an even g-point, so both g-points of a lane lie in one band and its band values are one load each
 // (the RRTMGP g-point sets: 16 per band).  Round 4, C4: SW solver -1.7 % alone, steps -0.8 % (3 alternating pairs)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? kCkWavesNN : kCkWaves, bool kTn = false,
-          class V = f2, bool kEmk = false, bool kBandPair = false, int P1C = kCkP1>
+          class V = f2, bool kEmk = false, bool kBandPair = false, int P1C = kCkP1, int AHEAD = 1>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -301,6 +305,19 @@ __global__ void __launch_bounds__(512, WAVES)
       body(B, idx(min(i + 1, count - 1)), i + 1 < count);
     }
   };
+  // the same walk two chunks ahead through three buffers (same bodies in the same order: same bits)
+  auto walk3 = [&](auto &&load, auto &&body, int count, auto &&idx, auto &A, auto &B, auto &C) {
+    load(A, idx(0));
+    load(B, idx(min(1, count - 1)));
+    for (int i = 0; i < count; i += 3) {
+      load(C, idx(min(i + 2, count - 1)));
+      body(A, idx(i), true);
+      load(A, idx(min(i + 3, count - 1)));
+      body(B, idx(min(i + 1, count - 1)), i + 1 < count);
+      load(B, idx(min(i + 4, count - 1)));
+      body(C, idx(min(i + 2, count - 1)), i + 2 < count);
+    }
+  };
 
   // ---- pass 1: direct beam, checkpoint at every chunk top ----
   // Steps of P1 = kCkP1 * K layers: pass 1 has little arithmetic per layer, so it needs many loads in flight.
@@ -385,7 +402,12 @@ __global__ void __launch_bounds__(512, WAVES)
       CW.stv(alb_b, valid && ck > 0 ? vWs : kBufOOB, sA0 + row * (uint32_t)ck);
       CW.stv(src_b, valid && ck > 0 ? vWs : kBufOOB, sS0 + row * (uint32_t)ck);
     };
-    walk(load2, body2, nck, [&](int i) { return nck - 1 - i; }, A, B);
+    if constexpr (AHEAD == 2) {
+      Chunk C;
+      walk3(load2, body2, nck, [&](int i) { return nck - 1 - i; }, A, B, C);
+    } else {
+      walk(load2, body2, nck, [&](int i) { return nck - 1 - i; }, A, B);
+    }
   }
   // ---- pass 3: top -> bottom fluxes + ordered broadband sums ----
   // idle lanes (past the block's columns) store their ring values to one spare slot instead of branching around the
@@ -480,7 +502,12 @@ __global__ void __launch_bounds__(512, WAVES)
         flush(min(R, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     };
-    walk(load3, body3, nck, [](int i) { return i; }, A, B);
+    if constexpr (AHEAD == 2) {
+      Chunk C;
+      walk3(load3, body3, nck, [](int i) { return i; }, A, B, C);
+    } else {
+      walk(load3, body3, nck, [](int i) { return i; }, A, B);
+    }
   }
 }
 
@@ -555,7 +582,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   // waves per CU)
   if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
     return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
-                                   kCkEmkSmall, false, kCkP1Small>,
+                                   kCkEmkSmall, false, kCkP1Small, kCkAheadSmall>,
               nullptr, nullptr, nullptr, kCkRingSmall, (int)(sizeof(VSmall) / sizeof(float)));
   return go(sw_2stream_ck_kernel<false, false, kCkK, false, kCkRing, kCkWavesNN, kCkTnNN, f2, kCkEmkNN>, nullptr,
             nullptr, nullptr);

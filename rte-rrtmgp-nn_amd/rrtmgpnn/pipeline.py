@@ -383,14 +383,45 @@ class ClearSkyStep:
                 except Exception:
                     pass
 
-    def step(self, timing=None):
+    def retargeted_calls(self, ins, outs):
+        """self.calls with the io_tensors() inputs and outputs replaced by `ins` / `outs` (tensors of the same shapes:
+        another block's resident inputs, slices of a rank's flux slab), intermediates and contexts shared.  Pointer
+        arguments are replaced by value -- an address inside an io tensor (the lw_tail launch's column offset) maps to
+        the same offset in its replacement -- inside the gas-pointer arrays too."""
+        old_ins, old_outs = self.io_tensors()
+        if len(ins) != len(old_ins) or len(outs) != len(old_outs):
+            raise ValueError("retargeted_calls: io tensor count differs")
+        spans = []
+        for a, b in zip(list(old_ins) + list(old_outs), list(ins) + list(outs)):
+            if tuple(a.shape) != tuple(b.shape) or a.dtype != b.dtype or not b.is_contiguous():
+                raise ValueError("retargeted_calls: %s -> %s" % (tuple(a.shape), tuple(b.shape)))
+            spans.append((a.data_ptr(), a.numel() * a.element_size(), b.data_ptr()))
+        ptr_t = type(self._g_lw)
+
+        def mapped(p):
+            for a0, n, b0 in spans:
+                if a0 <= p < a0 + n:
+                    return b0 + (p - a0)
+            return p
+
+        def sub(v):
+            if isinstance(v, int) and not isinstance(v, bool) and v > 4096:
+                return mapped(v)
+            if isinstance(v, ptr_t):
+                return ptr_array([mapped(p) if p else None for p in v])
+            return v
+        return [(n, f, tuple(sub(v) for v in a)) for n, f, a in self.calls]
+
+    def step(self, timing=None, calls=None):
         """Issue one step.  timing: a dict name -> list; each launch is then bracketed by timing events recorded on
-        the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended."""
-        fork_after = "get_col_dry" if any(n == "get_col_dry" for n, _, _ in self.calls) else None
+        the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended.  calls: another
+        block's retargeted_calls() instead of self.calls."""
+        calls = self.calls if calls is None else calls
+        fork_after = "get_col_dry" if any(n == "get_col_dry" for n, _, _ in calls) else None
         if self.overlap and fork_after is None:  # fused step: the chains share no kernel; fork at the start
             self._fork.record(self.ctx.stream)
             self.ctx2.stream.wait_event(self._fork)
-        for name, fn, args in self.calls:
+        for name, fn, args in calls:
             if self.sw_after and name == "sw_solver":
                 self.ctx2.stream.wait_event(self._gate2)
             if name == "lw_solver_tail":
@@ -419,9 +450,10 @@ class ClearSkyStep:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)
 
-    def capture(self):
-        """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`."""
-        self.step()  # warm-up: kernel attributes + workspace allocation happen outside capture
+    def capture(self, calls=None):
+        """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`.  calls:
+        capture another block's retargeted_calls() instead (the graph is returned, self.graph is left alone)."""
+        self.step(calls=calls)  # warm-up: kernel attributes + workspace allocation happen outside capture
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.dev)
@@ -432,11 +464,12 @@ class ClearSkyStep:
         with torch.cuda.stream(s):
             self.ctx.use_stream(s)
             with torch.cuda.graph(g, stream=s):
-                self.step()
+                self.step(calls=calls)
         self.ctx.use_stream(old)
         if self.overlap:
             self.ctx2.use_stream(old2)
-        self.graph = g
+        if calls is None:
+            self.graph = g
         return g
 
     def replay(self):
@@ -477,18 +510,22 @@ class ClearSkyStep:
 
 class ChunkedRank:
     """A rank's column range [lo, hi) streamed through one step in chunks (bench.py --global: a C5 rank holds more
-    columns than one step's block).  Every chunk's inputs stay resident in HBM; `run()` copies each chunk's inputs
-    into the step's input tensors (device to device, on the step's stream), replays the step (its hipGraph when
-    captured) and copies its fluxes into the rank's flux slab `flux` (lw_up, lw_dn, sw_up, sw_dn, sw_dir; (hi - lo,
-    nlay + 1) each).  A short last chunk runs through a second step of its own shape.
+    columns than one step's block).  Every chunk's inputs stay resident in HBM.  Default (direct=True): each chunk runs
+    the step's kernels retargeted to its own inputs and to its rows of the rank's flux slab `flux` (lw_up, lw_dn,
+    sw_up, sw_dn, sw_dir; (hi - lo, nlay + 1) each) -- one captured hipGraph per chunk over the shared intermediates
+    and workspaces, no copies.  direct=False: `run()` copies each chunk's inputs into the step's input tensors (device
+    to device, on the step's stream), replays the step and copies its fluxes into the slab.  A short last chunk runs
+    through a second step of its own shape.
 
     problem(c0, c1) -> (prob, clouds): columns [c0, c1) of the global problem.  make_step(prob, clouds) -> a
     ClearSkyStep of that block's shape."""
 
-    def __init__(self, lo, hi, chunk, problem, make_step, use_graph=True):
+    def __init__(self, lo, hi, chunk, problem, make_step, use_graph=True, direct=True):
         self.lo, self.hi = lo, hi
         self.chunks = [(c, min(c + chunk, hi)) for c in range(lo, hi, chunk)] or [(lo, lo)]
         self.steps, self._run_of, self.chunk_ins, self._step_of = [], [], [], []
+        multi = len(self.chunks) > 1
+        self.direct = direct and multi
         for k, (c0, c1) in enumerate(self.chunks):
             prob, clouds = problem(c0, c1)
             if k == 0:
@@ -498,7 +535,8 @@ class ChunkedRank:
                 st = make_step(prob, clouds)
                 self.steps.append(st)
                 ins, _ = st.io_tensors()
-                self.chunk_ins.append([t.clone() for t in ins] if len(self.chunks) > 1 else None)
+                # copied mode: the first chunk's inputs are kept apart (the step's own are overwritten by the others')
+                self.chunk_ins.append([t.clone() for t in ins] if multi and not self.direct else None)
                 if use_graph:
                     st.capture()
             else:
@@ -511,11 +549,24 @@ class ChunkedRank:
         self.flux = list(outs) if self.single else [
             torch.empty((hi - lo,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev) for o in outs]
         self.use_graph = use_graph
+        if self.direct:
+            # chunk k: its own resident inputs (the first chunk of a step: the step's own tensors) and its rows of the
+            # slab; the graphs of one step share its intermediates, so they replay one after another on its stream
+            self._calls, self._graphs = [], []
+            for k, ((c0, c1), st) in enumerate(zip(self.chunks, self._step_of)):
+                ins = self.chunk_ins[k] if self.chunk_ins[k] is not None else st.io_tensors()[0]
+                calls = st.retargeted_calls(ins, [f[c0 - lo:c1 - lo] for f in self.flux])
+                self._calls.append(calls)
+                self._graphs.append(st.capture(calls) if use_graph else None)
 
     def run(self):
         if self.single:
             st = self.step
             st.replay() if self.use_graph else st.step()
+            return
+        if self.direct:
+            for st, calls, g in zip(self._step_of, self._calls, self._graphs):
+                g.replay() if g is not None else st.step(calls=calls)
             return
         for (c0, c1), st, src in zip(self.chunks, self._step_of, self.chunk_ins):
             ins, outs = st.io_tensors()

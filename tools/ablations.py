@@ -97,8 +97,11 @@ def parametric(name):
     if f[0] == "swck_nnw" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkWavesNN = %s;" % f[1],
                  r"constexpr int kCkWavesNN = \d+;")]
-    if f[0] == "mlp_packin" and len(f) == 1:
-        return [("kernels_nn32.hip", None, "constexpr bool kMlpPackedIn = true;", r"constexpr bool kMlpPackedIn = \w+;")]
+    if f[0] == "mlp_packin" and len(f) == 2:
+        return [("kernels_nn32.hip", None, "constexpr bool kMlpPackedIn = %s;" % ("true" if f[1] == "1" else "false"),
+                 r"constexpr bool kMlpPackedIn = \w+;")]
+    if f[0] == "swck_ahead" and len(f) == 2:
+        return [("kernels_sw_ck.hip", None, "constexpr int kCkAheadSmall = %s;" % f[1], r"constexpr int kCkAheadSmall = \d+;")]
     if f[0] == "swck_p1small" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkP1Small = %s;" % f[1], r"constexpr int kCkP1Small = \d+;")]
     if f[0] == "swck_vsmall" and len(f) == 2:
