@@ -26,6 +26,8 @@ clouds=(lwp, iwp, rel, rei) makes it the all-sky step of examples/all-sky/rrtmgp
 added as a two-stream increment; the SW solver then sees a non-zero asymmetry parameter.
 """
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -35,12 +37,16 @@ from .api import GAUSS_DS, GAUSS_WTS, Context
 
 
 # calls of the SW chain (issued on the second stream when overlapping)
-SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver"}
+SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver",
+            "predict_nn_sw_b", "sw_solver_b"}
+# the second column part of a split SW chain (ClearSkyStep sw_split), issued on a third stream
+SW_CHAIN_B = {"predict_nn_sw_b", "sw_solver_b"}
 
 
 # issue order of the fused step (stable sort; names not listed keep their place at the end)
 FUSED_ORDER = ["get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", "predict_nn_lw", "lw_solver",
-               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver", "lw_solver_tail"]
+               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver", "predict_nn_sw_b",
+               "sw_solver_b", "lw_solver_tail"]
 
 
 def issue_order(calls, fused, lw_after=""):
@@ -69,7 +75,8 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0, lw_tail=0.0):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0, lw_tail=0.0,
+                 sw_split=0.0):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
@@ -278,6 +285,38 @@ class ClearSkyStep:
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
         self.sw_priority = sw_priority
+        # sw_split: the SW chain of the first fraction of the columns and of the rest as two chains on two streams,
+        # the second part's network after the first's (clear sky, fused, overlapped): the first part's solver starts
+        # while the second part's network runs (same kernels on column ranges: same bits)
+        self.sw_split_cols = 0
+        if sw_split and fused and overlap and not self.allsky:
+            n1 = min(max(int(round(float(sw_split) * ncol)), 1), ncol - 1)
+            self.sw_split_cols = n1
+            n2, G, b = ncol - n1, self.ng_sw, 4
+            out = []
+            for nm, fn, a in self.calls:
+                if nm == "predict_nn_sw":
+                    a = list(a)
+                    h, t = list(a), list(a)
+                    h[1], t[1] = n1, n2
+                    for k, v in ((5, n1 * nlay * b), (6, n1 * nlay * b), (7, n1 * (nlay + 1) * b), (8, n1 * nlay * b),
+                                 (12, n1 * nlay * G * b), (13, n1 * nlay * G * b)):
+                        t[k] = t[k] + v
+                    # every gas is 2-D here (gas_args): its column block moves with the columns
+                    t[9] = ptr_array([(q + n1 * nlay * b) if q else None for q in a[9]])
+                    out += [(nm, fn, tuple(h)), ("predict_nn_sw_b", fn, tuple(t))]
+                elif nm == "sw_solver":
+                    a = list(a)
+                    h, t = list(a), list(a)
+                    h[3], t[3] = n1, n2
+                    for k, v in ((5, n1 * G * b), (7, n1 * nlay * G * b), (8, n1 * nlay * G * b), (10, n1 * b),
+                                 (11, n1 * G * b), (12, n1 * G * b), (13, n1 * (nlay + 1) * b),
+                                 (14, n1 * (nlay + 1) * b), (15, n1 * (nlay + 1) * b)):
+                        t[k] = t[k] + v
+                    out += [(nm, fn, tuple(h)), ("sw_solver_b", fn, tuple(t))]
+                else:
+                    out.append((nm, fn, a))
+            self.calls = out
         self._finish(overlap, lw_after, sw_after, lw_net_cus, sw_net_cus)
         if self.lw_tail_cols:
             self._tail_gate = torch.cuda.Event()
@@ -303,7 +342,7 @@ class ClearSkyStep:
         names = [n for n, _, _ in self.calls]
         gate = ""
         if overlap and self.fused and "predict_nn_sw" in names and "predict_nn_lw" in names:
-            gate = "predict_nn_sw"
+            gate = "predict_nn_sw_b" if "predict_nn_sw_b" in names else "predict_nn_sw"
         if sw_after is None:
             sw_after = ""
         self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
@@ -352,7 +391,12 @@ class ClearSkyStep:
             self.sw_net_cus = int(sw_net_cus or 0)
             if self.sw_net_cus:
                 check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx2.h, self.sw_net_cus), "context_set_mlp_max_cus")
-            self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
+            self.ctx3 = None
+            if getattr(self, "sw_split_cols", 0):
+                self.ctx3 = Context(self.dev.index, self._sw_stream())
+                self._split_gate, self._join3 = torch.cuda.Event(), torch.cuda.Event()
+            self.calls = [(n, f, ((self.ctx3.h if n in SW_CHAIN_B else self.ctx2.h,) + tuple(a[1:]))
+                           if n in SW_CHAIN else a) for n, f, a in self.calls]
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
 
@@ -365,6 +409,8 @@ class ClearSkyStep:
 
     def stream_for(self, name):
         """The torch stream a call of `self.calls` is issued on."""
+        if self.overlap and name in SW_CHAIN_B and getattr(self, "ctx3", None) is not None:
+            return self.ctx3.stream
         return self.ctx2.stream if (self.overlap and name in SW_CHAIN) else self.ctx.stream
 
     def _cloud_optics(self, which, lut, icergh):
@@ -396,7 +442,6 @@ class ClearSkyStep:
             if tuple(a.shape) != tuple(b.shape) or a.dtype != b.dtype or not b.is_contiguous():
                 raise ValueError("retargeted_calls: %s -> %s" % (tuple(a.shape), tuple(b.shape)))
             spans.append((a.data_ptr(), a.numel() * a.element_size(), b.data_ptr()))
-        ptr_t = type(self._g_lw)
 
         def mapped(p):
             for a0, n, b0 in spans:
@@ -407,7 +452,7 @@ class ClearSkyStep:
         def sub(v):
             if isinstance(v, int) and not isinstance(v, bool) and v > 4096:
                 return mapped(v)
-            if isinstance(v, ptr_t):
+            if isinstance(v, ctypes.Array) and v._type_ is ctypes.c_void_p:  # gas pointers (any length)
                 return ptr_array([mapped(p) if p else None for p in v])
             return v
         return [(n, f, tuple(sub(v) for v in a)) for n, f, a in self.calls]
@@ -426,6 +471,8 @@ class ClearSkyStep:
                 self.ctx2.stream.wait_event(self._gate2)
             if name == "lw_solver_tail":
                 self.ctx.stream.wait_event(self._tail_gate)
+            if name == "predict_nn_sw_b":
+                self.ctx3.stream.wait_event(self._split_gate)
             if timing is not None:
                 s = self.stream_for(name)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -440,8 +487,10 @@ class ClearSkyStep:
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
             if self.overlap and name == self.lw_after:
-                self._gate.record(self.ctx2.stream)
+                self._gate.record(self.stream_for(name))
                 self.ctx.stream.wait_event(self._gate)
+            if name == "predict_nn_sw" and getattr(self, "ctx3", None) is not None:
+                self._split_gate.record(self.ctx2.stream)
             if self.sw_after and name == self.sw_after:
                 self._gate2.record(self.ctx.stream)
             if name == "sw_solver" and getattr(self, "lw_tail_cols", 0):
@@ -449,6 +498,9 @@ class ClearSkyStep:
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)
+            if getattr(self, "ctx3", None) is not None:
+                self._join3.record(self.ctx3.stream)
+                self.ctx.stream.wait_event(self._join3)
 
     def capture(self, calls=None):
         """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`.  calls:
@@ -461,6 +513,9 @@ class ClearSkyStep:
         if self.overlap:
             old2 = self.ctx2.stream
             self.ctx2.use_stream(self._sw_stream())
+            if getattr(self, "ctx3", None) is not None:
+                old3 = self.ctx3.stream
+                self.ctx3.use_stream(self._sw_stream())
         with torch.cuda.stream(s):
             self.ctx.use_stream(s)
             with torch.cuda.graph(g, stream=s):
@@ -468,6 +523,8 @@ class ClearSkyStep:
         self.ctx.use_stream(old)
         if self.overlap:
             self.ctx2.use_stream(old2)
+            if getattr(self, "ctx3", None) is not None:
+                self.ctx3.use_stream(old3)
         if calls is None:
             self.graph = g
         return g

@@ -100,6 +100,14 @@ def parametric(name):
     if f[0] == "mlp_packin" and len(f) == 2:
         return [("kernels_nn32.hip", None, "constexpr bool kMlpPackedIn = %s;" % ("true" if f[1] == "1" else "false"),
                  r"constexpr bool kMlpPackedIn = \w+;")]
+    if f[0] == "mlp_stagger" and len(f) == 3:  # waves >= 4 of a block start N x 64 cycles late, at priority P
+        code = "  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwaves = blockDim.x >> 6;\n"
+        extra = ""
+        if int(f[1]) > 0:
+            extra += "  if (wave >= 4) { for (int i_ = 0; i_ < %d; i_++) __builtin_amdgcn_s_sleep(32); }\n" % (int(f[1]) // 32)
+        if int(f[2]) > 0:
+            extra += "  if (wave >= 4) __builtin_amdgcn_s_setprio(%d);\n" % int(f[2])
+        return [("kernels_nn32.hip", code, extra, "after")]
     if f[0] == "swck_ahead" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkAheadSmall = %s;" % f[1], r"constexpr int kCkAheadSmall = \d+;")]
     if f[0] == "swck_p1small" and len(f) == 2:
