@@ -65,12 +65,6 @@ def parse():
     ap.add_argument("--lw-net-cus", type=int, default=None,
                     help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
                          "choice: 5/8 of the CUs at small grids, where the LW chain follows the SW network)")
-    ap.add_argument("--lw-tail", type=float, default=0.0,
-                    help="fraction of the columns whose LW solver runs as a second launch after the SW solver "
-                         "(pipeline.ClearSkyStep lw_tail; 0: one LW solver launch)")
-    ap.add_argument("--sw-split", type=float, default=0.0,
-                    help="run the SW chain of this fraction of the columns and of the rest as two chains on two streams, "
-                         "the second part's network after the first's (pipeline.ClearSkyStep sw_split; 0: one chain)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],
@@ -275,8 +269,7 @@ def main():
                                                      overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
                                                      lw_after=lw_after, sw_after=sw_after,
                                                      sw_priority=args.sw_priority, lw_net_cus=args.lw_net_cus,
-                                                     sw_net_cus=args.sw_net_cus, lw_tail=args.lw_tail,
-                                                     sw_split=args.sw_split),
+                                                     sw_net_cus=args.sw_net_cus),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first
@@ -384,13 +377,7 @@ def main():
             _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx.h, step.lw_net_cus), "context_set_mlp_max_cus")
         if serial and getattr(step, "sw_net_cus", 0):
             _lib.check(step.L.rrtmgpnn_context_set_mlp_max_cus(step.ctx2.h, step.sw_net_cus), "context_set_mlp_max_cus")
-        res = {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
-        if "lw_solver_tail" in res:  # the LW solver's two launches (lw_tail) are one stage
-            res["lw_solver"] += res.pop("lw_solver_tail")
-        for part in ("predict_nn_sw", "sw_solver"):  # the two column parts of a split SW chain (sw_split)
-            if part + "_b" in res:
-                res[part] += res.pop(part + "_b")
-        return res
+        return {name: sum(a.elapsed_time(b) for a, b in pairs) / len(pairs) for name, pairs in timing.items()}
 
     stages = time_stages(True)
     stages_ov = time_stages(False) if step.overlap else None
@@ -522,12 +509,7 @@ def main():
                                  (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
                                  (" (LW network on %d CUs)" % step.lw_net_cus if step.lw_net_cus else "") +
                                  (", the SW solver after %s" % step.sw_after if step.sw_after else "") +
-                                 (", SW stream priority %d" % step.sw_priority if step.sw_priority else "") +
-                                 (", the LW solver of the last %d columns after the SW solver" % step.lw_tail_cols
-                                  if getattr(step, "lw_tail_cols", 0) else "") +
-                                 (", the SW chain in two column parts (%d + %d) on two streams"
-                                  % (step.sw_split_cols, step.ncol - step.sw_split_cols)
-                                  if getattr(step, "sw_split_cols", 0) else ""),
+                                 (", SW stream priority %d" % step.sw_priority if step.sw_priority else ""),
                        "kernels": ("class-layer sequence" if not step.fused else
                                    "fused Planck-in-LW-solver, g=0 elided" +
                                    (", cloud increments fused into both solvers" if step.allsky else ""))},

@@ -26,8 +26,6 @@ clouds=(lwp, iwp, rel, rei) makes it the all-sky step of examples/all-sky/rrtmgp
 added as a two-stream increment; the SW solver then sees a non-zero asymmetry parameter.
 """
 
-import ctypes
-
 import numpy as np
 import torch
 
@@ -37,16 +35,12 @@ from .api import GAUSS_DS, GAUSS_WTS, Context
 
 
 # calls of the SW chain (issued on the second stream when overlapping)
-SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver",
-            "predict_nn_sw_b", "sw_solver_b"}
-# the second column part of a split SW chain (ClearSkyStep sw_split), issued on a third stream
-SW_CHAIN_B = {"predict_nn_sw_b", "sw_solver_b"}
+SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver"}
 
 
 # issue order of the fused step (stable sort; names not listed keep their place at the end)
 FUSED_ORDER = ["get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", "predict_nn_lw", "lw_solver",
-               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver", "predict_nn_sw_b",
-               "sw_solver_b", "lw_solver_tail"]
+               "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver"]
 
 
 def issue_order(calls, fused, lw_after=""):
@@ -75,8 +69,7 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0, lw_tail=0.0,
-                 sw_split=0.0):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
@@ -214,26 +207,6 @@ class ClearSkyStep:
                      (c, ncol, nlay, self.ng_lw, self.nb_lw, self._lims_lw, p(self.tau_lw), None, None,
                       p(self.cld_tau_lw), None, None)),
                 ]
-        # lw_tail: the last fraction of the columns' LW solver runs as a second launch ("lw_solver_tail") that waits for
-        # the SW solver (overlapped fused steps): the SW solver, the critical path, shares the chip with less LW work,
-        # and the tail runs on the chip it leaves (same kernel on a column range: same bits)
-        ntail = int(round(float(lw_tail) * ncol)) if (fused and sw and overlap) else 0
-        self.lw_tail_cols = ntail = min(max(ntail, 0), ncol - 1)
-        if ntail:
-            n1 = ncol - ntail
-            (nm, fn, a), = lw_calls
-            a = list(a)
-            head, tail = list(a), list(a)
-            head[3], tail[3] = n1, ntail
-            G, b = self.ng_lw, 4  # float bytes
-            off = {9: n1 * nlay * G * b, 10: n1 * nlay * G * b, 13: n1 * nlay * b, 14: n1 * (nlay + 1) * b,
-                   15: n1 * b, 22: n1 * self.nb_lw * b, 23: n1 * (nlay + 1) * b, 24: n1 * (nlay + 1) * b}
-            if self.allsky:  # the cloud optical depth by band sits after tau: every later index moves by one
-                off = {(k if k < 10 else k + 1): v for k, v in off.items()}
-                off[10] = n1 * nlay * self.nb_lw * b
-            for k, v in off.items():
-                tail[k] = tail[k] + v
-            lw_calls = [(nm, fn, tuple(head)), ("lw_solver_tail", fn, tuple(tail))]
         self.calls += lw_calls
         if not sw:
             self.calls = [c for c in self.calls if c[0] != "cloud_optics_sw"]
@@ -285,41 +258,7 @@ class ClearSkyStep:
                   g_sw, p(self.mu0), p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
         self.sw_priority = sw_priority
-        # sw_split: the SW chain of the first fraction of the columns and of the rest as two chains on two streams,
-        # the second part's network after the first's (clear sky, fused, overlapped): the first part's solver starts
-        # while the second part's network runs (same kernels on column ranges: same bits)
-        self.sw_split_cols = 0
-        if sw_split and fused and overlap and not self.allsky:
-            n1 = min(max(int(round(float(sw_split) * ncol)), 1), ncol - 1)
-            self.sw_split_cols = n1
-            n2, G, b = ncol - n1, self.ng_sw, 4
-            out = []
-            for nm, fn, a in self.calls:
-                if nm == "predict_nn_sw":
-                    a = list(a)
-                    h, t = list(a), list(a)
-                    h[1], t[1] = n1, n2
-                    for k, v in ((5, n1 * nlay * b), (6, n1 * nlay * b), (7, n1 * (nlay + 1) * b), (8, n1 * nlay * b),
-                                 (12, n1 * nlay * G * b), (13, n1 * nlay * G * b)):
-                        t[k] = t[k] + v
-                    # every gas is 2-D here (gas_args): its column block moves with the columns
-                    t[9] = ptr_array([(q + n1 * nlay * b) if q else None for q in a[9]])
-                    out += [(nm, fn, tuple(h)), ("predict_nn_sw_b", fn, tuple(t))]
-                elif nm == "sw_solver":
-                    a = list(a)
-                    h, t = list(a), list(a)
-                    h[3], t[3] = n1, n2
-                    for k, v in ((5, n1 * G * b), (7, n1 * nlay * G * b), (8, n1 * nlay * G * b), (10, n1 * b),
-                                 (11, n1 * G * b), (12, n1 * G * b), (13, n1 * (nlay + 1) * b),
-                                 (14, n1 * (nlay + 1) * b), (15, n1 * (nlay + 1) * b)):
-                        t[k] = t[k] + v
-                    out += [(nm, fn, tuple(h)), ("sw_solver_b", fn, tuple(t))]
-                else:
-                    out.append((nm, fn, a))
-            self.calls = out
         self._finish(overlap, lw_after, sw_after, lw_net_cus, sw_net_cus)
-        if self.lw_tail_cols:
-            self._tail_gate = torch.cuda.Event()
 
     def _finish(self, overlap, lw_after=None, sw_after=None, lw_net_cus=None, sw_net_cus=0):
         # fused: the small kernels that do not depend on a network's output go first in their chain, ahead of the big
@@ -342,7 +281,7 @@ class ClearSkyStep:
         names = [n for n, _, _ in self.calls]
         gate = ""
         if overlap and self.fused and "predict_nn_sw" in names and "predict_nn_lw" in names:
-            gate = "predict_nn_sw_b" if "predict_nn_sw_b" in names else "predict_nn_sw"
+            gate = "predict_nn_sw"
         if sw_after is None:
             sw_after = ""
         self.lw_after = (gate if lw_after is None else lw_after) if overlap else ""
@@ -391,12 +330,7 @@ class ClearSkyStep:
             self.sw_net_cus = int(sw_net_cus or 0)
             if self.sw_net_cus:
                 check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx2.h, self.sw_net_cus), "context_set_mlp_max_cus")
-            self.ctx3 = None
-            if getattr(self, "sw_split_cols", 0):
-                self.ctx3 = Context(self.dev.index, self._sw_stream())
-                self._split_gate, self._join3 = torch.cuda.Event(), torch.cuda.Event()
-            self.calls = [(n, f, ((self.ctx3.h if n in SW_CHAIN_B else self.ctx2.h,) + tuple(a[1:]))
-                           if n in SW_CHAIN else a) for n, f, a in self.calls]
+            self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
             self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
 
@@ -409,8 +343,6 @@ class ClearSkyStep:
 
     def stream_for(self, name):
         """The torch stream a call of `self.calls` is issued on."""
-        if self.overlap and name in SW_CHAIN_B and getattr(self, "ctx3", None) is not None:
-            return self.ctx3.stream
         return self.ctx2.stream if (self.overlap and name in SW_CHAIN) else self.ctx.stream
 
     def _cloud_optics(self, which, lut, icergh):
@@ -429,50 +361,16 @@ class ClearSkyStep:
                 except Exception:
                     pass
 
-    def retargeted_calls(self, ins, outs):
-        """self.calls with the io_tensors() inputs and outputs replaced by `ins` / `outs` (tensors of the same shapes:
-        another block's resident inputs, slices of a rank's flux slab), intermediates and contexts shared.  Pointer
-        arguments are replaced by value -- an address inside an io tensor (the lw_tail launch's column offset) maps to
-        the same offset in its replacement -- inside the gas-pointer arrays too."""
-        old_ins, old_outs = self.io_tensors()
-        if len(ins) != len(old_ins) or len(outs) != len(old_outs):
-            raise ValueError("retargeted_calls: io tensor count differs")
-        spans = []
-        for a, b in zip(list(old_ins) + list(old_outs), list(ins) + list(outs)):
-            if tuple(a.shape) != tuple(b.shape) or a.dtype != b.dtype or not b.is_contiguous():
-                raise ValueError("retargeted_calls: %s -> %s" % (tuple(a.shape), tuple(b.shape)))
-            spans.append((a.data_ptr(), a.numel() * a.element_size(), b.data_ptr()))
-
-        def mapped(p):
-            for a0, n, b0 in spans:
-                if a0 <= p < a0 + n:
-                    return b0 + (p - a0)
-            return p
-
-        def sub(v):
-            if isinstance(v, int) and not isinstance(v, bool) and v > 4096:
-                return mapped(v)
-            if isinstance(v, ctypes.Array) and v._type_ is ctypes.c_void_p:  # gas pointers (any length)
-                return ptr_array([mapped(p) if p else None for p in v])
-            return v
-        return [(n, f, tuple(sub(v) for v in a)) for n, f, a in self.calls]
-
-    def step(self, timing=None, calls=None):
+    def step(self, timing=None):
         """Issue one step.  timing: a dict name -> list; each launch is then bracketed by timing events recorded on
-        the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended.  calls: another
-        block's retargeted_calls() instead of self.calls."""
-        calls = self.calls if calls is None else calls
-        fork_after = "get_col_dry" if any(n == "get_col_dry" for n, _, _ in calls) else None
+        the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended."""
+        fork_after = "get_col_dry" if any(n == "get_col_dry" for n, _, _ in self.calls) else None
         if self.overlap and fork_after is None:  # fused step: the chains share no kernel; fork at the start
             self._fork.record(self.ctx.stream)
             self.ctx2.stream.wait_event(self._fork)
-        for name, fn, args in calls:
+        for name, fn, args in self.calls:
             if self.sw_after and name == "sw_solver":
                 self.ctx2.stream.wait_event(self._gate2)
-            if name == "lw_solver_tail":
-                self.ctx.stream.wait_event(self._tail_gate)
-            if name == "predict_nn_sw_b":
-                self.ctx3.stream.wait_event(self._split_gate)
             if timing is not None:
                 s = self.stream_for(name)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -487,25 +385,17 @@ class ClearSkyStep:
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
             if self.overlap and name == self.lw_after:
-                self._gate.record(self.stream_for(name))
+                self._gate.record(self.ctx2.stream)
                 self.ctx.stream.wait_event(self._gate)
-            if name == "predict_nn_sw" and getattr(self, "ctx3", None) is not None:
-                self._split_gate.record(self.ctx2.stream)
             if self.sw_after and name == self.sw_after:
                 self._gate2.record(self.ctx.stream)
-            if name == "sw_solver" and getattr(self, "lw_tail_cols", 0):
-                self._tail_gate.record(self.ctx2.stream)
         if self.overlap:
             self._join.record(self.ctx2.stream)
             self.ctx.stream.wait_event(self._join)
-            if getattr(self, "ctx3", None) is not None:
-                self._join3.record(self.ctx3.stream)
-                self.ctx.stream.wait_event(self._join3)
 
-    def capture(self, calls=None):
-        """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`.  calls:
-        capture another block's retargeted_calls() instead (the graph is returned, self.graph is left alone)."""
-        self.step(calls=calls)  # warm-up: kernel attributes + workspace allocation happen outside capture
+    def capture(self):
+        """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`."""
+        self.step()  # warm-up: kernel attributes + workspace allocation happen outside capture
         torch.cuda.synchronize(self.dev)
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.dev)
@@ -513,20 +403,14 @@ class ClearSkyStep:
         if self.overlap:
             old2 = self.ctx2.stream
             self.ctx2.use_stream(self._sw_stream())
-            if getattr(self, "ctx3", None) is not None:
-                old3 = self.ctx3.stream
-                self.ctx3.use_stream(self._sw_stream())
         with torch.cuda.stream(s):
             self.ctx.use_stream(s)
             with torch.cuda.graph(g, stream=s):
-                self.step(calls=calls)
+                self.step()
         self.ctx.use_stream(old)
         if self.overlap:
             self.ctx2.use_stream(old2)
-            if getattr(self, "ctx3", None) is not None:
-                self.ctx3.use_stream(old3)
-        if calls is None:
-            self.graph = g
+        self.graph = g
         return g
 
     def replay(self):
@@ -567,22 +451,18 @@ class ClearSkyStep:
 
 class ChunkedRank:
     """A rank's column range [lo, hi) streamed through one step in chunks (bench.py --global: a C5 rank holds more
-    columns than one step's block).  Every chunk's inputs stay resident in HBM.  Default (direct=True): each chunk runs
-    the step's kernels retargeted to its own inputs and to its rows of the rank's flux slab `flux` (lw_up, lw_dn,
-    sw_up, sw_dn, sw_dir; (hi - lo, nlay + 1) each) -- one captured hipGraph per chunk over the shared intermediates
-    and workspaces, no copies.  direct=False: `run()` copies each chunk's inputs into the step's input tensors (device
-    to device, on the step's stream), replays the step and copies its fluxes into the slab.  A short last chunk runs
-    through a second step of its own shape.
+    columns than one step's block).  Every chunk's inputs stay resident in HBM; `run()` copies each chunk's inputs
+    into the step's input tensors (device to device, on the step's stream), replays the step (its hipGraph when
+    captured) and copies its fluxes into the rank's flux slab `flux` (lw_up, lw_dn, sw_up, sw_dn, sw_dir; (hi - lo,
+    nlay + 1) each).  A short last chunk runs through a second step of its own shape.
 
     problem(c0, c1) -> (prob, clouds): columns [c0, c1) of the global problem.  make_step(prob, clouds) -> a
     ClearSkyStep of that block's shape."""
 
-    def __init__(self, lo, hi, chunk, problem, make_step, use_graph=True, direct=True):
+    def __init__(self, lo, hi, chunk, problem, make_step, use_graph=True):
         self.lo, self.hi = lo, hi
         self.chunks = [(c, min(c + chunk, hi)) for c in range(lo, hi, chunk)] or [(lo, lo)]
         self.steps, self._run_of, self.chunk_ins, self._step_of = [], [], [], []
-        multi = len(self.chunks) > 1
-        self.direct = direct and multi
         for k, (c0, c1) in enumerate(self.chunks):
             prob, clouds = problem(c0, c1)
             if k == 0:
@@ -592,8 +472,7 @@ class ChunkedRank:
                 st = make_step(prob, clouds)
                 self.steps.append(st)
                 ins, _ = st.io_tensors()
-                # copied mode: the first chunk's inputs are kept apart (the step's own are overwritten by the others')
-                self.chunk_ins.append([t.clone() for t in ins] if multi and not self.direct else None)
+                self.chunk_ins.append([t.clone() for t in ins] if len(self.chunks) > 1 else None)
                 if use_graph:
                     st.capture()
             else:
@@ -606,24 +485,11 @@ class ChunkedRank:
         self.flux = list(outs) if self.single else [
             torch.empty((hi - lo,) + tuple(o.shape[1:]), dtype=o.dtype, device=dev) for o in outs]
         self.use_graph = use_graph
-        if self.direct:
-            # chunk k: its own resident inputs (the first chunk of a step: the step's own tensors) and its rows of the
-            # slab; the graphs of one step share its intermediates, so they replay one after another on its stream
-            self._calls, self._graphs = [], []
-            for k, ((c0, c1), st) in enumerate(zip(self.chunks, self._step_of)):
-                ins = self.chunk_ins[k] if self.chunk_ins[k] is not None else st.io_tensors()[0]
-                calls = st.retargeted_calls(ins, [f[c0 - lo:c1 - lo] for f in self.flux])
-                self._calls.append(calls)
-                self._graphs.append(st.capture(calls) if use_graph else None)
 
     def run(self):
         if self.single:
             st = self.step
             st.replay() if self.use_graph else st.step()
-            return
-        if self.direct:
-            for st, calls, g in zip(self._step_of, self._calls, self._graphs):
-                g.replay() if g is not None else st.step(calls=calls)
             return
         for (c0, c1), st, src in zip(self.chunks, self._step_of, self.chunk_ins):
             ins, outs = st.io_tensors()

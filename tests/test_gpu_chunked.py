@@ -1,8 +1,7 @@
 """GPU: the chunked rank path bench.py --global takes when a rank holds more columns than one step's block
 (C5 at N < 8: 8, 4 or 2 chunks per rank).  pipeline.ChunkedRank copies each chunk's HBM-resident inputs into the
 captured step's buffers, replays the graph and copies the fluxes into the rank's slab; a short last chunk runs through
-a step of its own shape.  Direct (the default): each chunk's captured graph runs the step's kernels on the chunk's own
-inputs and writes the slab's rows (retargeted pointers, no copies).  The slab must equal, bit for bit, one independent ClearSkyStep per chunk -- the last chunk
+a step of its own shape.  The slab must equal, bit for bit, one independent ClearSkyStep per chunk -- the last chunk
 included -- and stay so over repeated runs (stale buffers or a missed copy would show as a chunk holding another
 chunk's fluxes)."""
 import numpy as np
@@ -31,19 +30,16 @@ def _problem(config):
     return problem
 
 
-@pytest.mark.parametrize("direct", [True, False], ids=["direct", "copied"])
 @pytest.mark.parametrize("config,lo,hi,chunk,graph", [
     ("rfmip", 10, 10 + 3 * 64, 64, True),          # 3 full chunks
     ("rfmip", 1700, 1700 + 3 * 48 + 17, 48, True),  # 3 full + a short last chunk (wraps the 1800 RFMIP columns)
     ("synthetic", 1000, 1000 + 4 * 40, 40, False),  # eager launches, synthetic clear sky
     ("allsky", 0, 3 * 32 + 5, 32, True),            # all-sky step (clouds), ragged last chunk
 ])
-def test_chunked_rank_equals_independent_steps(dev, config, lo, hi, chunk, graph, direct):
+def test_chunked_rank_equals_independent_steps(dev, config, lo, hi, chunk, graph):
     from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
     problem = _problem(config)
-    rank = ChunkedRank(lo, hi, chunk, problem, lambda p, c: ClearSkyStep(p, device=0, clouds=c), use_graph=graph,
-                       direct=direct)
-    assert rank.direct == direct
+    rank = ChunkedRank(lo, hi, chunk, problem, lambda p, c: ClearSkyStep(p, device=0, clouds=c), use_graph=graph)
     assert len(rank.chunks) >= 3
     keys = ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir")
     want = []

@@ -391,60 +391,3 @@ def test_set_stream_inside_a_global_capture(dev, rfmip):
     for k in ref:
         np.testing.assert_array_equal(ref[k], got[k], err_msg=k)
 
-
-@pytest.mark.parametrize("allsky", [False, True])
-@pytest.mark.parametrize("frac", [0.3, 0.5])
-def test_lw_tail_is_bitwise_identical(dev, rfmip, allsky, frac):
-    """ClearSkyStep(lw_tail=f): the LW solver of the last f of the columns as a second launch that waits for the SW
-    solver gives the one-stream step's fluxes bit for bit, eager and replayed as a hipGraph."""
-    from rrtmgpnn import data
-    from rrtmgpnn.pipeline import ClearSkyStep
-    prob = subset(rfmip, np.arange(3, 1800, 4))
-    clouds = data.allsky_clouds(prob, data.load_cloud_optics("lw")) if allsky else None
-    one = ClearSkyStep(prob, device=0, clouds=clouds, overlap=False)
-    two = ClearSkyStep(prob, device=0, clouds=clouds, lw_tail=frac)
-    assert two.lw_tail_cols == int(round(frac * prob["ncol"]))
-    names = [n for n, _, _ in two.calls]
-    assert names.index("lw_solver_tail") > names.index("sw_solver")
-    one.step()
-    two.step()
-    torch.cuda.synchronize()
-    a, b = one.fluxes(), two.fluxes()
-    two.capture()
-    for t in (two.lw_up, two.lw_dn, two.sw_up, two.sw_dn, two.sw_dir):
-        t.fill_(float("nan"))
-    two.replay()
-    two.replay()
-    torch.cuda.synchronize()
-    c = two.fluxes()
-    for k in a:
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-        np.testing.assert_array_equal(a[k], c[k], err_msg=k)
-
-
-@pytest.mark.parametrize("frac", [0.5, 0.35])
-def test_sw_split_is_bitwise_identical(dev, rfmip, frac):
-    """ClearSkyStep(sw_split=f): the SW chain of the first f of the columns and of the rest on two streams (the second
-    part's network after the first's, the LW chain after both networks) gives the one-stream step's fluxes bit for bit,
-    eager and replayed as a hipGraph."""
-    from rrtmgpnn.pipeline import ClearSkyStep
-    prob = subset(rfmip, np.arange(2, 1800, 3))
-    one = ClearSkyStep(prob, device=0, overlap=False)
-    two = ClearSkyStep(prob, device=0, sw_split=frac)
-    assert two.sw_split_cols == int(round(frac * prob["ncol"]))
-    names = [n for n, _, _ in two.calls]
-    assert names.index("predict_nn_sw_b") > names.index("predict_nn_sw") and two.lw_after == "predict_nn_sw_b"
-    one.step()
-    two.step()
-    torch.cuda.synchronize()
-    a, b = one.fluxes(), two.fluxes()
-    two.capture()
-    for t in (two.lw_up, two.lw_dn, two.sw_up, two.sw_dn, two.sw_dir):
-        t.fill_(float("nan"))
-    two.replay()
-    two.replay()
-    torch.cuda.synchronize()
-    c = two.fluxes()
-    for k in a:
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-        np.testing.assert_array_equal(a[k], c[k], err_msg=k)

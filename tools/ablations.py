@@ -63,6 +63,23 @@ ABLATIONS.update({
           float ta""", "replace")],
 })
 
+ABLATIONS.update({
+    # SW pair: the epilogue's arithmetic replaced by the raw network outputs (stores kept): its VALU share
+    "mlp32_sw_noepi": [("kernels_nn32.hip", """          float ta = sdA * (yA[r] + bA);
+          ta = ta + mnA;
+          const float vabs = pow8(ta) * cdr[r];
+          float tr = sdB * (yB[r] + bB);
+          tr = tr + mnB;
+          const float vray = pow8(tr) * cdr[r];
+          const float tot = vabs + vray, ssa = vray / tot;""", """          const float tot = yA[r], ssa = yB[r];  // ablation mlp32_sw_noepi""", "replace")],
+    # every network's output-layer MFMA chains skipped (zero accumulators): their share
+    "mlp32_noout": [("kernels_nn32.hip", """      const floatx16 yA = mfma_chain_t<AN3>(iA + LA.l3, go, hA, lane);
+      floatx16 yB = {};
+      if constexpr (kPair) yB = mfma_chain_t<BN3>(iB + LB.l3, go, hB, lane);""", """      floatx16 yA = {}, yB = {};  // ablation mlp32_noout
+      yA[0] = hA[0];
+      if constexpr (kPair) yB[0] = hB[0];""", "replace")],
+})
+
 # Variants that keep the bits (tools/kernel_ab.py checks them bitwise against the default library): A/B candidates
 ABLATIONS.update({
     # SW checkpointed solver: scheduling fences between a pass's chunk bodies and their prefetches (rounds 2-3)
