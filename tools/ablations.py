@@ -80,6 +80,19 @@ ABLATIONS.update({
       if constexpr (kPair) yB[0] = hB[0];""", "replace")],
 })
 
+_LW_UP = """          const float T = solver_exp_neg(-t, etab);
+          const float fact = (t > tau_thresh) ? solver_div(1.0f - T, t) - T : t * (0.5f - 1.0f / 3.0f * t);
+          const float S = (1.0f - T) * lvup"""
+ABLATIONS.update({
+    # LW no-scattering solver: the up pass without its exp (T from a cheap stand-in), or without exp and division --
+    # the share a down-pass cache of the transmittance (and of fact) could save
+    "lw_up_noexp": [("kernels_rte.hip", _LW_UP, _LW_UP.replace("solver_exp_neg(-t, etab)", "1.0f - 0.5f * t")
+                     + "  /* ablation lw_up_noexp */", "replace")],
+    "lw_up_noexpdiv": [("kernels_rte.hip", _LW_UP, _LW_UP.replace("solver_exp_neg(-t, etab)", "1.0f - 0.5f * t")
+                        .replace("solver_div(1.0f - T, t)", "(1.0f - T) * t") + "  /* ablation lw_up_noexpdiv */",
+                        "replace")],
+})
+
 # Variants that keep the bits (tools/kernel_ab.py checks them bitwise against the default library): A/B candidates
 ABLATIONS.update({
     # SW checkpointed solver: scheduling fences between a pass's chunk bodies and their prefetches (rounds 2-3)
@@ -125,6 +138,10 @@ def parametric(name):
         if int(f[2]) > 0:
             extra += "  if (wave >= 4) __builtin_amdgcn_s_setprio(%d);\n" % int(f[2])
         return [("kernels_nn32.hip", code, extra, "after")]
+    if f[0] == "lw_ldspad" and len(f) == 2:  # the LW solver's blocks hold KB more LDS each (fewer blocks per CU)
+        return [("kernels_rte.hip", "  extern __shared__ __attribute__((aligned(16))) float smem[];\n  const int icol = blockIdx.x, g = threadIdx.x;\n",
+                 "  __shared__ float pad_[%d * 256];\n  if (ngpt == -12345) { pad_[threadIdx.x] = 1.0f; flux_up[0] = pad_[threadIdx.x ^ 1]; }\n"
+                 % int(f[1]), "after")]
     if f[0] == "swck_ahead" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkAheadSmall = %s;" % f[1], r"constexpr int kCkAheadSmall = \d+;")]
     if f[0] == "swck_p1small" and len(f) == 2:
