@@ -62,9 +62,6 @@ def parse():
                     "choice)")
     ap.add_argument("--sw-priority", type=int, default=0, help="priority of the SW chain's stream (-1: high)")
     ap.add_argument("--sw-net-cus", type=int, default=0, help="the SW network's blocks on at most this many CUs (0: all)")
-    ap.add_argument("--no-sw-beam", action="store_true",
-                    help="the SW solver forms its direct beam itself (default: the SW network hands it over where the "
-                         "solver takes its small-grid kernel)")
     ap.add_argument("--lw-net-cus", type=int, default=None,
                     help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
                          "choice: 5/8 of the CUs at small grids, where the LW chain follows the SW network)")
@@ -272,7 +269,7 @@ def main():
                                                      overlap=not args.no_overlap, sw=args.config not in ("c1", "c2"),
                                                      lw_after=lw_after, sw_after=sw_after,
                                                      sw_priority=args.sw_priority, lw_net_cus=args.lw_net_cus,
-                                                     sw_net_cus=args.sw_net_cus, sw_beam=not args.no_sw_beam),
+                                                     sw_net_cus=args.sw_net_cus),
                            use_graph=use_graph)
     step = rank_run.step
     prob, clouds = rank_run.first

@@ -186,21 +186,6 @@ int rrtmgpnn_gas_optics_sw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngp
                               const float *tlay, const float *plev, const float *vmr_h2o,
                               const float *const *gas_conc, const int *gas_ndims,
                               const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g);
-/* MI355X: rrtmgpnn_gas_optics_sw_nn followed on the same context by rrtmgpnn_sw_solver_2stream (rte_sw's solver
- * call, mo_rte_sw.F90:249-257 -> sw_solver_2stream, mo_rte_solver_kernels.F90:541-692) with these top_at_1, inc_flux
- * (ngpt, ncol) and mu0 (ncol), tau and ssa as outputs here and inputs there, g = NULL: where that solver call takes the
- * checkpointed small-grid kernel, the network kernel also forms its pass 1 -- the direct-beam transmittances
- * exp(-tau/mu0) and the beam at every chunk top, into the context workspace -- and the solver call starts at pass 2.
- * tau / ssa / g and the fluxes are bit-identical to the two plain calls.  The hand-over holds for the NEXT entry on the
- * context only, and only if it is that solver call with the same tau, mu0, inc_flux, sizes and orientation (anything
- * else: the solver forms the beam itself); tau, mu0 and inc_flux must not change in between. */
-int rrtmgpnn_gas_optics_sw_nn_beam(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
-                                   const float *tlay, const float *plev, const float *vmr_h2o,
-                                   const float *const *gas_conc, const int *gas_ndims,
-                                   const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g, int top_at_1,
-                                   const float *inc_flux, const float *mu0);
-/* SW solver calls on this context that started from a beam handed over by rrtmgpnn_gas_optics_sw_nn_beam. */
-int rrtmgpnn_context_get_sw_beam_handoffs(rrtmgpnn_context *ctx, long long *n);
 /* Generic MLP forward (network_type%output_sgemm_flat, neural/mod_network.F90:273-354):
  * out(ny, nbatch) = net(x(nx, nbatch)), last-layer activation applied, no post-processing. */
 int rrtmgpnn_network_forward(rrtmgpnn_context *ctx, const rrtmgpnn_network *net, long long nbatch,

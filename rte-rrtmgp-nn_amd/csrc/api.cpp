@@ -79,7 +79,6 @@ static int finalize_network(rrtmgpnn_network *net)
 static int check_ctx(rrtmgpnn_context *ctx)
 {
   if (!ctx) return fail(RRTMGPNN_ERR_ARGUMENT, "null context");
-  ctx->call_gen++;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return fail(RRTMGPNN_ERR_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
   return RRTMGPNN_OK;
@@ -217,13 +216,6 @@ int rrtmgpnn_context_get_mlp_max_cus(rrtmgpnn_context *ctx, int *cus)
   if (int rc = check_ctx(ctx)) return rc;
   if (!cus) return fail(RRTMGPNN_ERR_ARGUMENT, "null cus");
   *cus = ctx->mlp_max_cus;
-  return RRTMGPNN_OK;
-}
-
-int rrtmgpnn_context_get_sw_beam_handoffs(rrtmgpnn_context *ctx, long long *n)
-{
-  if (!ctx || !n) return fail(RRTMGPNN_ERR_ARGUMENT, "get_sw_beam_handoffs: null argument");
-  *n = ctx->sw_beam_handoffs;
   return RRTMGPNN_OK;
 }
 
@@ -576,13 +568,12 @@ int rrtmgpnn_gas_optics_lw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngp
   return rrtmgpnn_predict_nn_lw(ctx, ncol, nlay, ngpt, ninputs, x, cd, nets, nnets, tau, pfrac);
 }
 
-// rrtmgpnn_gas_optics_sw_nn, and with beam (top_at_1, inc_flux, mu0 non-null) the SW solver's pass 1 as well
-static int gas_optics_sw_nn_impl(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
-                                 const float *tlay, const float *plev, const float *vmr_h2o,
-                                 const float *const *gas_conc, const int *gas_ndims,
-                                 const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g,
-                                 const int *top_at_1, const float *inc_flux, const float *mu0)
+int rrtmgpnn_gas_optics_sw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
+                              const float *tlay, const float *plev, const float *vmr_h2o,
+                              const float *const *gas_conc, const int *gas_ndims,
+                              const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g)
 {
+  if (int rc = check_ctx(ctx)) return rc;
   if (!nets || !nets[0] || !tau || ncol < 0 || ngpt < 1) return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_sw_nn: bad argument");
   MlpInputs in;
   if (int rc = fused_inputs("gas_optics_sw_nn", nets[0], ninputs, nlay, play, tlay, plev, vmr_h2o, gas_conc, gas_ndims,
@@ -595,52 +586,12 @@ static int gas_optics_sw_nn_impl(rrtmgpnn_context *ctx, int ncol, int nlay, int 
     if (!B || B->dims[0] != ninputs || A->dims[A->nlayers] != ngpt || B->dims[B->nlayers] != ngpt ||
         !A->has_out_scaling() || !B->has_out_scaling())
       return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_sw_nn: absorption / Rayleigh networks missing or inconsistent");
-    int nrw = 0;
-    long long tn_off = 0;
-    if (top_at_1 && sw_beam_applies(ctx, ngpt, nlay, ncol, &nrw, &tn_off)) {
-      void *ws = nullptr;
-      if (int rc = ctx->workspace(sizeof(float) * sw_2stream_ck_ws_floats(ngpt, nlay, ncol, true, false, true), &ws))
-        return rc;
-      in.beam_mu0 = mu0; in.beam_inc = inc_flux; in.beam_ws = (float *)ws; in.beam_tn_off = tn_off;
-      in.beam_nrw = nrw; in.beam_top_at_1 = *top_at_1 ? 1 : 0;
-      const int rc = launch_mlp32(ctx, MLP_SW_PAIR, A, B, N, ngpt, nullptr, nullptr, tau, ssa, g, &in);
-      if (rc == RRTMGPNN_OK) {
-        auto &bm = ctx->sw_beam;
-        bm.gen = ctx->call_gen; bm.tau = tau; bm.mu0 = mu0; bm.inc = inc_flux; bm.ws = ws;
-        bm.ncol = ncol; bm.nlay = nlay; bm.ngpt = ngpt; bm.top_at_1 = in.beam_top_at_1;
-        return RRTMGPNN_OK;
-      }
-      if (rc != RRTMGPNN_ERR_UNSUPPORTED) return rc;
-      in.beam_ws = nullptr;  // no beam-forming instance for these networks: the plain pair, the solver's own pass 1
-    }
     const int rc = launch_mlp(ctx, MLP_SW_PAIR, A, B, N, ngpt, nullptr, nullptr, tau, ssa, g, &in);
     if (rc != RRTMGPNN_ERR_UNSUPPORTED) return rc;
   }
   const float *x = nullptr, *cd = nullptr;
   if (int rc = fused_fallback(ctx, ncol, nlay, in, ninputs, &x, &cd)) return rc;
   return rrtmgpnn_predict_nn_sw(ctx, ncol, nlay, ngpt, ninputs, x, cd, nets, tau, ssa, g);
-}
-
-int rrtmgpnn_gas_optics_sw_nn(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
-                              const float *tlay, const float *plev, const float *vmr_h2o,
-                              const float *const *gas_conc, const int *gas_ndims,
-                              const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g)
-{
-  if (int rc = check_ctx(ctx)) return rc;
-  return gas_optics_sw_nn_impl(ctx, ncol, nlay, ngpt, ninputs, play, tlay, plev, vmr_h2o, gas_conc, gas_ndims, nets, tau,
-                               ssa, g, nullptr, nullptr, nullptr);
-}
-
-int rrtmgpnn_gas_optics_sw_nn_beam(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *play,
-                                   const float *tlay, const float *plev, const float *vmr_h2o,
-                                   const float *const *gas_conc, const int *gas_ndims,
-                                   const rrtmgpnn_network *const *nets, float *tau, float *ssa, float *g, int top_at_1,
-                                   const float *inc_flux, const float *mu0)
-{
-  if (int rc = check_ctx(ctx)) return rc;
-  if (!inc_flux || !mu0) return fail(RRTMGPNN_ERR_ARGUMENT, "gas_optics_sw_nn_beam: inc_flux and mu0 are required");
-  return gas_optics_sw_nn_impl(ctx, ncol, nlay, ngpt, ninputs, play, tlay, plev, vmr_h2o, gas_conc, gas_ndims, nets, tau,
-                               ssa, g, &top_at_1, inc_flux, mu0);
 }
 
 int rrtmgpnn_predict_nn_sw(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, int ninputs, const float *nn_inputs,
@@ -776,17 +727,6 @@ int rrtmgpnn_sw_solver_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int nc
   if (!inc_flux || !tau || !ssa || !mu0 || !sfc_alb_dir_gpt || !sfc_alb_dif_gpt || !flux_up || !flux_dn ||
       !flux_dir || ngpt < 1 || nlay < 1 || ncol < 0)
     return fail(RRTMGPNN_ERR_ARGUMENT, "sw_solver_2stream: bad argument");
-  // the beam the SW pair formed for this call (rrtmgpnn_gas_optics_sw_nn_beam, the previous entry on the context)
-  const auto bm = ctx->sw_beam;
-  ctx->sw_beam = rrtmgpnn_context::SwBeam{};
-  const auto &ex = ctx->extras;
-  if (bm.tau && bm.gen + 1 == ctx->call_gen && bm.tau == tau && bm.mu0 == mu0 && bm.inc == inc_flux && !g &&
-      bm.ncol == ncol && bm.nlay == nlay && bm.ngpt == ngpt && bm.top_at_1 == (top_at_1 ? 1 : 0) && bm.ws == ctx->ws &&
-      !ex.gpt_up && !ex.gpt_dn && !ex.gpt_dir) {
-    ctx->sw_beam_handoffs++;
-    return launch_sw_2stream_beam(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, mu0,
-                                  sfc_alb_dir_gpt, sfc_alb_dif_gpt, flux_up, flux_dn, flux_dir);
-  }
   return launch_sw_2stream(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, sfc_alb_dir_gpt,
                            sfc_alb_dif_gpt, nullptr, nullptr, nullptr, nullptr, flux_up, flux_dn, flux_dir);
 }

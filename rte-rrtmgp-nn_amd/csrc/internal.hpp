@@ -62,18 +62,6 @@ struct rrtmgpnn_context {
     const float *lw_Ds = nullptr;
     float *gpt_up = nullptr, *gpt_dn = nullptr, *gpt_dir = nullptr;
   } extras;
-  // every C entry taking the context counts itself here (check_ctx), so a hand-over between two entries can require
-  // that they are consecutive on the context
-  unsigned long long call_gen = 0;
-  // the direct beam the SW pair formed for the SW solver call that follows (rrtmgpnn_gas_optics_sw_nn_beam): valid for
-  // the next entry on this context only (gen + 1), with the same tau, mu0, incident flux, sizes and orientation
-  struct SwBeam {
-    unsigned long long gen = 0;
-    const float *tau = nullptr, *mu0 = nullptr, *inc = nullptr;
-    const void *ws = nullptr;
-    int ncol = 0, nlay = 0, ngpt = 0, top_at_1 = 0;
-  } sw_beam;
-  long long sw_beam_handoffs = 0;  // SW solver calls that started from a handed-over beam
   void *ws = nullptr;
   size_t ws_bytes = 0;
   bool ws_pinned = false;
@@ -176,15 +164,7 @@ struct MlpInputs {
   int nlay;
   GasArgs gas;
   float mn[kMaxInputs], mx[kMaxInputs];
-  // the SW pair only (rrtmgpnn_gas_optics_sw_nn_beam): also form the SW solver's pass 1 -- beam checkpoints (ngpt,
-  // beam_nrw, ncol) at beam_ws, transmittances (ngpt, nlay, ncol) at beam_ws + beam_tn_off (kernels_nn32.hip BEAM)
-  const float *beam_mu0 = nullptr, *beam_inc = nullptr;
-  float *beam_ws = nullptr;
-  long long beam_tn_off = 0;
-  int beam_nrw = 0, beam_top_at_1 = 0;
 };
-// layers per checkpoint chunk of the SW solver's small-grid instance, which the beam-forming SW pair writes for
-constexpr int kSwBeamK = 3;
 int launch_mlp(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A, const rrtmgpnn_network *B,
                long long nbatch, int ngpt, const float *x, const float *col_dry, float *out0, float *out1,
                float *out2, const MlpInputs *in = nullptr);
@@ -234,19 +214,12 @@ int launch_sw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
 // kernels_sw_ck.hip (checkpointed passes; called by launch_sw_2stream for even ngpt in mode 3)
 // the checkpointed SW kernel's small-grid instance applies (clear sky, g = 0, no g-point outputs, the grid in one round)
 bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bool inc, bool gpt);
-// the clear-sky NN solver call (g = 0, no increment, no g-point outputs) takes the small-grid checkpointed instance,
-// whose pass 1 the SW pair can form (rrtmgpnn_gas_optics_sw_nn_beam); its checkpoint rows per column and the float
-// offset of its transmittance plane in the workspace
-bool sw_beam_applies(const rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int *nrw, long long *tn_off);
-int launch_sw_2stream_beam(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
-                           const float *inc_flux_dif, const float *tau, const float *ssa, const float *mu0,
-                           const float *alb_dir, const float *alb_dif, float *flux_up, float *flux_dn, float *flux_dir);
 size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn);
 int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
-                         float *flux_dn, float *flux_dir, bool beam_in = false);
+                         float *flux_dn, float *flux_dir);
 // kernels_lw_scat.hip
 int launch_lw_rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
                     const float *wts, const float *inc_flux, const float *tau, const float *ssa, const float *g,

@@ -179,20 +179,7 @@ struct Mlp32Args {
   uint32_t gsm[kMaxInputs], glm[kMaxInputs], grec[kMaxInputs];
   // the same per input as a 2-bit code (0 absent, 1 scalar, 2 1-D, 3 2-D), 16 inputs per word (kMlpPackedIn)
   uint32_t gcode[(kMaxInputs + 15) / 16];
-  // SW pair with the direct beam (BEAM instances): mu0 (ncol), the incident flux (ngpt, ncol), the SW solver's
-  // workspace -- beam checkpoints (ngpt, nrw, ncol) at ws, transmittances (ngpt, nlay, ncol) at ws + tn_off
-  const float *mu0, *inc;
-  float *ws;
-  long long tn_off;
-  int nrw;
 };
-
-// The SW pair can also form the SW solver's pass 1 (kernels_sw_ck.hip's small-grid instance): the direct-beam
-// transmittances exp(-tau/mu0) of every element it predicts, and the beam walked down each column with its value at
-// every chunk top -- the solver then starts at pass 2 and never re-reads tau for the beam.  A wave owns whole columns
-// (ceil(nlay/32) tiles, the top one first) so the walk stays in its registers: after a g-tile pair's epilogue one
-// v_permlane32_swap per register gives every lane all 32 rows of one g-point (lane half h: g-tile 2q + h), and the lane
-// multiplies them down in layer order -- pass 1's products, in pass 1's order, the same bits.
 
 // In-kernel inputs of the LW pair: per-input multipliers and ranges from the packed codes (a few scalar ops per tile)
 // and the gas pointers re-read per tile, instead of 3 x 18 words and 18 buffer descriptors held across the tile loop
@@ -278,25 +265,21 @@ constexpr int kMlp32Threads = 512, kSwNT = 512, kSwWPE = 1;
 // A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  The host guarantees that the
 // g-tiles are full: ngpt = 32 NGT (LW pair) or 2 ngpt = 32 NGT (LW both).  Dynamic LDS: the weight images, then 32
 // floats per wave (the tile's column amounts, handed from the sample lanes to the row registers).
-// BEAM (MLP_SW_PAIR with XIN only): the direct beam as well (above); TOP1: the column's layer 0 is its top
 template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN,
-          int NT = kMlp32Threads, int WPE = 1, bool BEAM = false, bool TOP1 = false>
+          int NT = kMlp32Threads, int WPE = 1>
 __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
 {
   constexpr bool kPair = MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR;
-  static_assert(!BEAM || (MODE == MLP_SW_PAIR && XIN), "the beam is formed by the fused SW pair only");
   extern __shared__ floatx4 lds4[];
-  float *cds = (float *)lds4 + a.imgA_floats + (kPair ? a.imgB_floats : 0);
-  uint64_t *etab = (uint64_t *)(cds + 32 * (NT / 64));  // BEAM: the exp table after the waves' column-amount slots
   {
     const int n4 = (a.imgA_floats + (kPair ? a.imgB_floats : 0)) / 4, nA4 = a.imgA_floats / 4;
     const floatx4 *srcA = (const floatx4 *)a.imgA, *srcB = (const floatx4 *)a.imgB;
     for (int i = threadIdx.x; i < n4; i += blockDim.x) lds4[i] = i < nA4 ? srcA[i] : srcB[i - nA4];
-    if constexpr (BEAM) load_exp_table(etab);
   }
   __syncthreads();
   const float *imgA = (const float *)lds4;
   const float *imgB = imgA + a.imgA_floats;
+  float *cds = (float *)lds4 + a.imgA_floats + (kPair ? a.imgB_floats : 0);
   constexpr Img32 LA = img32_layout(KS, AH1, AN2, AH2, AN3, NGT);
   constexpr Img32 LB = img32_layout(KS, BH1, BN2, BH2, BN3, NGT);
   const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
@@ -309,9 +292,8 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
   // Layer-1 B operand of step s: input k = 2s + h of sample s0 + j.  XIN: raw[s] holds the state value input k is
   // formed from (s = 0: tlay / play; s = 1: h2o / o3; s > 1: gas k), raw[KS..KS+2] = h2o, p(lev ilay), p(lev ilay+1)
   constexpr int NR = XIN ? KS + 3 : KS;
-  // the 32 samples from s0 (a tile); loads past the batch return 0
-  auto load_x = [&](uint32_t s0, float (&xv)[NR]) {
-    const uint32_t s = s0 + (uint32_t)j;
+  auto load_x = [&](int tl, float (&xv)[NR]) {
+    const uint32_t s = (uint32_t)tl * 32u + (uint32_t)j;  // loads past the batch return 0
     if constexpr (XIN) {
       const uint32_t nlay = (uint32_t)a.nlay;
       const uint32_t icol = s / nlay, ilay = s - icol * nlay;
@@ -382,150 +364,13 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
     }
   };
 
-  if constexpr (BEAM) {
-    // a wave per column, its tiles top first (TOP1: tile 0 holds layers 0..31, the top; otherwise the last tile)
-    constexpr int K = kSwBeamK, NP = (NGT + 1) / 2;
-    const int nlay = a.nlay, tpc = (nlay + 31) / 32, ncolw = a.ncol;
-    auto tile_of = [&](int tt) { return TOP1 ? tt : tpc - 1 - tt; };
-    const int col0 = blockIdx.x * nwaves + wave, cstride = gridDim.x * nwaves;
-    float xn[NR];
-    load_x((uint32_t)(col0 * nlay + tile_of(0) * 32), xn);
-    for (int icol = col0; icol < ncolw; icol += cstride) {
-      const float mu0 = a.mu0[icol], mu0_inv = 1.0f / mu0;
-      // lane (j, h) walks g-point 32(2q + h) + j of g-tile pair q; Ftop = inc_flux * mu0 as the solver forms it
-      float Fd[NP];
-#pragma unroll
-      for (int q = 0; q < NP; q++) {
-        const int go = 2 * q + h;
-        Fd[q] = go < NGT ? a.inc[32 * go + j + (size_t)ngpt * icol] * mu0 : 0.0f;
-      }
-      const Buf oC(a.ws + (size_t)icol * a.nrw * ngpt, (uint32_t)a.nrw * (uint32_t)ngpt * 4u);
-      for (int tt = 0; tt < tpc; tt++) {
-        const int t = tile_of(tt);
-        const uint32_t s0 = (uint32_t)__builtin_amdgcn_readfirstlane(icol * nlay + t * 32);
-        const uint32_t nvalid = (uint32_t)min(32, nlay - t * 32);
-        float xv[NR];
-#pragma unroll
-        for (int k = 0; k < NR; k++) xv[k] = xn[k];
-        {
-          const int nc = tt + 1 < tpc ? icol : icol + cstride, nt = tt + 1 < tpc ? tile_of(tt + 1) : tile_of(0);
-          load_x((uint32_t)(nc * nlay + nt * 32), xn);  // past the batch: zeros, never used
-        }
-        int lds_off = 0;
-        asm volatile("" : "+s"(lds_off));
-        const float *iA = imgA + lds_off, *iB = imgB + lds_off;
-        const float cd = form_x(xv, iA + LA.xs);
-        float x1[KS];
-#pragma unroll
-        for (int k = 0; k < KS; k++) x1[k] = xv[k];
-        float hA[AN3], hB[BN3];
-        mlp32_hidden<KS, AH1, AN2, AH2, AN3, NGT>(iA, x1, lane, hA);
-        mlp32_hidden<KS, BH1, BN2, BH2, BN3, NGT>(iB, x1, lane, hB);
-        const uint32_t rows = nvalid * (uint32_t)ngpt * 4u;
-        const Buf o0(a.out0 + (size_t)s0 * ngpt, rows), o1(a.out1 + (size_t)s0 * ngpt, rows);
-        const Buf o2(a.out2 ? a.out2 + (size_t)s0 * ngpt : a.out0, a.out2 ? rows : 0u);
-        const Buf oT(a.ws + a.tn_off + (size_t)s0 * ngpt, rows);
-        float *slot = cds + wave * 32;
-        slot[j] = cd;
-        __builtin_amdgcn_wave_barrier();
-        float cdr[16];
-        uint32_t vo[16];
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const floatx4 v = *(const floatx4 *)&slot[8 * b + 4 * h];
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const uint32_t R = (uint32_t)(8 * b + 4 * h + i);
-            cdr[4 * b + i] = v[i];
-            vo[4 * b + i] = R < nvalid ? 4u * (R * (uint32_t)ngpt + (uint32_t)j) : kOOB;
-          }
-        }
-        // g-tile go: the SW pair's epilogue and stores (as below), and the rows' transmittances exp(-tau/mu0) in T
-        auto epi = [&](int go, float (&T)[16]) {
-          const floatx16 yA = mfma_chain_t<AN3>(iA + LA.l3, go, hA, lane);
-          const floatx16 yB = mfma_chain_t<BN3>(iB + LB.l3, go, hB, lane);
-          const int g = 32 * go + j;
-          const float bA = iA[LA.b3 + g], sdA = iA[LA.sd + g], mnA = iA[LA.mn + g];
-          const float bB = iB[LB.b3 + g], sdB = iB[LB.sd + g], mnB = iB[LB.mn + g];
-          float arg[16];
-#pragma unroll
-          for (int r = 0; r < 16; r++) {
-            float ta = sdA * (yA[r] + bA);
-            ta = ta + mnA;
-            const float vabs = pow8(ta) * cdr[r];
-            float tr = sdB * (yB[r] + bB);
-            tr = tr + mnB;
-            const float vray = pow8(tr) * cdr[r];
-            const float tot = vabs + vray, ssa = vray / tot;
-            const uint32_t off = vo[r] + 128u * go;
-            o0.st(tot, off);
-            o1.st(ssa, off);
-            arg[r] = -tot * mu0_inv;  // kernels_sw_ck.hip pass 1: -tau * (1 / mu0)
-          }
-          if (a.out2) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) o2.st(0.0f, vo[r] + 128u * go);
-          }
-          ref_expf_neg_batch<16>(arg, T, etab);
-#pragma unroll
-          for (int r = 0; r < 16; r++) oT.st(T[r], vo[r] + 128u * go);
-        };
-        // g-tiles in a loop (one copy of the epilogue and of the walk: the unrolled form was 64 KB of code): an even
-        // g-tile's transmittances wait in Te for its odd partner; after the odd one (or the last, unpaired, even one)
-        // lanes 32-63 of the even g-tile's registers swap with lanes 0-31 of the odd one's, so that every lane holds
-        // rows (r&3) + 8(r>>2) of its g-point (g-tile 2q + h) in A[r] and rows (r&3) + 8(r>>2) + 4 in B[r]; the lane
-        // then walks them.  Fd[0] is the current pair's beam: the array rotates after each pair.
-        float Te[16];
-#pragma unroll 1
-        for (int go = 0; go < NGT; go++) {
-          float Tc[16];
-          epi(go, Tc);
-          const bool odd = go & 1;
-          if (!odd && go + 1 < NGT) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) Te[r] = Tc[r];
-            continue;
-          }
-          float A[16], B[16];
-#pragma unroll
-          for (int r = 0; r < 16; r++) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(odd ? Te[r] : Tc[r]),
-                                                             __float_as_uint(odd ? Tc[r] : 0.0f), false, false);
-            A[r] = __uint_as_float(sw[0]);
-            B[r] = __uint_as_float(sw[1]);
-          }
-          const int q = go >> 1;
-          const bool gv = 2 * q + h < NGT;
-          const uint32_t vg = 4u * (uint32_t)(32 * (2 * q + h) + j);
-          // down the tile's rows in the walk's order: the beam at every chunk top (checkpoint row jt / K), then the
-          // layer's transmittance applied
-#pragma unroll
-          for (int k = 0; k < 32; k++) {
-            const int R = TOP1 ? k : 31 - k;
-            const float Tv = ((R >> 2) & 1) ? B[(R & 3) + 4 * (R >> 3)] : A[(R & 3) + 4 * (R >> 3)];
-            const int l = t * 32 + R, jt = TOP1 ? l : nlay - 1 - l;
-            if (R < (int)nvalid) {  // wave-uniform
-              if (jt % K == 0) oC.st(Fd[0], gv ? vg + 4u * (uint32_t)ngpt * (uint32_t)(jt / K) : kOOB);
-              Fd[0] = Tv * Fd[0];
-            }
-          }
-          const float f0 = Fd[0];
-#pragma unroll
-          for (int p = 0; p + 1 < NP; p++) Fd[p] = Fd[p + 1];
-          Fd[NP - 1] = f0;
-        }
-      }
-    }
-    return;
-  }
-
   float xn[NR];  // the next tile's inputs, loaded before this tile's stores
-  load_x((uint32_t)(blockIdx.x * nwaves + wave) * 32u, xn);
+  load_x(blockIdx.x * nwaves + wave, xn);
   for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += tstride) {
     float xv[NR];
 #pragma unroll
     for (int t = 0; t < NR; t++) xv[t] = xn[t];
-    load_x((uint32_t)(tile + tstride) * 32u, xn);
+    load_x(tile + tstride, xn);
     // The weight images are loop-invariant: left visible, their LDS reads are hoisted out of the tile loop and
     // spilled to scratch.  An offset the compiler cannot see through keeps them inside, next to their MFMAs.
     int lds_off = 0;
@@ -637,17 +482,16 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
 constexpr int kOccDevices = 64;
 
 template <int KS, int AH1, int AN2, int AH2, int AN3, int BH1, int BN2, int BH2, int BN3, int NGT, int MODE, bool XIN,
-          int NT = kMlp32Threads, int WPE = 1, bool BEAM = false, bool TOP1 = false>
+          int NT = kMlp32Threads, int WPE = 1>
 static int launch32(rrtmgpnn_context *ctx, Mlp32Args &a)
 {
-  auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN, NT, WPE, BEAM, TOP1>;
+  auto kern = mlp32_kernel<KS, AH1, AN2, AH2, AN3, BH1, BN2, BH2, BN3, NGT, MODE, XIN, NT, WPE>;
   const size_t lds = sizeof(float) * ((size_t)(a.imgA_floats + (MODE != MLP_LW_BOTH ? a.imgB_floats : 0)) +
-                                      32 * (NT / 64) + (BEAM ? 64 : 0));  // BEAM: + the exp table (32 x u64)
+                                      32 * (NT / 64));
   if (lds > 160 * 1024) return RRTMGPNN_ERR_UNSUPPORTED;
   if (lds > 64 * 1024)
     if (int rc = raise_lds_limit((const void *)kern)) return rc;
-  // work units the waves stride: 32-sample tiles, or (BEAM) whole columns
-  const long long ntiles = BEAM ? (long long)a.ncol : ((long long)a.nbatch + 31) / 32;
+  const long long ntiles = ((long long)a.nbatch + 31) / 32;
   const int wpb = NT / 64;
   int per_cu = std::min(std::max(1, (int)((160 * 1024) / std::max<size_t>(lds, 1))), 2048 / NT);
   const long long want = (ntiles + wpb - 1) / wpb;
@@ -742,15 +586,6 @@ int launch_mlp32(rrtmgpnn_context *ctx, MlpMode mode, const rrtmgpnn_network *A,
   }
   if (mode == MLP_SW_PAIR && shape32(A, 4, 1, 8, 1, 8, 7) && shape32(B, 4, 1, 8, 1, 8, 7)) {
     // the shipped g224 pair: absorption and Rayleigh 7-16-16-224
-    if (xin && in->beam_ws) {  // and the SW solver's pass 1 (rrtmgpnn_gas_optics_sw_nn_beam)
-      if (nbatch != (long long)a.ncol * in->nlay) return RRTMGPNN_ERR_UNSUPPORTED;
-      a.mu0 = in->beam_mu0; a.inc = in->beam_inc; a.ws = in->beam_ws; a.tn_off = in->beam_tn_off;
-      a.nrw = in->beam_nrw;
-      if (in->beam_top_at_1)
-        return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, true, kSwNT, kSwWPE, true, true>(ctx, a);
-      return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, true, kSwNT, kSwWPE, true, false>(ctx, a);
-    }
-    if (in && in->beam_ws) return RRTMGPNN_ERR_UNSUPPORTED;
     if (xin) return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, true, kSwNT, kSwWPE>(ctx, a);
     return launch32<4, 1, 8, 1, 8, 1, 8, 1, 8, 7, MLP_SW_PAIR, false, kSwNT, kSwWPE>(ctx, a);
   }

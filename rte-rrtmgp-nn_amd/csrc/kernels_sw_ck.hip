@@ -175,7 +175,7 @@ constexpr int kCkAheadSmall = 1;
 // (the RRTMGP g-point sets: 16 per band).  Round 4, C4: SW solver -1.7 % alone, steps -0.8 % (3 alternating pairs)
 template <bool kHasG, bool kInc, int K, bool kGpt = false, int R = kCkRing,
           int WAVES = (!kHasG && !kInc && !kGpt) ? kCkWavesNN : kCkWaves, bool kTn = false,
-          class V = f2, bool kEmk = false, bool kBandPair = false, int P1C = kCkP1, int AHEAD = 1, bool kBeamIn = false>
+          class V = f2, bool kEmk = false, bool kBandPair = false, int P1C = kCkP1, int AHEAD = 1>
 __global__ void __launch_bounds__(512, WAVES)
     sw_2stream_ck_kernel(int ngpt, int nlay, int ncol, int top_at_1, int ncb, const float *__restrict__ inc_flux,
                          const float *__restrict__ inc_dif, const float *__restrict__ tau,
@@ -187,8 +187,6 @@ __global__ void __launch_bounds__(512, WAVES)
                          float *__restrict__ gpt_dn, float *__restrict__ gpt_dir)
 {
   static_assert(R % K == 0, "the flux ring must hold whole chunks");
-  // kBeamIn: pass 1 was formed by the SW pair (kernels_nn32.hip BEAM) into this workspace's beam rows and plane
-  static_assert(!kBeamIn || (kTn && K == kSwBeamK), "a handed-over beam needs the transmittance plane and its chunks");
   constexpr bool kG0 = !kHasG && !kInc;  // g is the literal 0 (the NN path)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // `ncb` columns per block: lane t works on column c = t / (ngpt/NPL), g-points g .. g + NPL - 1
@@ -324,14 +322,7 @@ __global__ void __launch_bounds__(512, WAVES)
   // ---- pass 1: direct beam, checkpoint at every chunk top ----
   // Steps of P1 = kCkP1 * K layers: pass 1 has little arithmetic per layer, so it needs many loads in flight.
   V Fd = Ftop;
-  if constexpr (kBeamIn) {
-    // the beam at the surface, from the last chunk's checkpoint through its layers as pass 1 walks them
-    const int ckl = nck - 1, n = nlay - ckl * K;
-    Fd = CW.ldv(vW, row * (uint32_t)ckl);
-#pragma unroll
-    for (int p = 0; p < K; p++)
-      if (p < n) Fd = CT.ldv(vL, row * (uint32_t)lay(ckl * K + p)) * Fd;
-  } else {
+  {
     constexpr int P1 = P1C * K;
     const int np1 = (nlay + P1 - 1) / P1;
     struct Buf1 {
@@ -546,7 +537,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
-                         float *flux_dn, float *flux_dir, bool beam_in)
+                         float *flux_dn, float *flux_dir)
 {
   const int ncb2 = 2 * (ngpt / 2) <= 512 ? 2 : 1;  // two columns per block where 512 lanes hold them
   const BandArgs nob{};
@@ -589,47 +580,12 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   if (g) return go(sw_2stream_ck_kernel<true, false, kCkK>, nullptr, nullptr, nullptr);
   // the small-grid instance when the clear-sky grid fits in one round of resident waves (2 g-points per lane, 16
   // waves per CU)
-  if (sw_ck_small(ctx, ngpt, ncol, false, false, false) && beam_in)
-    return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
-                                   kCkEmkSmall, false, kCkP1Small, kCkAheadSmall, true>,
-              nullptr, nullptr, nullptr, kCkRingSmall, (int)(sizeof(VSmall) / sizeof(float)));
-  if (beam_in) return fail(RRTMGPNN_ERR_ARGUMENT, "sw solver: a handed-over beam needs the small-grid instance");
   if (sw_ck_small(ctx, ngpt, ncol, false, false, false))
     return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
                                    kCkEmkSmall, false, kCkP1Small, kCkAheadSmall>,
               nullptr, nullptr, nullptr, kCkRingSmall, (int)(sizeof(VSmall) / sizeof(float)));
   return go(sw_2stream_ck_kernel<false, false, kCkK, false, kCkRing, kCkWavesNN, kCkTnNN, f2, kCkEmkNN>, nullptr,
             nullptr, nullptr);
-}
-
-}  // namespace rrtmgpnn
-
-namespace rrtmgpnn {
-
-bool sw_beam_applies(const rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int *nrw, long long *tn_off)
-{
-  const int mode = ctx->sw_kernel >= 0 ? ctx->sw_kernel : g_sw_kernel_default;
-  if (!kCkTnSmall || kCkKSmall != kSwBeamK || ngpt % 2 != 0 || ngpt > 256 || nlay < 1 || ncol < 1 ||
-      (mode != 0 && mode != 3) || !sw_ck_small(ctx, ngpt, ncol, false, false, false))
-    return false;
-  const int nck = (nlay + kSwBeamK - 1) / kSwBeamK;
-  *nrw = 3 * nck + 2;
-  *tn_off = (long long)ngpt * (*nrw) * ncol;
-  return true;
-}
-
-int launch_sw_2stream_beam(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
-                           const float *inc_flux_dif, const float *tau, const float *ssa, const float *mu0,
-                           const float *alb_dir, const float *alb_dif, float *flux_up, float *flux_dn, float *flux_dir)
-{
-  int nrw = 0;
-  long long tn_off = 0;
-  if (!sw_beam_applies(ctx, ngpt, nlay, ncol, &nrw, &tn_off))
-    return fail(RRTMGPNN_ERR_ARGUMENT, "sw solver: the handed-over beam no longer applies");
-  void *ws = nullptr;
-  if (int rc = ctx->workspace(sizeof(float) * sw_2stream_ck_ws_floats(ngpt, nlay, ncol, true, false, true), &ws)) return rc;
-  return launch_sw_2stream_ck(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, nullptr, mu0, alb_dir,
-                              alb_dif, nullptr, nullptr, nullptr, nullptr, ws, flux_up, flux_dn, flux_dir, true);
 }
 
 }  // namespace rrtmgpnn

@@ -61,9 +61,6 @@ SIGNATURES = {
                                           P(c_vp), c_int, c_vp, c_vp]),
     "rrtmgpnn_gas_optics_sw_nn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, P(c_vp), P(c_int),
                                           P(c_vp), c_vp, c_vp, c_vp]),
-    "rrtmgpnn_gas_optics_sw_nn_beam": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, P(c_vp),
-                                               P(c_int), P(c_vp), c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
-    "rrtmgpnn_context_get_sw_beam_handoffs": (c_int, [c_vp, ctypes.POINTER(c_ll)]),
     "rrtmgpnn_network_forward": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),
     "rrtmgpnn_compute_planck_source_nn": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int,
                                                   P(c_int), c_float, c_float, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -75,12 +75,6 @@ class Context:
         check(_lib.lib().rrtmgpnn_context_get_mlp_max_cus(self.h, ctypes.byref(v)), "context_get_mlp_max_cus")
         return v.value
 
-    def sw_beam_handoffs(self):
-        """SW solver calls on this context that started from the beam rrtmgpnn_gas_optics_sw_nn_beam handed over."""
-        v = ctypes.c_longlong(0)
-        check(_lib.lib().rrtmgpnn_context_get_sw_beam_handoffs(self.h, ctypes.byref(v)), "context_get_sw_beam_handoffs")
-        return v.value
-
     def set_mlp_kernel(self, mode):
         """0: the gas-optics networks on 32x32x2 MFMA tiles where instantiated (default); 1: 16x16x4 (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_mlp_kernel(self.h, int(mode)), "context_set_mlp_kernel")

@@ -69,10 +69,8 @@ def _t(a, dev):
 class ClearSkyStep:
     def __init__(self, prob, device=0, nmus=1, ctx=None, lw_models=("lw_abs", "lw_pfrac"),
                  sw_models=("sw_abs", "sw_ray"), fused=True, clouds=None, icergh=2, cloud_lut=True, overlap=True,
-                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0, sw_beam=True):
+                 sw=True, lw_after=None, sw_after=None, sw_priority=0, lw_net_cus=None, sw_net_cus=0):
         # sw=False: the LW half alone (config C2, rrtmgp_rfmip_lw.F90): gas optics LW + Planck + rte_lw
-        # sw_beam (fused clear sky): the SW network also forms the SW solver's direct beam
-        # (rrtmgpnn_gas_optics_sw_nn_beam), where the solver takes its small-grid checkpointed kernel
         # lw_after: the SW-chain call the LW chain starts after on two streams (None: the default gate in _finish;
         # "": the chains start together)
         self.dev = torch.device("cuda", device)
@@ -217,15 +215,7 @@ class ClearSkyStep:
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
         g_sw = None if fused else p(self.g_sw)
-        self.sw_beam = bool(fused and sw_beam and not self.allsky)
-        if self.sw_beam:  # the solver call below is the next call on this context: it starts from the handed beam
-            self.calls += [
-                ("predict_nn_sw", L.rrtmgpnn_gas_optics_sw_nn_beam,
-                 (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.play), p(self.tlay), p(self.plev), p(self.gases["h2o"]),
-                  self._g_sw, self._nd_sw, self._nets_sw, p(self.tau_sw), p(self.ssa_sw), g_sw, self.top_at_1,
-                  p(self.toa), p(self.mu0))),
-            ]
-        elif fused:
+        if fused:
             self.calls += [
                 ("predict_nn_sw", L.rrtmgpnn_gas_optics_sw_nn,
                  (c, ncol, nlay, self.ng_sw, self.nx_sw, p(self.play), p(self.tlay), p(self.plev), p(self.gases["h2o"]),
