@@ -142,6 +142,13 @@ def parametric(name):
         return [("kernels_rte.hip", "  extern __shared__ __attribute__((aligned(16))) float smem[];\n  const int icol = blockIdx.x, g = threadIdx.x;\n",
                  "  __shared__ float pad_[%d * 256];\n  if (ngpt == -12345) { pad_[threadIdx.x] = 1.0f; flux_up[0] = pad_[threadIdx.x ^ 1]; }\n"
                  % int(f[1]), "after")]
+    if f[0] == "mlp_lw" and len(f) == 3:  # the fused LW pair's threads per block and waves-per-SIMD floor
+        return [("kernels_nn32.hip", "return launch32<9, 2, 29, 2, 29, 1, 8, 1, 8, 8, MLP_LW_PAIR, true>(ctx, a);",
+                 "return launch32<9, 2, 29, 2, 29, 1, 8, 1, 8, 8, MLP_LW_PAIR, true, %s, %s>(ctx, a);" % tuple(f[1:]),
+                 "replace")]
+    if f[0] == "mlp_unroll" and len(f) == 2:  # output g-tiles per unrolled step (both pairs)
+        return [("kernels_nn32.hip", "#pragma unroll 1\n    for (int go = 0; go < NGT; go++) out_tile(go);",
+                 "#pragma unroll %s\n    for (int go = 0; go < NGT; go++) out_tile(go);" % f[1], "replace")]
     if f[0] == "swck_ahead" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkAheadSmall = %s;" % f[1], r"constexpr int kCkAheadSmall = \d+;")]
     if f[0] == "swck_p1small" and len(f) == 2:
