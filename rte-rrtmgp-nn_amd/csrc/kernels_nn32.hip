@@ -261,8 +261,8 @@ __device__ __forceinline__ void mlp32_hidden(const float *__restrict__ img, cons
 // equal or slower at C3 and C4 (SW network alone, alternating on one box, round 3: 12 waves +29 % at C3; 4 waves
 // +1 %).  Round 5, the LW pair alone: 12-wave blocks (3 waves per SIMD, 168 VGPRs) +27-38 % at C3, 16-wave blocks
 // +13 % at C3 and +23 % at C4 (profiles/r05/ab/lwshape_c{3,4}.txt); one g-tile per step instead of two equal alone
-// and in C3 steps, C4 steps -0.6 % (3 of 3 alternating pairs; the SW network's in-step stage 62 -> 55 us, a smaller
-// kernel; profiles/r05/ab/u1_*.txt).  A/B knob: tools/ablations.py mlp_unroll.
+// and in C3 steps, C4 steps -0.6 % (3 of 3 alternating pairs; the SW network's in-step stage 62 -> 55 us, 29 -> 9 KB of
+// code; profiles/r05/ab/u1_*.txt).  A/B knob: tools/ablations.py mlp_unroll.
 constexpr int kMlp32Threads = 512, kSwNT = 512, kSwWPE = 1;
 
 // A: (KS, AH1, AN2, AH2, AN3), B: (KS, BH1, BN2, BH2, BN3) -- B unused for MLP_LW_BOTH.  The host guarantees that the
