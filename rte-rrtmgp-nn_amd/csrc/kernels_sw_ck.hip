@@ -118,9 +118,6 @@ __device__ __forceinline__ void ck_inc(V &t1, V &w1, V &g1, V t2, V w2, V g2)
 // (C3 flush 18 us from 31 us with one lane per column); flux-ring rows are padded by 4 floats, so the lanes of one
 // partial read different banks
 constexpr bool kCkFlushLanes = true;
-// the passes' chunk walks with one copy of each body (register buffers moved after each chunk) instead of two bodies
-// alternating between the buffers: half the code
-constexpr bool kCkOneBody = false;
 __host__ __device__ constexpr int ck_ring_stride(int ngpt) { return ngpt + 4; }
 
 }  // namespace
@@ -301,22 +298,11 @@ __global__ void __launch_bounds__(512, WAVES)
   // 4: C3 SW solver -0.6 to -2.5 %, C4 -1.1 %, tools/kernel_ab.py).
   auto walk = [&](auto &&load, auto &&body, int count, auto &&idx, auto &A, auto &B) {
     load(A, idx(0));
-    if constexpr (kCkOneBody) {
-      // one copy of the body: the next chunk's loads go to B, and B moves into A after the body (its loads have had
-      // the body's time to arrive)
-#pragma unroll 1
-      for (int i = 0; i < count; i++) {
-        load(B, idx(min(i + 1, count - 1)));
-        body(A, idx(i), true);
-        A = B;
-      }
-    } else {
-      for (int i = 0; i < count; i += 2) {
-        load(B, idx(min(i + 1, count - 1)));
-        body(A, idx(i), true);
-        load(A, idx(min(i + 2, count - 1)));
-        body(B, idx(min(i + 1, count - 1)), i + 1 < count);
-      }
+    for (int i = 0; i < count; i += 2) {
+      load(B, idx(min(i + 1, count - 1)));
+      body(A, idx(i), true);
+      load(A, idx(min(i + 2, count - 1)));
+      body(B, idx(min(i + 1, count - 1)), i + 1 < count);
     }
   };
   // the same walk two chunks ahead through three buffers (same bodies in the same order: same bits)

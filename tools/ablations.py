@@ -149,9 +149,6 @@ def parametric(name):
     if f[0] == "mlp_unroll" and len(f) == 2:  # output g-tiles per unrolled step (both pairs)
         return [("kernels_nn32.hip", "#pragma unroll 1\n    for (int go = 0; go < NGT; go++) out_tile(go);",
                  "#pragma unroll %s\n    for (int go = 0; go < NGT; go++) out_tile(go);" % f[1], "replace")]
-    if f[0] == "swck_onebody" and len(f) == 2:
-        return [("kernels_sw_ck.hip", None, "constexpr bool kCkOneBody = %s;" % ("true" if f[1] == "1" else "false"),
-                 r"constexpr bool kCkOneBody = \w+;")]
     if f[0] == "swck_ahead" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkAheadSmall = %s;" % f[1], r"constexpr int kCkAheadSmall = \d+;")]
     if f[0] == "swck_p1small" and len(f) == 2:
