@@ -176,6 +176,16 @@ def fortran_bench(args):
         "column_layers_per_s": round(1800 * 60 / (ms * 1e-3), 1)}), flush=True)
 
 
+def result_stream():
+    """The stream for the result line alone: the process's fd 1 is pointed at stderr from here on, so whatever a
+    library writes to stdout (gloo's connection notes under a launcher, runtime chatter) cannot mix with the one line
+    the caller parses.  Returns a stream on the original stdout."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     args = parse()
     if args.fortran:
@@ -196,6 +206,7 @@ def main():
     if plan == "spawn":
         sys.exit(shard.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:], torch.cuda.device_count()))
 
+    result = result_stream()  # a rank (or the single process): only its result line reaches stdout
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     # one process per GPU; with more ranks than GPUs (rehearsing the N-rank path on a smaller box) ranks share
@@ -530,7 +541,7 @@ def main():
                                          if os.environ.get("RRTMGPNN_VISIBLE_DEVICES") else "outer launcher"),
                             "world_size": world, "visible_devices": ndev, "backend": backend,
                             "ranks_per_device": -(-world // ndev)}
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result, flush=True)
     if world > 1:
         dist.destroy_process_group()
         if not gather_check["ok"] or (c5g and c5g.get("gather_check") and not c5g["gather_check"]["ok"]):

@@ -200,6 +200,21 @@ def test_spawn_ranks_starts_n_processes(tmp_path, capsys):
     assert "[chatter] rank 0" in cap.err and "[chatter] rank 1" in cap.err
 
 
+def test_bench_result_stream_keeps_stdout_to_the_line():
+    """Under an outer launcher a rank's libraries may write to stdout (gloo's '[Gloo] Rank 0 is connected ...');
+    bench.result_stream() points fd 1 at stderr, so the caller reads only the result line."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path.insert(0, %r); import bench\n"
+            "r = bench.result_stream()\n"
+            "print('[Gloo] chatter', flush=True); os.write(1, b'raw fd write\\n')\n"
+            "r.write('{\"ok\": 1}\\n'); r.flush()\n") % ROOT
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout == '{"ok": 1}\n'
+    assert "[Gloo] chatter" in p.stderr and "raw fd write" in p.stderr
+
+
 def test_synthetic_problem_column_ranges_are_slices_of_the_whole():
     """bench.py builds each rank's shard (and each chunk of it) as a column range of one global synthetic problem:
     a range generated alone must equal the same columns of the whole, at 60 and 137 layers."""
