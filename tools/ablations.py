@@ -149,6 +149,18 @@ def parametric(name):
     if f[0] == "mlp_unroll" and len(f) == 2:  # output g-tiles per unrolled step (both pairs)
         return [("kernels_nn32.hip", "#pragma unroll 1\n    for (int go = 0; go < NGT; go++) out_tile(go);",
                  "#pragma unroll %s\n    for (int go = 0; go < NGT; go++) out_tile(go);" % f[1], "replace")]
+    if f[0] == "flush_unroll" and len(f) == 3:  # the ordered flushes' loads in flight: LW (ring_flush_lanes), SW
+        return [("rte_device.hpp", "#pragma unroll 8\n    for (int m = 0; m < n4; m++) sum = sum + r[4 * m];\n    part[",
+                 "#pragma unroll %s\n    for (int m = 0; m < n4; m++) sum = sum + r[4 * m];\n    part[" % f[1], "replace"),
+                ("rte_device.hpp", """#pragma unroll 8
+      for (int m = 0; m < n4; m++) sum = (sum + r[4 * m]) + r2[4 * m];
+    } else {
+#pragma unroll 8
+      for (int m = 0; m < n4; m++) sum = sum + r[4 * m];""", """#pragma unroll %s
+      for (int m = 0; m < n4; m++) sum = (sum + r[4 * m]) + r2[4 * m];
+    } else {
+#pragma unroll %s
+      for (int m = 0; m < n4; m++) sum = sum + r[4 * m];""" % (f[2], f[2]), "replace")]
     if f[0] == "swck_ahead" and len(f) == 2:
         return [("kernels_sw_ck.hip", None, "constexpr int kCkAheadSmall = %s;" % f[1], r"constexpr int kCkAheadSmall = \d+;")]
     if f[0] == "swck_p1small" and len(f) == 2:
