@@ -228,11 +228,16 @@ __device__ __forceinline__ void ring_flush_sw_lanes(const float *ring, int ncb, 
   const int t = threadIdx.x;
   const int per_q = ncb * n * 4;  // lanes per quantity
   if (t < 3 * per_q) {  // idle lanes of the last wave walk nothing (the branch is per lane only in that wave)
-    const int q = t / per_q, rem = t - q * per_q, row = rem >> 2, j = rem & 3;
-    const int c = row / n, sl = row - c * n;
-    const float *rc = ring + (size_t)c * 3 * R * stride;
-    const float *r = rc + ((size_t)q * R + slot0 + sl) * stride + j;
-    const float *r2 = rc + ((size_t)2 * R + slot0 + sl) * stride + j;
+    // the lane's (quantity, column, slot, partial) by comparisons and 24-bit products: integer division by the
+    // runtime per_q and n took ~40 dependent VALU ops (quarter-rate multiplies among them) before every flush
+    const int q = (t >= per_q) + (t >= 2 * per_q);  // three quantities
+    const int rem = t - (int)__umul24((unsigned)q, (unsigned)per_q), row = rem >> 2, j = rem & 3;
+    const int c = (ncb > 1 && row >= n) + (ncb > 2 && row >= 2 * n) + (ncb > 3 && row >= 3 * n);  // ncb <= 4
+    const int sl = row - (int)__umul24((unsigned)c, (unsigned)n);
+    // LDS offsets (well under 2^24 floats)
+    const int rc = (int)__umul24((unsigned)c, (unsigned)(3 * R * stride)) + j;
+    const float *r = ring + rc + (int)__umul24((unsigned)(q * R + slot0 + sl), (unsigned)stride);
+    const float *r2 = ring + rc + (int)__umul24((unsigned)(2 * R + slot0 + sl), (unsigned)stride);
     const int n4 = ngpt >> 2;
     float sum = 0.0f;
     if (q == 1 && !kTotal) {
@@ -247,7 +252,7 @@ __device__ __forceinline__ void ring_flush_sw_lanes(const float *ring, int ncb, 
     const int icol = icol0 + c;
     if (j == 0 && icol < ncol) {
       float *o = q == 0 ? o_up : (q == 1 ? o_dn : o_dir);
-      o[lev0 + sl * dl + (size_t)nlev * icol] = ((sum + p1) + p2) + p3;
+      o[lev0 + (dl > 0 ? sl : -sl) + (size_t)nlev * icol] = ((sum + p1) + p2) + p3;  // dl = +-1
     }
   }
   __syncthreads();
