@@ -285,6 +285,9 @@ def main():
     step = rank_run.step
     prob, clouds = rank_run.first
     ncol, nlay = step.ncol, step.nlay
+    # everything below runs on the step's own stream (its graph replays, the chunk copies, the host-resident copies),
+    # not on the legacy null stream
+    torch.cuda.set_stream(step.ctx.stream)
     run_one = step.replay if use_graph else step.step
     run = rank_run.run
 
@@ -487,6 +490,27 @@ def main():
         end_to_end = {"value": round(total_cols / (elapsed + gather_ms * 1e-3), 1), "unit": "columns/s",
                       "note": "all ranks' columns over the timed steps plus one final flux all-gather"}
 
+    config = {"workload": workload, "global_columns": global_cols, "ncol_per_gpu": hi - lo,
+              "chunk_columns": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
+              "ngpt_sw": step.ng_sw if step.sw else None,
+              "parallelism": "column-sharded (shard.column_range), 1 process per GPU",
+              "launch": ("hipGraph replay" if use_graph else "eager") +
+                        (", LW and SW chains on two streams" if step.overlap else "") +
+                        (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
+                        (" (LW network on %d CUs)" % step.lw_net_cus if step.lw_net_cus else "") +
+                        (", the SW solver after %s" % step.sw_after if step.sw_after else "") +
+                        (", SW stream priority %d" % step.sw_priority if step.sw_priority else ""),
+              "kernels": ("class-layer sequence" if not step.fused else
+                          "fused Planck-in-LW-solver, g=0 elided" +
+                          (", cloud increments fused into both solvers" if step.allsky else ""))}
+    step_sw = step.sw
+    # the main line's steps, workspaces and chunk inputs are released before c5_global allocates its own (at C5 each
+    # holds ~116 GB of the device's 288: both at once can exceed HBM)
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    rank_run.close()
+    del rank_run, step, ins, outs, h_ins, h_outs, run, run_one
+    torch.cuda.empty_cache()
+
     # ---- BASELINE configs[4] as stated: 1e6 x 137 columns over the ranks (strong scaling), in every line ----
     c5g = None
     if args.config == "c5" and scaling == "strong" and global_cols == C5_GLOBAL_COLS:
@@ -498,7 +522,7 @@ def main():
     # ---- CPU baseline: C restatement (oracle, bit-identical to the reference's RTE/MLP) on host cores ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(prob, clouds, args.cpu_seconds, args.cpu_kind, sw=step.sw, bind=args.cpu_bind)
+        cpu = cpu_baseline(prob, clouds, args.cpu_seconds, args.cpu_kind, sw=step_sw, bind=args.cpu_bind)
 
     if rank == 0:
         out = {
@@ -511,19 +535,7 @@ def main():
                                 round(total_cols / elapsed_unsettled, 1)),
             "higher_is_better": True,
             "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data_desc,
-            "config": {"workload": workload, "global_columns": global_cols, "ncol_per_gpu": hi - lo,
-                       "chunk_columns": ncol, "nlay": nlay, "ngpt_lw": step.ng_lw,
-                       "ngpt_sw": step.ng_sw if step.sw else None,
-                       "parallelism": "column-sharded (shard.column_range), 1 process per GPU",
-                       "launch": ("hipGraph replay" if use_graph else "eager") +
-                                 (", LW and SW chains on two streams" if step.overlap else "") +
-                                 (", the LW chain after %s" % step.lw_after if step.lw_after else "") +
-                                 (" (LW network on %d CUs)" % step.lw_net_cus if step.lw_net_cus else "") +
-                                 (", the SW solver after %s" % step.sw_after if step.sw_after else "") +
-                                 (", SW stream priority %d" % step.sw_priority if step.sw_priority else ""),
-                       "kernels": ("class-layer sequence" if not step.fused else
-                                   "fused Planck-in-LW-solver, g=0 elided" +
-                                   (", cloud increments fused into both solvers" if step.allsky else ""))},
+            "config": config,
             "column_layers_per_s": round(value * nlay, 1),
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -571,7 +583,7 @@ def c5_global(args, world, rank, dev):
     lo, hi = shard.column_range(G, rank, world)
     torch.cuda.synchronize(dev)
     free0 = torch.cuda.mem_get_info(dev)[0]
-    chunks = [(c, min(c + CH, hi)) for c in range(lo, hi, CH)]
+    chunks = shard.chunk_ranges(lo, hi, CH)
     t0 = time.perf_counter()
     with ThreadPoolExecutor(max(1, min(8, len(chunks)))) as ex:
         futs = {c: ex.submit(data.synthetic_problem, c[1] - c[0], NL, seed=20251015, col0=c[0]) for c in chunks}
@@ -579,6 +591,7 @@ def c5_global(args, world, rank, dev):
                          lambda p, c: ClearSkyStep(p, device=dev.index), use_graph=not args.no_graph)
     rr.first = None  # the first chunk's host arrays are not needed here
     setup_s = time.perf_counter() - t0
+    torch.cuda.set_stream(rr.step.ctx.stream)
     for _ in range(args.c5_warmup):
         rr.run()
     torch.cuda.synchronize(dev)
@@ -640,6 +653,8 @@ def c5_global(args, world, rank, dev):
                                        "resident inputs); plus the flux slab and, at N > 1, the gathered array"},
            "data": "synthetic columns interpolated from RFMIP profiles (PCG64 streams seeded by (20251015, column "
                    "block)), generated per chunk on host threads (setup_s, outside the timed region)"}
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    rr.close()
     del rr, slab
     torch.cuda.empty_cache()
     return res

@@ -376,6 +376,14 @@ int rrtmgpnn_compute_heating_rate(rrtmgpnn_context *ctx, int ncol, int nlay, con
  * Same layouts as rrtmgpnn_compute_heating_rate. */
 int rrtmgpnn_calc_heating_rate_k_day(rrtmgpnn_context *ctx, int ncol, int nlay, const float *flux_up,
                                      const float *flux_dn, const float *plev, float *hr_k_day);
+/* The RFMIP SW driver's per-block boundary conditions (examples/rfmip-clear-sky/rrtmgp_rfmip_sw.F90:403-434), with
+ * gas_optics_ext's toa_src(igpt, icol) = solar_source(igpt) (rrtmgp/mo_gas_optics_rrtmgp.F90:594-599): per column
+ * def_tsi = sum over g of toa_src in g order, toa_flux = toa_src * tsi / def_tsi, sfc_alb_gpt(g, icol) = sfc_alb(icol),
+ * mu0 = merge(cos(sza * deg_to_rad), 1, usecol), usecol = sza < 90 - 2 spacing(90) (:236-238), cos with glibc's cosf
+ * algorithm (the reference built here links it).  solar_source DEVICE (ngpt) after set_tsi; tsi, sfc_alb, sza DEVICE
+ * (ncol); outputs DEVICE toa_flux and sfc_alb_gpt (ngpt, ncol), mu0 (ncol). */
+int rrtmgpnn_sw_boundary_rfmip(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
+                               const float *sfc_alb, const float *sza, float *toa_flux, float *sfc_alb_gpt, float *mu0);
 /* ty_optical_props_2str%delta_scale([for]) (rte/mo_optical_props.F90:576-604; kernels
  * rte/kernels/mo_optical_props_kernels.F90:41-92) on n values in place.  fwd == NULL: f = g**2. */
 int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);

@@ -1095,6 +1095,15 @@ int rrtmgpnn_calc_heating_rate_k_day(rrtmgpnn_context *ctx, int ncol, int nlay, 
   return launch_heating_rate(ctx, ncol, nlay, 1, scaling, 0.0f, flux_up, flux_dn, plev, hr_k_day);
 }
 
+int rrtmgpnn_sw_boundary_rfmip(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
+                               const float *sfc_alb, const float *sza, float *toa_flux, float *sfc_alb_gpt, float *mu0)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (ngpt < 1 || ncol < 0 || !solar_source || !tsi || !sfc_alb || !sza || !toa_flux || !sfc_alb_gpt || !mu0)
+    return fail(RRTMGPNN_ERR_ARGUMENT, "sw_boundary_rfmip: bad argument");
+  return launch_sw_boundary(ctx, ngpt, ncol, solar_source, tsi, sfc_alb, sza, toa_flux, sfc_alb_gpt, mu0);
+}
+
 // ---- data files: RBIN, classic netCDF, netCDF-4 (datafile.cpp) ----
 struct rrtmgpnn_file {
   DataFile df;

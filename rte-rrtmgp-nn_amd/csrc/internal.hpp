@@ -146,6 +146,8 @@ int launch_increment_bybnd(rrtmgpnn_context *ctx, int ncol, int nlay, int ngpt, 
                            float *ssa1, float *g1, const float *tau2, const float *ssa2, const float *g2);
 int launch_heating_rate(rrtmgpnn_context *ctx, int ncol, int nlay, int k_day, float c0, float c1, const float *up,
                         const float *dn, const float *plev, float *hr);
+int launch_sw_boundary(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
+                       const float *sfc_alb, const float *sza, float *toa, float *alb, float *mu0);
 int launch_delta_scale(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);
 // kernels_nn.hip
 struct GasArgs {
@@ -214,12 +216,13 @@ int launch_sw_noscat(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int to
 // kernels_sw_ck.hip (checkpointed passes; called by launch_sw_2stream for even ngpt in mode 3)
 // the checkpointed SW kernel's small-grid instance applies (clear sky, g = 0, no g-point outputs, the grid in one round)
 bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bool inc, bool gpt);
-size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn);
+// planes: the large-grid instances' workspace planes (kCkTnNN, kCkTnInc, ...); false after that allocation failed
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn, bool planes = true);
 int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
-                         float *flux_dn, float *flux_dir);
+                         float *flux_dn, float *flux_dir, bool planes = true);
 // kernels_lw_scat.hip
 int launch_lw_rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
                     const float *wts, const float *inc_flux, const float *tau, const float *ssa, const float *g,

@@ -1,4 +1,14 @@
-// kernels_fluxes.hip -- post-processing of the broadband fluxes.
+// kernels_fluxes.hip -- the RFMIP driver's per-block SW boundary conditions and the post-processing of the broadband
+// fluxes.
+//
+//  * sw_boundary_kernel  : the per-block work of examples/rfmip-clear-sky/rrtmgp_rfmip_sw.F90 between gas_optics and
+//                          rte_sw (:403-434), with gas_optics_ext's toa_src(igpt, icol) = solar_source(igpt)
+//                          (rrtmgp/mo_gas_optics_rrtmgp.F90:594-599) in front of it: per column def_tsi = the sum of
+//                          toa_src over g-points in g order, toa = toa_src * tsi / def_tsi, the spectrally constant
+//                          surface albedo expanded to every g-point, mu0 = merge(cos(sza * deg_to_rad), 1, usecol)
+//                          with usecol = sza < 90 - 2 spacing(90) (rrtmgp_rfmip_sw.F90:236-238) and glibc's cosf
+//                          (libm_ref.hpp ref_cosf).  A block holds kBcCols columns: one lane per column forms its sum
+//                          (the reference's sequential order), then the block writes the (ngpt, kBcCols) slabs.
 //
 //  * heating_rate_kernel : layer heating rates from the level fluxes and pressures, in the fork's (nlay+1, ncol)
 //                          level-fastest flux layout.  Two forms, both term by term:
@@ -11,8 +21,51 @@
 // Elementwise and HBM-bound: one thread per (layer, column), layer fastest, so a wave reads 65 contiguous levels of
 // each array and writes 64 contiguous layers.  -ffp-contract=off keeps the reference's roundings.
 #include "internal.hpp"
+#include "libm_ref.hpp"
 
 namespace rrtmgpnn {
+
+constexpr int kBcCols = 8;
+
+__global__ void __launch_bounds__(256) sw_boundary_kernel(int ngpt, int ncol, const float *__restrict__ solar_source,
+                                                          const float *__restrict__ tsi,
+                                                          const float *__restrict__ sfc_alb,
+                                                          const float *__restrict__ sza, float deg_to_rad,
+                                                          float sza_max, float *__restrict__ toa,
+                                                          float *__restrict__ alb, float *__restrict__ mu0)
+{
+  __shared__ float def_tsi[kBcCols];
+  const int c0 = blockIdx.x * kBcCols, t = threadIdx.x;
+  if (t < kBcCols && c0 + t < ncol) {
+    float s = 0.0f;  // def_tsi_s = def_tsi_s + toa_flux(igpt, icol), igpt = 1..ngpt
+    for (int g = 0; g < ngpt; g++) s = s + solar_source[g];
+    def_tsi[t] = s;
+    const float z = sza[c0 + t];
+    mu0[c0 + t] = z < sza_max ? ref_cosf(z * deg_to_rad) : 1.0f;
+  }
+  __syncthreads();
+  const int nc = min(kBcCols, ncol - c0);
+  for (int i = t; i < nc * ngpt; i += blockDim.x) {
+    const int c = i / ngpt, g = i - c * ngpt;
+    const size_t k = (size_t)(c0 + c) * ngpt + g;
+    toa[k] = solar_source[g] * tsi[c0 + c] / def_tsi[c];
+    alb[k] = sfc_alb[c0 + c];
+  }
+}
+
+int launch_sw_boundary(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
+                       const float *sfc_alb, const float *sza, float *toa, float *alb, float *mu0)
+{
+  if (ncol == 0) return RRTMGPNN_OK;
+  // deg_to_rad = acos(-1._wp) / 180._wp in working precision (rrtmgp_rfmip_sw.F90:106); the usecol bound
+  // 90 - 2 spacing(90) = 90 - 2^-16 (spacing(90.) = 2^-17 in fp32)
+  volatile float pi = 3.14159265358979323846f;
+  const float deg_to_rad = pi / 180.0f, sza_max = 90.0f - 2.0f * 0x1p-17f;
+  hipLaunchKernelGGL(sw_boundary_kernel, dim3((unsigned)((ncol + kBcCols - 1) / kBcCols)), dim3(256), 0, ctx->stream,
+                     ngpt, ncol, solar_source, tsi, sfc_alb, sza, deg_to_rad, sza_max, toa, alb, mu0);
+  RRTMGPNN_LAUNCH_CHECK("sw_boundary_kernel");
+  return RRTMGPNN_OK;
+}
 
 template <bool kDay>
 __global__ void __launch_bounds__(256) heating_rate_kernel(long long n, int nlay, float c0, float c1,

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 
 namespace rrtmgpnn {
 
@@ -743,14 +744,28 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   const bool x2 = !ck && (ngpt % 2) == 0 && mode != 1;
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc ? 3 : 0);
-  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), inc,
-                                                     !g && !inc && !gpt)
+  const bool small = ck && sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), nn = !g && !inc && !gpt;
+  const size_t nws = ck ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, small, inc, nn)
                         : 4 * (size_t)ngpt * (nlay + 1) * ncol + nlp * (size_t)ngpt * nlay * ncol;
-  int rc = ctx->workspace(sizeof(float) * nws, &ws);
+  // RRTMGPNN_SW_NO_PLANES=1 (read once per process): take the fallback below from the start (tests/test_gpu_sw_planes.py)
+  static const bool no_planes = [] {
+    const char *e = std::getenv("RRTMGPNN_SW_NO_PLANES");
+    return e && e[0] == '1';
+  }();
+  const size_t nws0 = ck && !small ? sw_2stream_ck_ws_floats(ngpt, nlay, ncol, false, inc, nn, false) : nws;
+  int rc = no_planes && nws0 < nws ? RRTMGPNN_ERR_DEVICE : ctx->workspace(sizeof(float) * nws, &ws);
+  bool planes = true;
+  if (rc == RRTMGPNN_ERR_DEVICE && nws0 < nws && !ctx->ws_pinned) {
+    // the large-grid instances' workspace planes (up to 3x the checkpoints) did not fit: the instances without them
+    // give the same bits in the workspace a call needed before round 5
+    (void)hipGetLastError();
+    planes = false;
+    rc = ctx->workspace(sizeof(float) * nws0, &ws);
+  }
   if (rc) return rc;
   if (ck)
     return launch_sw_2stream_ck(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
-                                alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);
+                                alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir, planes);
   if (x2)
     return launch_sw_2stream_x2(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
                                 alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);

@@ -141,7 +141,9 @@ constexpr int kCkWavesNN = 3;
 // alone 33.23: with both, pass 3 reads no tau), whole steps 66.63 -> 64.77 ms (2 alternating pairs); the large grid is
 // then at HBM (199 GB per launch at 6.3 TB/s) where it was at its VALU floor (valu_busy 0.99, 3.35 TB/s).  C4 all sky:
 // the transmittance plane 1.480 -> 1.458 ms alone (1.50 -> 1.435 in steps), steps within noise (-0.5 %); exp(-k tau)
-// +1.3 %.  A/B knobs: tools/ablations.py swck_nnplanes / swck_incplanes.
+// +1.3 %.  A/B knobs: tools/ablations.py swck_nnplanes / swck_incplanes.  The planes cost workspace (C5 shard: 15.7 ->
+// 46.4 GB): when that allocation fails, launch_sw_2stream retries without them and these instances run without planes
+// (the round-4 forms; same bits).
 constexpr bool kCkTnNN = true, kCkEmkNN = true;
 constexpr bool kCkTnInc = true, kCkEmkInc = false;
 
@@ -155,7 +157,8 @@ constexpr bool kCkTnInc = true, kCkEmkInc = false;
 // 3 read instead of evaluating the exp again, and pass 2's exp(-tau k) in a second plane that pass 3 reads (C3: SW
 // solver -3.7 %, step -3.7 %, alternating A/B on one box).  One g-point per lane (twice the waves to hide latency with;
 // packed fp32 issues at the same cost per element as scalar fp32 on gfx950, tools/valu_rates.hip) measured slower than
-// two, and so did the transmittance plane in the all-sky (fused-increment) instances.
+// two.  (The transmittance plane in the all-sky instances measured slower in round 3; on the round-4 kernels it was
+// faster at C4 and is on there since round 5: kCkTnInc above.)
 // Round 4 (alone, alternating, bitwise; with the fence-free walk): K = 3 with a ring of 9 levels (three chunks per
 // flush, 7 flushes per column instead of 8) -2.3 % against K = 4 / ring 8; K = 3 / ring 6 +3 %, K = 2 / ring 6 +5 %,
 // K = 5 / ring 10 equal; a 3-wave floor equal.  A ring of 12 levels would not leave room for three blocks per CU.
@@ -520,12 +523,13 @@ bool sw_ck_small(const rrtmgpnn_context *ctx, int ngpt, int ncol, bool has_g, bo
 // workspace floats of the checkpointed kernel (sized for the smaller of the chunk lengths, so it holds either
 // instance) plus the planes of the instance that runs: small-grid clear sky, large-grid clear sky (NN: g = NULL, no
 // increment, no g-point outputs) or all sky (inc)
-size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn)
+size_t sw_2stream_ck_ws_floats(int ngpt, int nlay, int ncol, bool small, bool inc, bool nn, bool planes)
 {
-  const int np = small ? (int)kCkTnSmall + (int)kCkEmkSmall
-                 : nn  ? (int)kCkTnNN + (int)kCkEmkNN
-                 : inc ? (int)kCkTnInc + (int)kCkEmkInc
-                       : 0;
+  const int np = small  ? (int)kCkTnSmall + (int)kCkEmkSmall
+                 : !planes ? 0
+                 : nn     ? (int)kCkTnNN + (int)kCkEmkNN
+                 : inc    ? (int)kCkTnInc + (int)kCkEmkInc
+                          : 0;
   const size_t tn = (size_t)np * ngpt * nlay * ncol;
   const int k = std::min(kCkK, kCkKSmall);
   const size_t nck = (size_t)(nlay + k - 1) / k;
@@ -537,7 +541,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
-                         float *flux_dn, float *flux_dir)
+                         float *flux_dn, float *flux_dir, bool planes)
 {
   const int ncb2 = 2 * (ngpt / 2) <= 512 ? 2 : 1;  // two columns per block where 512 lanes hold them
   const BandArgs nob{};
@@ -546,6 +550,8 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
   // npl g-points per lane, ncb columns per block
   auto go = [&](auto kern, const float *tb, const float *sb, const float *gb, int ring = kCkRing, int npl = 2) -> int {
     const int ncb = npl == 2 ? ncb2 : columns_per_block(ngpt);
+    if (ncb > kFlushLanesMaxCols)  // the flush's lane -> column map (ring_flush_sw_lanes) covers at most 4 columns
+      return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: more columns per block than the ordered flush maps");
     const int threads = (ncb * (ngpt / npl) + 63) / 64 * 64;
     const dim3 grid((ncol + ncb - 1) / ncb), block(threads);
     const size_t lds = sizeof(float) * (kExpTabFloats + (size_t)ncb * 3 * ring * ck_ring_stride(ngpt) + 4);  // + spare
@@ -570,6 +576,16 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     for (int i = 0; i < b.nbnd; i++) pair = pair && ((b.lims[2 * i] - 1) % 2 == 0);
     constexpr int W = kCkWaves;
     constexpr bool T = kCkTnInc, E = kCkEmkInc;
+    if (!planes) {  // the workspace planes did not fit (launch_sw_2stream's fallback): the same bits, recomputed
+      if (pair && g)
+        return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W, false, f2, false, true>, tau_bnd, ssa_bnd,
+                  g_bnd);
+      if (pair)
+        return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, W, false, f2, false, true>, tau_bnd, ssa_bnd,
+                  g_bnd);
+      if (g) return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W>, tau_bnd, ssa_bnd, g_bnd);
+      return go(sw_2stream_ck_kernel<false, true, kCkK, false, kCkRing, W>, tau_bnd, ssa_bnd, g_bnd);
+    }
     if (pair && g)
       return go(sw_2stream_ck_kernel<true, true, kCkK, false, kCkRing, W, T, f2, E, true>, tau_bnd, ssa_bnd, g_bnd);
     if (pair)
@@ -584,6 +600,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
     return go(sw_2stream_ck_kernel<false, false, kCkKSmall, false, kCkRingSmall, kCkWavesSmall, kCkTnSmall, VSmall,
                                    kCkEmkSmall, false, kCkP1Small, kCkAheadSmall>,
               nullptr, nullptr, nullptr, kCkRingSmall, (int)(sizeof(VSmall) / sizeof(float)));
+  if (!planes) return go(sw_2stream_ck_kernel<false, false, kCkK, false, kCkRing, kCkWavesNN>, nullptr, nullptr, nullptr);
   return go(sw_2stream_ck_kernel<false, false, kCkK, false, kCkRing, kCkWavesNN, kCkTnNN, f2, kCkEmkNN>, nullptr,
             nullptr, nullptr);
 }

@@ -57,6 +57,43 @@ __device__ __forceinline__ float ref_expf_tab(float x, const uint64_t *tab)
 
 __device__ __forceinline__ float ref_expf(float x) { return ref_expf_tab(x, kExpTab); }
 
+// glibc 2.35 cosf (sysdeps/ieee754/flt-32/s_cosf.c with s_sincosf_data.c's table: a pi/2 reduction and double
+// polynomials, rounded once), for |y| < 120 -- the SW boundary's mu0 = cos(sza * deg_to_rad) (rrtmgp_rfmip_sw.F90:431-434;
+// zenith angles of [0, 180] degrees).  tools/check_libm_ref_cosf.c checks the restatement against the host's cosf on
+// every float of [-4, 4] (both of glibc's builds, with and without FMA contraction, give the same bits there).
+__device__ __forceinline__ float ref_cosf(float y)
+{
+  // {c0, c1, c2, c3, c4} of the cosine polynomial, and of its negation for quadrants 2 and 3; s1..s3 of the sine
+  constexpr double c[2][5] = {{0x1p0, -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10,
+                               0x1.99343027bf8c3p-16},
+                              {-0x1p0, 0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10,
+                               -0x1.99343027bf8c3p-16}};
+  constexpr double s1 = -0x1.555545995a603p-3, s2 = 0x1.1107605230bc4p-7, s3 = -0x1.994eb3774cf24p-13;
+  constexpr double hpi_inv = 0x1.45F306DC9C883p+23, hpi = 0x1.921FB54442D18p0;
+  const uint32_t top = (__float_as_uint(y) >> 20) & 0x7ff;
+  double x = (double)y;
+  int n = 0, q = 0;
+  if (top < ((0x3f490fdbu >> 20) & 0x7ff)) {  // |y| < pi/4
+    if (top < ((0x39800000u >> 20) & 0x7ff)) return 1.0f;  // |y| < 2^-12
+    n = 1;
+  } else {
+    const double r = x * hpi_inv;
+    q = ((int32_t)r + 0x800000) >> 24;
+    x = __fma_rn(-(double)q, hpi, x);
+    x = (q & 1) == (q & 2) / 2 ? x : -x;  // sign[q & 3] = {1, -1, -1, 1}
+    n = q ^ 1;
+  }
+  const double x2 = x * x;
+  const int t = (q & 2) ? 1 : 0;
+  if ((n & 1) == 0) {
+    const double x3 = x * x2, sa = __fma_rn(x2, s3, s2), x5 = x3 * x2, s = __fma_rn(x3, s1, x);
+    return (float)__fma_rn(x5, sa, s);
+  }
+  const double x4 = x2 * x2, c2 = __fma_rn(x2, c[t][4], c[t][3]), c1 = __fma_rn(x2, c[t][1], c[t][0]), x6 = x4 * x2;
+  const double cc = __fma_rn(x4, c[t][2], c1);
+  return (float)__fma_rn(x6, c2, cc);
+}
+
 // Branch-free form for the solvers' inner loops: the main path is evaluated for every x and glibc's
 // over/underflow cases are applied by selection afterwards (x < -0x1.9fe368p6: 0, including -inf;
 // x > 0x1.62e42ep6: +inf).  A nan propagates through the main path (glibc returns x + x: also a nan).

@@ -219,6 +219,10 @@ __device__ __forceinline__ void ring_flush_sw(const float *ring, int ncb, int n,
 // are ordered quantity-major, so with 64 lanes per (quantity) group a wave walks one quantity only: the down sums (two
 // adds per step) and the others do not share a wave's instruction stream.  Same partials, same additions, same order,
 // same bits as ring_flush_sw; about a quarter of its instructions on the critical wave.
+// ring_flush_sw_lanes maps a lane's row to its column with three comparisons: at most this many columns per block
+// (the SW launchers refuse more before launching)
+constexpr int kFlushLanesMaxCols = 4;
+
 template <int R, bool kTotal = false>
 __device__ __forceinline__ void ring_flush_sw_lanes(const float *ring, int ncb, int n, int lev0, int dl, int ngpt,
                                                     int nlev, int icol0, int ncol, float *o_up, float *o_dn,
@@ -232,7 +236,7 @@ __device__ __forceinline__ void ring_flush_sw_lanes(const float *ring, int ncb, 
     // runtime per_q and n took ~40 dependent VALU ops (quarter-rate multiplies among them) before every flush
     const int q = (t >= per_q) + (t >= 2 * per_q);  // three quantities
     const int rem = t - (int)__umul24((unsigned)q, (unsigned)per_q), row = rem >> 2, j = rem & 3;
-    const int c = (ncb > 1 && row >= n) + (ncb > 2 && row >= 2 * n) + (ncb > 3 && row >= 3 * n);  // ncb <= 4
+    const int c = (ncb > 1 && row >= n) + (ncb > 2 && row >= 2 * n) + (ncb > 3 && row >= 3 * n);  // ncb <= kFlushLanesMaxCols
     const int sl = row - (int)__umul24((unsigned)c, (unsigned)n);
     // LDS offsets (well under 2^24 floats)
     const int rc = (int)__umul24((unsigned)c, (unsigned)(3 * R * stride)) + j;

@@ -109,6 +109,7 @@ SIGNATURES = {
                                          c_vp]),
     "rrtmgpnn_increment": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_delta_scale_2str": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_sw_boundary_rfmip": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_file_open": (c_int, [c_char_p, P(c_vp)]),
     "rrtmgpnn_file_close": (c_int, [c_vp]),
     "rrtmgpnn_file_nvars": (c_int, [c_vp, P(c_int)]),
@@ -145,6 +146,40 @@ def lib():
             f.argtypes = args
         _lib = h
     return _lib
+
+
+_hip = None
+
+
+def _hip_runtime():
+    """The process's HIP runtime (torch's libamdhip64.so.7, which librrtmgpnn.so also binds by soname)."""
+    global _hip
+    if _hip is None:
+        h = ctypes.CDLL("libamdhip64.so.7")
+        h.hipStreamCreateWithPriority.restype = c_int
+        h.hipStreamCreateWithPriority.argtypes = [P(c_vp), ctypes.c_uint, c_int]
+        h.hipStreamDestroy.restype = c_int
+        h.hipStreamDestroy.argtypes = [c_vp]
+        h.hipSetDevice.restype = c_int
+        h.hipSetDevice.argtypes = [c_int]
+        _hip = h
+    return _hip
+
+
+def stream_create(device, priority=0):
+    """A non-blocking HIP stream of the caller's own (not one of torch's pooled streams, which other objects are
+    handed round-robin): the raw handle; free it with stream_destroy once nothing uses it."""
+    h = _hip_runtime()
+    s = c_vp()
+    rc = h.hipSetDevice(int(device)) or h.hipStreamCreateWithPriority(ctypes.byref(s), 1, int(priority))
+    if rc:
+        raise RrtmgpnnError("hipStreamCreateWithPriority failed (hip error %d)" % rc)
+    return s.value
+
+
+def stream_destroy(handle):
+    if handle:
+        _hip_runtime().hipStreamDestroy(handle)
 
 
 def check(rc, what=""):

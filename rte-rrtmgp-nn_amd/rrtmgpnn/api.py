@@ -79,10 +79,15 @@ class Context:
         """0: the gas-optics networks on 32x32x2 MFMA tiles where instantiated (default); 1: 16x16x4 (bit-identical)."""
         check(_lib.lib().rrtmgpnn_context_set_mlp_kernel(self.h, int(mode)), "context_set_mlp_kernel")
 
+    def close(self):
+        """Destroy the context now (its workspace and buffer pool); the handle is unusable afterwards."""
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            _lib.lib().rrtmgpnn_context_destroy(h)
+
     def __del__(self):
         try:
-            if getattr(self, "h", None):
-                _lib.lib().rrtmgpnn_context_destroy(self.h)
+            self.close()
         except Exception:
             pass
 

@@ -90,6 +90,44 @@ def seqsum(a, axis=-1):
     return np.take(np.cumsum(np.asarray(a, np.float32), axis=axis, dtype=np.float32), -1, axis=axis)
 
 
+_fh = float.fromhex
+# s_sincosf_data.c: the cosine polynomial (and its negation, quadrants 2-3), the sine polynomial, 2/pi * 2^24 and pi/2
+_COSF_C = (tuple(map(_fh, ("0x1p0", "-0x1.ffffffd0c621cp-2", "0x1.55553e1068f19p-5", "-0x1.6c087e89a359dp-10",
+                           "0x1.99343027bf8c3p-16"))),
+           tuple(map(_fh, ("-0x1p0", "0x1.ffffffd0c621cp-2", "-0x1.55553e1068f19p-5", "0x1.6c087e89a359dp-10",
+                           "-0x1.99343027bf8c3p-16"))))
+_COSF_S = tuple(map(_fh, ("-0x1.555545995a603p-3", "0x1.1107605230bc4p-7", "-0x1.994eb3774cf24p-13")))
+_COSF_HPI_INV, _COSF_HPI = _fh("0x1.45F306DC9C883p+23"), _fh("0x1.921FB54442D18p0")
+
+
+def ref_cosf(y):
+    """cosf as glibc 2.35 evaluates it (sysdeps/ieee754/flt-32/s_cosf.c: a pi/2 reduction and double polynomials,
+    rounded once), elementwise for |y| < 120 -- what the reference's driver gets from cos() in working precision when
+    built against glibc, as here (rrtmgp_rfmip_sw.F90:431-434).  numpy's own float32 cos rounds differently on a
+    quarter of the RFMIP zenith angles.  The device's copy is csrc/libm_ref.hpp ref_cosf; both are checked against
+    the host's cosf (tools/check_libm_ref_cosf.c on every float of [-4, 4], tests/test_host.py)."""
+    y = np.asarray(y, np.float32)
+    if np.any(np.abs(y) >= np.float32(120.0)):
+        raise ValueError("ref_cosf: |y| >= 120 is outside the restated path")
+    top = (y.view(np.uint32) >> np.uint32(20)) & np.uint32(0x7FF)
+    x = y.astype(np.float64)
+    small = top < ((0x3F490FDB >> 20) & 0x7FF)  # |y| < pi/4: no reduction, the cosine polynomial
+    q = np.where(small, 0, ((x * _COSF_HPI_INV).astype(np.int32) + 0x800000) >> 24)
+    xr = np.where(small, x, x - q * _COSF_HPI)
+    xr = np.where(small | ((q & 1) == (q & 2) // 2), xr, -xr)  # sign[q & 3] = 1, -1, -1, 1
+    n = np.where(small, 1, q ^ 1)
+    x2 = xr * xr
+    t = (q & 2) != 0
+    c = [np.where(t, _COSF_C[1][k], _COSF_C[0][k]) for k in range(5)]
+    x4 = x2 * x2
+    # sinf_poly, in its order: c = (c0 + x2 c1) + x4 c2, then c + x6 (c3 + x2 c4); s = (x + x3 s1) + x5 (s2 + x2 s3)
+    cosp = ((c[0] + x2 * c[1]) + x4 * c[2]) + (x4 * x2) * (c[3] + x2 * c[4])
+    x3 = xr * x2
+    sinp = (xr + x3 * _COSF_S[0]) + (x3 * x2) * (_COSF_S[1] + x2 * _COSF_S[2])
+    out = np.where((n & 1) == 0, sinp, cosp).astype(np.float32)
+    return np.where(top < ((0x39800000 >> 20) & 0x7FF), np.float32(1.0), out)  # |y| < 2^-12: 1
+
+
 def set_tsi(solar_source, tsi):
     """ty_gas_optics_rrtmgp%set_tsi (rrtmgp/mo_gas_optics_rrtmgp.F90:1097-1120), float32."""
     s = np.asarray(solar_source, np.float32)
@@ -133,7 +171,7 @@ def rfmip_problem(lw_press_clamp=True, fields=None):
     # rrtmgp_rfmip_sw.F90:285-287, 432-434
     usecol = sza < np.float32(90.0) - np.float32(2.0) * spacing(90.0)
     deg_to_rad = np.float32(np.arccos(np.float32(-1.0)) / np.float32(180.0))
-    mu0 = np.where(usecol, np.cos(sza * deg_to_rad, dtype=np.float32), np.float32(1.0)).astype(np.float32)
+    mu0 = np.where(usecol, ref_cosf(sza * deg_to_rad), np.float32(1.0)).astype(np.float32)
     return {
         "ncol": ncol, "nlay": nlay, "top_at_1": top_at_1,
         "play": np.ascontiguousarray(play), "plev": np.ascontiguousarray(plev),

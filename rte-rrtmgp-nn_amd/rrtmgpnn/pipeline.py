@@ -15,10 +15,12 @@ instead of being written and re-read.  fused=False issues exactly the class laye
 What one step computes is exactly the drivers' per-block work
 (examples/rfmip-clear-sky/rrtmgp_rfmip_lw.F90:399-441, rrtmgp_rfmip_sw.F90:374-451):
 compute_nn_inputs, get_col_dry, both NN models per stream with post-processing, the Planck sources,
-the band->g emissivity expansion, both solvers and the broadband reductions.  Constant driver-side
-inputs that do not depend on the atmospheric state are prepared once: the SW incident flux
-(solar_source after set_tsi, renormalised to each column's TSI) and the per-g-point albedos.
-col_dry is computed once per step and shared by LW and SW (same h2o and plev).
+the band->g emissivity expansion, the SW boundary conditions (gas_optics_ext's incident flux
+renormalised to each column's TSI, the per-g-point surface albedo and mu0 = cos(sza), formed from the
+block's TSI, albedo and zenith angle: rrtmgpnn_sw_boundary_rfmip, rrtmgp_rfmip_sw.F90:403-434), both
+solvers and the broadband reductions.  The step's inputs are the driver's per-column state; the only
+data prepared once are the model's (network weights, the Planck table, solar_source after set_tsi).
+The unfused step computes col_dry once and shares it between LW and SW (same h2o and plev).
 
 clouds=(lwp, iwp, rel, rei) makes it the all-sky step of examples/all-sky/rrtmgp_allsky.F90:366-446
 (config C4) with NN gas optics: cloud optics by band (LUT by default, ice roughness 2 as in the example,
@@ -29,7 +31,7 @@ added as a two-stream increment; the SW solver then sees a non-zero asymmetry pa
 import numpy as np
 import torch
 
-from . import _lib, data
+from . import _lib, data, shard
 from ._lib import check, float_array, int_array, ptr_array
 from .api import GAUSS_DS, GAUSS_WTS, Context
 
@@ -39,7 +41,7 @@ SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw"
 
 
 # issue order of the fused step (stable sort; names not listed keep their place at the end)
-FUSED_ORDER = ["get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", "predict_nn_lw", "lw_solver",
+FUSED_ORDER = ["sw_boundary", "get_col_dry", "expand_emis", "nn_inputs_lw", "cloud_optics_lw", "predict_nn_lw", "lw_solver",
                "nn_inputs_sw", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver"]
 
 
@@ -58,7 +60,9 @@ def issue_order(calls, fused, lw_after=""):
             raise ValueError("lw_after: %r is not a call of this fused step's SW chain" % lw_after)
         cut = names.index(lw_after)
         head = [c for i, c in enumerate(calls) if c[0] in SW_CHAIN and i <= cut]
-        calls = head + [c for c in calls if c not in head]
+        # the SW boundary conditions (LW stream) stay ahead of the gate: they run beside the SW network
+        pre = [c for c in calls if c[0] == "sw_boundary"]
+        calls = pre + head + [c for c in calls if c not in head and c not in pre]
     return calls
 
 
@@ -77,7 +81,12 @@ class ClearSkyStep:
         self.allsky = clouds is not None
         self.fused = fused
         self._own_ctx = ctx is None  # a caller's context keeps its settings (the LW network's CU cap below)
-        self.ctx = ctx or Context(device)
+        # Streams: the step's own non-blocking HIP streams (_lib.stream_create), held for its lifetime, destroyed by
+        # close() after its graph and contexts -- never torch's pooled streams, which torch hands out round-robin to
+        # every caller, nor the legacy null stream.  Captures run on these same streams and replays launch on the LW
+        # one (the round-5 host segfault).
+        self._streams, self._closed, self.graph, self.ctx2 = [], False, None, None
+        self.ctx = ctx or Context(device, self._new_stream())
         L = self.L = _lib.lib()
         self.kd_lw, self.kd_sw = data.load_kdist("lw"), data.load_kdist("sw")
         self.ncol, self.nlay = ncol, nlay = prob["ncol"], prob["nlay"]
@@ -102,8 +111,10 @@ class ClearSkyStep:
         ins = self._inputs(prob, clouds)
         self.play, self.plev, self.tlay, self.tlev, self.tsfc = ins[:5]
         self.gases = dict(zip(self._gas_names, ins[5:5 + len(self._gas_names)]))
-        self.sfc_emis, self.mu0, self.toa, self.alb = ins[5 + len(self._gas_names):9 + len(self._gas_names)]
+        self.sfc_emis, self.sza, self.tsi, self.sfc_alb = ins[5 + len(self._gas_names):9 + len(self._gas_names)]
         self.totplnk = _t(self.kd_lw["totplnk"], dev)
+        # gas_optics_ext's toa_src per g-point: solar_source after set_tsi(1361) (rrtmgp_rfmip_sw.F90:317)
+        self.solar_source = _t(data.set_tsi(self.kd_sw["solar_source"], 1361.0), dev)
         self.sfc_lay = 1 if prob["play"][0, 0] > prob["play"][0, nlay - 1] else nlay
 
         # ---- intermediates / outputs ----
@@ -115,6 +126,8 @@ class ClearSkyStep:
         self.sw = sw
         if sw:
             self.tau_sw, self.ssa_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
+            # the SW boundary conditions, formed every step (rrtmgpnn_sw_boundary_rfmip)
+            self.toa, self.alb, self.mu0 = f(ncol, self.ng_sw), f(ncol, self.ng_sw), f(ncol)
         if not fused:  # arrays the fused step never materialises
             self.lev_src = f(ncol, nlay + 1, self.ng_lw)
             self.sfc_src, self.sfc_jac = f(ncol, self.ng_lw), f(ncol, self.ng_lw)
@@ -212,6 +225,11 @@ class ClearSkyStep:
             self.calls = [c for c in self.calls if c[0] != "cloud_optics_sw"]
             self._finish(False)
             return
+        # the driver's SW boundary conditions, on the LW context: at the head of the LW stream, beside the SW network
+        # (the SW solver waits for it), not on the SW chain's critical path
+        self.calls.insert(0, ("sw_boundary", L.rrtmgpnn_sw_boundary_rfmip,
+                              (c, self.ng_sw, ncol, p(self.solar_source), p(self.tsi), p(self.sfc_alb), p(self.sza),
+                               p(self.toa), p(self.alb), p(self.mu0))))
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
         g_sw = None if fused else p(self.g_sw)
@@ -331,15 +349,21 @@ class ClearSkyStep:
             if self.sw_net_cus:
                 check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx2.h, self.sw_net_cus), "context_set_mlp_max_cus")
             self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
-            self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
+            self._fork, self._join, self._bc = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
+
+    def _new_stream(self, priority=0):
+        """A stream owned by this step (destroyed in close())."""
+        h = _lib.stream_create(self.dev.index, priority)
+        self._streams.append(h)
+        return torch.cuda.ExternalStream(h, device=self.dev)
 
     def _sw_stream(self):
         # default priority: a high-priority SW stream (critical path) was measured 25 % slower at C3 -- it takes every
         # CU first and the chains stop overlapping (tools/ab_prio.sh)
         # sw_priority < 0: a higher-priority stream (the two-solvers-side-by-side schedule, so the SW solver's blocks are
         # dispatched ahead of the LW solver's when both are ready)
-        return torch.cuda.Stream(self.dev, priority=getattr(self, "sw_priority", 0))
+        return self._new_stream(getattr(self, "sw_priority", 0))
 
     def stream_for(self, name):
         """The torch stream a call of `self.calls` is issued on."""
@@ -352,18 +376,59 @@ class ClearSkyStep:
         check(self.L.rrtmgpnn_cloud_optics_set_ice_roughness(h, int(icergh)), "set_ice_roughness")
         return h
 
-    def __del__(self):
+    def close(self):
+        """Release the step's device state in dependency order: finish its work, destroy its hipGraph, then its
+        contexts (workspaces, buffer pools) and cloud-optics objects, then its streams.  Left to garbage collection the
+        order is the attribute dict's (the contexts before the graph whose nodes address their workspaces).  Idempotent;
+        the step is unusable afterwards."""
+        if getattr(self, "_closed", True):
+            return
+        self._closed = True
+        torch.cuda.synchronize(self.dev)
+        g, self.graph = getattr(self, "graph", None), None
+        if g is not None:
+            g.reset()
         for k in ("cloud_lw", "cloud_sw"):
             h = getattr(self, k, None)
             if h:
-                try:
-                    self.L.rrtmgpnn_cloud_optics_destroy(h)
-                except Exception:
-                    pass
+                self.L.rrtmgpnn_cloud_optics_destroy(h)
+                setattr(self, k, None)
+        if getattr(self, "ctx2", None) is not None:
+            self.ctx2.close()
+        if self._own_ctx:
+            self.ctx.close()
+        streams, self._streams = self._streams, []
+        for h in streams:
+            _lib.stream_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _enter(self):
+        """Order the step after the caller's current stream (the step runs on its own streams); returns the caller's
+        stream when it differs from the step's, for _leave."""
+        cur = torch.cuda.current_stream(self.dev)
+        if cur.cuda_stream == self.ctx.stream.cuda_stream:
+            return None
+        self.ctx.stream.wait_stream(cur)
+        return cur
+
+    def _leave(self, cur):
+        if cur is not None:
+            cur.wait_stream(self.ctx.stream)
 
     def step(self, timing=None):
-        """Issue one step.  timing: a dict name -> list; each launch is then bracketed by timing events recorded on
-        the stream it runs on (the step's own concurrency is unchanged) and (start, end) is appended."""
+        """Issue one step, ordered after the caller's current stream's work and before its later work.  timing: a dict
+        name -> list; each launch is then bracketed by timing events recorded on the stream it runs on (the step's own
+        concurrency is unchanged) and (start, end) is appended."""
+        cur = self._enter()
+        self._issue(timing)
+        self._leave(cur)
+
+    def _issue(self, timing=None):
         fork_after = "get_col_dry" if any(n == "get_col_dry" for n, _, _ in self.calls) else None
         if self.overlap and fork_after is None:  # fused step: the chains share no kernel; fork at the start
             self._fork.record(self.ctx.stream)
@@ -371,6 +436,8 @@ class ClearSkyStep:
         for name, fn, args in self.calls:
             if self.sw_after and name == "sw_solver":
                 self.ctx2.stream.wait_event(self._gate2)
+            if self.overlap and name == "sw_solver":  # its boundary conditions come from the LW stream
+                self.ctx2.stream.wait_event(self._bc)
             if timing is not None:
                 s = self.stream_for(name)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -381,6 +448,8 @@ class ClearSkyStep:
             if timing is not None:
                 e1.record(s)
                 timing.setdefault(name, []).append((e0, e1))
+            if self.overlap and name == "sw_boundary":
+                self._bc.record(self.ctx.stream)
             if self.overlap and name == fork_after:
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
@@ -394,37 +463,54 @@ class ClearSkyStep:
             self.ctx.stream.wait_event(self._join)
 
     def capture(self):
-        """Capture one step into a hipGraph (torch.cuda.CUDAGraph) on a side stream; replay with `replay()`."""
+        """Capture one step into a hipGraph (torch.cuda.CUDAGraph); replay with `replay()`.  The capture runs on the
+        step's own streams (a caller's context, which may sit on the legacy null stream, is moved to a capture stream
+        the step owns for the duration), with events of its own: no stream or event of the graph is shared with
+        another graph or with eager steps."""
         self.step()  # warm-up: kernel attributes + workspace allocation happen outside capture
         torch.cuda.synchronize(self.dev)
+        if self.graph is not None:
+            self.graph.reset()
+            self.graph = None
+        self._fork, self._join, self._bc = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
+        if self.lw_after:
+            self._gate = torch.cuda.Event()
+        if self.sw_after:
+            self._gate2 = torch.cuda.Event()
         g = torch.cuda.CUDAGraph()
-        s = torch.cuda.Stream(self.dev)
-        old = self.ctx.stream
-        if self.overlap:
-            old2 = self.ctx2.stream
-            self.ctx2.use_stream(self._sw_stream())
-        with torch.cuda.stream(s):
-            self.ctx.use_stream(s)
+        old = None
+        if not self._own_ctx:
+            if getattr(self, "_cap_stream", None) is None:
+                self._cap_stream = self._new_stream()
+            old = self.ctx.stream
+            self.ctx.use_stream(self._cap_stream)
+        s = self.ctx.stream
+        try:
             with torch.cuda.graph(g, stream=s):
-                self.step()
-        self.ctx.use_stream(old)
-        if self.overlap:
-            self.ctx2.use_stream(old2)
+                self._issue()
+        finally:
+            if old is not None:
+                self.ctx.use_stream(old)
         self.graph = g
         return g
 
     def replay(self):
-        self.graph.replay()
+        """Launch the captured step on the step's stream, ordered after the caller's current stream's work and before
+        its later work."""
+        cur = self._enter()
+        with torch.cuda.stream(self.ctx.stream):
+            self.graph.replay()
+        self._leave(cur)
 
     def _inputs(self, prob, clouds=None):
         """Device input tensors of a host problem, in io_tensors() order: the state, the gases, the surface emissivity
-        by band, mu0, the renormalised incident flux per g-point and the albedo per g-point (+ the cloud fields)."""
+        by band, and the driver's per-column SW state -- solar zenith angle, TSI, surface albedo (rrtmgp_rfmip_sw.F90:
+        244-259) -- (+ the cloud fields)."""
         dev = self.dev
         ins = [_t(prob[k], dev) for k in ("play", "plev", "tlay", "tlev", "tsfc")]
         ins += [_t(prob["gases"][k], dev) for k in self._gas_names]
         ins += [_t(np.repeat(prob["sfc_emis"][:, None], self.nb_lw, axis=1), dev),  # (ncol, nband)
-                _t(prob["mu0"], dev), _t(data.toa_flux(prob, self.kd_sw), dev),
-                _t(np.repeat(prob["sfc_alb"][:, None], self.ng_sw, axis=1), dev)]
+                _t(prob["sza"], dev), _t(prob["tsi"], dev), _t(prob["sfc_alb"], dev)]
         if clouds is not None:
             ins += [_t(a, dev) for a in clouds]
         return ins
@@ -438,8 +524,8 @@ class ClearSkyStep:
 
     def io_tensors(self):
         """(inputs, outputs): the device tensors a host-resident caller would upload / download per step."""
-        ins = [self.play, self.plev, self.tlay, self.tlev, self.tsfc, *self.gases.values(), self.sfc_emis, self.mu0,
-               self.toa, self.alb]
+        ins = [self.play, self.plev, self.tlay, self.tlev, self.tsfc, *self.gases.values(), self.sfc_emis, self.sza,
+               self.tsi, self.sfc_alb]
         if self.allsky:
             ins += [self.lwp, self.iwp, self.rel, self.rei]
         return ins, [self.lw_up, self.lw_dn, self.sw_up, self.sw_dn, self.sw_dir]
@@ -461,7 +547,7 @@ class ChunkedRank:
 
     def __init__(self, lo, hi, chunk, problem, make_step, use_graph=True):
         self.lo, self.hi = lo, hi
-        self.chunks = [(c, min(c + chunk, hi)) for c in range(lo, hi, chunk)] or [(lo, lo)]
+        self.chunks = shard.chunk_ranges(lo, hi, chunk)
         self.steps, self._run_of, self.chunk_ins, self._step_of = [], [], [], []
         for k, (c0, c1) in enumerate(self.chunks):
             prob, clouds = problem(c0, c1)
@@ -487,16 +573,33 @@ class ChunkedRank:
         self.use_graph = use_graph
 
     def run(self):
+        """One pass over the rank's columns, ordered after the caller's current stream's work and before its later
+        work (the chunks run on their steps' own streams; no ordering is needed between the two steps' chunks: their
+        buffers and slab rows are disjoint)."""
         if self.single:
             st = self.step
             st.replay() if self.use_graph else st.step()
             return
+        cur = torch.cuda.current_stream(self.step.dev)
+        used = []
         for (c0, c1), st, src in zip(self.chunks, self._step_of, self.chunk_ins):
             ins, outs = st.io_tensors()
-            with torch.cuda.stream(st.ctx.stream):
-                for d, s in zip(ins, src):
-                    d.copy_(s, non_blocking=True)
-            st.replay() if self.use_graph else st.step()
-            with torch.cuda.stream(st.ctx.stream):
+            s = st.ctx.stream
+            if st not in used:
+                used.append(st)
+                if s.cuda_stream != cur.cuda_stream:
+                    s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                for d, x in zip(ins, src):
+                    d.copy_(x, non_blocking=True)
+                st.replay() if self.use_graph else st.step()
                 for r, o in zip(self.flux, outs):
                     r[c0 - self.lo:c1 - self.lo].copy_(o, non_blocking=True)
+        for st in used:
+            if st.ctx.stream.cuda_stream != cur.cuda_stream:
+                cur.wait_stream(st.ctx.stream)
+
+    def close(self):
+        """Release every step (ClearSkyStep.close: graph, contexts, streams, in that order)."""
+        for st in self.steps:
+            st.close()

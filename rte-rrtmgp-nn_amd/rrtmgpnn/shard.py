@@ -98,15 +98,37 @@ def verify_gather(full, local, ncol, rank, world):
 
 
 def gather_columns(local, ncol, world):
-    """All-gather per-rank (ncol_local, ...) slabs into the full (ncol, ...) array on every rank.
-    Shards may differ by one column; they are padded to equal size for the collective."""
+    """All-gather per-rank (ncol_local, ...) slabs into the full (ncol, ...) array on every rank, with one
+    all_gather_into_tensor into one preallocated output.  When world divides ncol (every driver case: 1e6 and
+    N x 1800 columns over 1, 2, 4, 8 ranks) the shards are equal, the rank's slab is sent as it is and the output IS
+    the global array: one (ncol, ...) allocation per rank.  Otherwise shards differ by one column: they are padded to
+    equal size for the collective and the padded output is compacted (one more copy)."""
     per = -(-ncol // world)
-    pad = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[:local.shape[0]] = local
-    outs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(outs, pad)
+    inp = local.contiguous()
+    if inp.shape[0] != per:
+        inp = torch.zeros((per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        inp[:local.shape[0]] = local
+    out = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, inp)
+    if world * per == ncol:
+        return out
     parts = []
     for r in range(world):
         lo, hi = column_range(ncol, r, world)
-        parts.append(outs[r][:hi - lo])
+        parts.append(out[r * per:r * per + hi - lo])
     return torch.cat(parts, dim=0)
+
+
+def chunk_ranges(lo, hi, chunk):
+    """The chunks pipeline.ChunkedRank streams the column range [lo, hi) through: [(c0, c1)], at most `chunk`
+    columns each, the last one possibly short (it then runs through a second step of its own shape)."""
+    return [(c, min(c + chunk, hi)) for c in range(lo, hi, chunk)] or [(lo, lo)]
+
+
+def chunk_plan(ncol, world, chunk):
+    """Every rank's chunk sizes for a global problem of ncol columns: [(rank, [c1 - c0 for each chunk])]."""
+    plan = []
+    for r in range(world):
+        lo, hi = column_range(ncol, r, world)
+        plan.append((r, [c1 - c0 for c0, c1 in chunk_ranges(lo, hi, chunk)]))
+    return plan

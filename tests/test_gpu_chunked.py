@@ -59,3 +59,48 @@ def test_chunked_rank_equals_independent_steps(dev, config, lo, hi, chunk, graph
             for k, g in zip(keys, got):
                 np.testing.assert_array_equal(g[c0 - lo:c1 - lo], w[k],
                                               err_msg="%s, chunk %d..%d, run %d" % (k, c0, c1, rep))
+
+
+def test_chunked_rank_after_torn_down_ranks(dev):
+    """The round-5 segfault's sequence, on today's code: ranks whose steps were captured several times
+    (the removed direct mode held one graph per chunk on each step) are replayed and torn down -- once by close(),
+    once left to garbage collection -- and a rank with two step shapes (3 x 48 columns + a short chunk of 17) is then
+    built, captured and replayed three times.  Its slab must equal one independent step per chunk bit for bit."""
+    import gc
+    from rrtmgpnn.pipeline import ChunkedRank, ClearSkyStep
+    problem = _problem("rfmip")
+    lo, hi, chunk = 1700, 1700 + 3 * 48 + 17, 48
+    make = lambda p, c: ClearSkyStep(p, device=0, clouds=c)  # noqa: E731
+    for explicit in (True, False):
+        old = ChunkedRank(lo, hi, chunk, problem, make, use_graph=True)
+        for st in old.steps:
+            for _ in range(4):
+                st.capture()
+        for _ in range(2):
+            old.run()
+        torch.cuda.synchronize()
+        if explicit:
+            old.close()
+        del old
+        gc.collect()
+    rank = ChunkedRank(lo, hi, chunk, problem, make, use_graph=True)
+    assert len({st.ncol for st in rank.steps}) == 2
+    want = []
+    for c0, c1 in rank.chunks:
+        st = ClearSkyStep(problem(c0, c1)[0], device=0)
+        st.step()
+        torch.cuda.synchronize()
+        want.append(st.fluxes())
+        st.close()
+    keys = ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir")
+    for rep in range(3):
+        for t in rank.flux:
+            t.fill_(float("nan"))
+        rank.run()
+        torch.cuda.synchronize()
+        got = [t.cpu().numpy() for t in rank.flux]
+        for (c0, c1), w in zip(rank.chunks, want):
+            for k, g in zip(keys, got):
+                np.testing.assert_array_equal(g[c0 - lo:c1 - lo], w[k], err_msg="%s, chunk %d..%d, run %d"
+                                              % (k, c0, c1, rep))
+    rank.close()

@@ -117,44 +117,46 @@ def test_fused_gas_optics_equals_separate_calls(dev, rfmip, ncol, mlp_kernel):
     from rrtmgpnn.pipeline import ClearSkyStep
     prob = subset(rfmip, np.arange(ncol) * 7 % 1800)
     st = ClearSkyStep(prob, device=0, fused=False, overlap=False)
-    L, c, p = _lib.lib(), st.ctx.h, (lambda t: t.data_ptr())
-    nl, nc = st.nlay, st.ncol
-    for name in ("get_col_dry", "nn_inputs_lw", "predict_nn_lw", "nn_inputs_sw", "predict_nn_sw"):
-        fn, args = next((f, a) for n, f, a in st.calls if n == name)
-        check(fn(*args), name)
-    torch.cuda.synchronize()
-    ref = [t.clone() for t in (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)]
-    got = [torch.full_like(t, float("nan")) for t in ref]
-    check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, st.ng_lw, st.nx_lw, p(st.play), p(st.tlay), p(st.plev),
-                                      p(st.gases["h2o"]), st._g_lw, st._nd_lw, st._nets_lw, len(st.lw_nets),
-                                      p(got[0]), p(got[1])), "gas_optics_lw_nn")
-    check(L.rrtmgpnn_gas_optics_sw_nn(c, nc, nl, st.ng_sw, st.nx_sw, p(st.play), p(st.tlay), p(st.plev),
-                                      p(st.gases["h2o"]), st._g_sw, st._nd_sw, st._nets_sw, p(got[2]), p(got[3]), None),
-          "gas_optics_sw_nn")
-    torch.cuda.synchronize()
-    for k, (a, b) in enumerate(zip(ref, got)):
-        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=str(k))
-    # the g128 single-output model (18-64-64-256, no in-kernel instance): nn_inputs + col_dry in the workspace
-    from rrtmgpnn._lib import int_array
-    hb = _lib.c_vp()
-    check(L.rrtmgpnn_network_load(c, data.path("lw_g128_both").encode(), hb), "network_load")
-    names = data.rbin.unchars(data.load_model("lw_g128_both")["input_names"])
-    g_b = ptr_array([st.gases[n].data_ptr() if (k >= 2 and n in st.gases) else None for k, n in enumerate(names)])
-    nd_b = int_array([2] * len(names))
-    nets_b = ptr_array([hb.value])
-    nx = len(names)
-    x = torch.empty((nc, nl, nx), device=dev)
-    cd = torch.empty((nc, nl), device=dev)
-    out = [torch.full((nc, nl, 128), float("nan"), device=dev) for _ in range(4)]
-    check(L.rrtmgpnn_compute_nn_inputs(c, nc, nl, nx, p(st.play), p(st.tlay), g_b, nd_b, hb, p(x)), "nn_inputs")
-    check(L.rrtmgpnn_get_col_dry(c, nc, nl, p(st.gases["h2o"]), p(st.plev), p(cd)), "col_dry")
-    check(L.rrtmgpnn_predict_nn_lw(c, nc, nl, 128, nx, p(x), p(cd), nets_b, 1, p(out[0]), p(out[1])), "predict")
-    check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, 128, nx, p(st.play), p(st.tlay), p(st.plev), p(st.gases["h2o"]),
-                                      g_b, nd_b, nets_b, 1, p(out[2]), p(out[3])), "gas_optics_lw_nn both")
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(out[0].cpu().numpy(), out[2].cpu().numpy())
-    np.testing.assert_array_equal(out[1].cpu().numpy(), out[3].cpu().numpy())
-    L.rrtmgpnn_network_destroy(hb)
+    # the step runs on its own streams: torch work on the arrays it hands its raw C calls is ordered on them too
+    with torch.cuda.stream(st.ctx.stream):
+        L, c, p = _lib.lib(), st.ctx.h, (lambda t: t.data_ptr())
+        nl, nc = st.nlay, st.ncol
+        for name in ("get_col_dry", "nn_inputs_lw", "predict_nn_lw", "nn_inputs_sw", "predict_nn_sw"):
+            fn, args = next((f, a) for n, f, a in st.calls if n == name)
+            check(fn(*args), name)
+        torch.cuda.synchronize()
+        ref = [t.clone() for t in (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)]
+        got = [torch.full_like(t, float("nan")) for t in ref]
+        check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, st.ng_lw, st.nx_lw, p(st.play), p(st.tlay), p(st.plev),
+                                          p(st.gases["h2o"]), st._g_lw, st._nd_lw, st._nets_lw, len(st.lw_nets),
+                                          p(got[0]), p(got[1])), "gas_optics_lw_nn")
+        check(L.rrtmgpnn_gas_optics_sw_nn(c, nc, nl, st.ng_sw, st.nx_sw, p(st.play), p(st.tlay), p(st.plev),
+                                          p(st.gases["h2o"]), st._g_sw, st._nd_sw, st._nets_sw, p(got[2]), p(got[3]), None),
+              "gas_optics_sw_nn")
+        torch.cuda.synchronize()
+        for k, (a, b) in enumerate(zip(ref, got)):
+            np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=str(k))
+        # the g128 single-output model (18-64-64-256, no in-kernel instance): nn_inputs + col_dry in the workspace
+        from rrtmgpnn._lib import int_array
+        hb = _lib.c_vp()
+        check(L.rrtmgpnn_network_load(c, data.path("lw_g128_both").encode(), hb), "network_load")
+        names = data.rbin.unchars(data.load_model("lw_g128_both")["input_names"])
+        g_b = ptr_array([st.gases[n].data_ptr() if (k >= 2 and n in st.gases) else None for k, n in enumerate(names)])
+        nd_b = int_array([2] * len(names))
+        nets_b = ptr_array([hb.value])
+        nx = len(names)
+        x = torch.empty((nc, nl, nx), device=dev)
+        cd = torch.empty((nc, nl), device=dev)
+        out = [torch.full((nc, nl, 128), float("nan"), device=dev) for _ in range(4)]
+        check(L.rrtmgpnn_compute_nn_inputs(c, nc, nl, nx, p(st.play), p(st.tlay), g_b, nd_b, hb, p(x)), "nn_inputs")
+        check(L.rrtmgpnn_get_col_dry(c, nc, nl, p(st.gases["h2o"]), p(st.plev), p(cd)), "col_dry")
+        check(L.rrtmgpnn_predict_nn_lw(c, nc, nl, 128, nx, p(x), p(cd), nets_b, 1, p(out[0]), p(out[1])), "predict")
+        check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, 128, nx, p(st.play), p(st.tlay), p(st.plev), p(st.gases["h2o"]),
+                                          g_b, nd_b, nets_b, 1, p(out[2]), p(out[3])), "gas_optics_lw_nn both")
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out[0].cpu().numpy(), out[2].cpu().numpy())
+        np.testing.assert_array_equal(out[1].cpu().numpy(), out[3].cpu().numpy())
+        L.rrtmgpnn_network_destroy(hb)
 
 
 @pytest.mark.parametrize("allsky", [False, True])
@@ -264,30 +266,32 @@ def test_fused_gas_optics_special_pressures(dev, rfmip, mlp_kernel):
     from rrtmgpnn._lib import check
     prob = subset(rfmip, np.arange(37) * 11 % 1800)
     st = ClearSkyStep(prob, device=0, fused=False, overlap=False)
-    special = np.array([0.0, -0.0, 1.0, 1e-40, 1.4e-45, 1.17549435e-38, -5.0, np.inf, -np.inf, np.nan, 3.4e38, 1e-30,
-                        0.5, 2.0, 100.0, 1.0000001], np.float32)
-    play = st.play.view(st.ncol, st.nlay)
-    play[3, :len(special)] = torch.as_tensor(special, device=dev)
-    L, c, p = _lib.lib(), st.ctx.h, (lambda t: t.data_ptr())
-    nl, nc = st.nlay, st.ncol
-    for name in ("get_col_dry", "nn_inputs_lw", "predict_nn_lw", "nn_inputs_sw", "predict_nn_sw"):
-        fn, args = next((f, a) for n, f, a in st.calls if n == name)
-        check(fn(*args), name)
-    torch.cuda.synchronize()
-    ref = [t.clone() for t in (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)]
-    got = [torch.full_like(t, 7.0) for t in ref]
-    check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, st.ng_lw, st.nx_lw, p(st.play), p(st.tlay), p(st.plev),
-                                      p(st.gases["h2o"]), st._g_lw, st._nd_lw, st._nets_lw, len(st.lw_nets),
-                                      p(got[0]), p(got[1])), "gas_optics_lw_nn")
-    check(L.rrtmgpnn_gas_optics_sw_nn(c, nc, nl, st.ng_sw, st.nx_sw, p(st.play), p(st.tlay), p(st.plev),
-                                      p(st.gases["h2o"]), st._g_sw, st._nd_sw, st._nets_sw, p(got[2]), p(got[3]), None),
-          "gas_optics_sw_nn")
-    torch.cuda.synchronize()
-    for k, (a, b) in enumerate(zip(ref, got)):
-        a, b = a.cpu().numpy(), b.cpu().numpy()
-        assert np.isnan(a).any() == np.isnan(b).any(), k
-        np.testing.assert_array_equal(a.view(np.uint32)[~np.isnan(a)], b.view(np.uint32)[~np.isnan(b)], err_msg=str(k))
-        np.testing.assert_array_equal(np.isnan(a), np.isnan(b), err_msg=str(k))
+    # the step runs on its own streams: torch work on the arrays it hands its raw C calls is ordered on them too
+    with torch.cuda.stream(st.ctx.stream):
+        special = np.array([0.0, -0.0, 1.0, 1e-40, 1.4e-45, 1.17549435e-38, -5.0, np.inf, -np.inf, np.nan, 3.4e38, 1e-30,
+                            0.5, 2.0, 100.0, 1.0000001], np.float32)
+        play = st.play.view(st.ncol, st.nlay)
+        play[3, :len(special)] = torch.as_tensor(special, device=dev)
+        L, c, p = _lib.lib(), st.ctx.h, (lambda t: t.data_ptr())
+        nl, nc = st.nlay, st.ncol
+        for name in ("get_col_dry", "nn_inputs_lw", "predict_nn_lw", "nn_inputs_sw", "predict_nn_sw"):
+            fn, args = next((f, a) for n, f, a in st.calls if n == name)
+            check(fn(*args), name)
+        torch.cuda.synchronize()
+        ref = [t.clone() for t in (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)]
+        got = [torch.full_like(t, 7.0) for t in ref]
+        check(L.rrtmgpnn_gas_optics_lw_nn(c, nc, nl, st.ng_lw, st.nx_lw, p(st.play), p(st.tlay), p(st.plev),
+                                          p(st.gases["h2o"]), st._g_lw, st._nd_lw, st._nets_lw, len(st.lw_nets),
+                                          p(got[0]), p(got[1])), "gas_optics_lw_nn")
+        check(L.rrtmgpnn_gas_optics_sw_nn(c, nc, nl, st.ng_sw, st.nx_sw, p(st.play), p(st.tlay), p(st.plev),
+                                          p(st.gases["h2o"]), st._g_sw, st._nd_sw, st._nets_sw, p(got[2]), p(got[3]), None),
+              "gas_optics_sw_nn")
+        torch.cuda.synchronize()
+        for k, (a, b) in enumerate(zip(ref, got)):
+            a, b = a.cpu().numpy(), b.cpu().numpy()
+            assert np.isnan(a).any() == np.isnan(b).any(), k
+            np.testing.assert_array_equal(a.view(np.uint32)[~np.isnan(a)], b.view(np.uint32)[~np.isnan(b)], err_msg=str(k))
+            np.testing.assert_array_equal(np.isnan(a), np.isnan(b), err_msg=str(k))
 
 
 @pytest.mark.parametrize("nlay", [1, 7, 37, 64, 65, 71, 137])
@@ -338,39 +342,43 @@ def test_network_cu_cap_is_bitwise(dev, rfmip, cap, mlp_kernel):
     from rrtmgpnn.pipeline import ClearSkyStep
     prob = subset(rfmip, np.arange(0, 1800, 4))
     st = ClearSkyStep(prob, device=0, overlap=False)
-    assert st.lw_net_cus == 0 and st.ctx.mlp_max_cus() == 0
-    calls = [(n, f, a) for n, f, a in st.calls if n in ("predict_nn_lw", "predict_nn_sw")]
-    outs = (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)
+    # the step runs on its own streams: torch work on the arrays it hands its raw C calls is ordered on them too
+    with torch.cuda.stream(st.ctx.stream):
+        assert st.lw_net_cus == 0 and st.ctx.mlp_max_cus() == 0
+        calls = [(n, f, a) for n, f, a in st.calls if n in ("predict_nn_lw", "predict_nn_sw")]
+        outs = (st.tau_lw, st.lay_src, st.tau_sw, st.ssa_sw)
 
-    def run():
-        for t in outs:
-            t.fill_(float("nan"))
-        for n, f, a in calls:
-            check(f(*a), n)
-        torch.cuda.synchronize()
-        return [t.cpu().numpy().copy() for t in outs]
+        def run():
+            for t in outs:
+                t.fill_(float("nan"))
+            for n, f, a in calls:
+                check(f(*a), n)
+            torch.cuda.synchronize()
+            return [t.cpu().numpy().copy() for t in outs]
 
-    ref = run()
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    n = 1 if cap == "1" else max(1, cus // 8)
-    st.ctx.set_mlp_max_cus(n)
-    assert st.ctx.mlp_max_cus() == n
-    got = run()
-    st.ctx.set_mlp_max_cus(0)
-    for k, (a, b) in enumerate(zip(ref, got)):
-        assert np.isfinite(a).all()
-        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=str(k))
-    with pytest.raises(ValueError):
-        ClearSkyStep(prob, device=0, overlap=False, lw_net_cus=64)
+        ref = run()
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        n = 1 if cap == "1" else max(1, cus // 8)
+        st.ctx.set_mlp_max_cus(n)
+        assert st.ctx.mlp_max_cus() == n
+        got = run()
+        st.ctx.set_mlp_max_cus(0)
+        for k, (a, b) in enumerate(zip(ref, got)):
+            assert np.isfinite(a).all()
+            np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32), err_msg=str(k))
+        with pytest.raises(ValueError):
+            ClearSkyStep(prob, device=0, overlap=False, lw_net_cus=64)
 
 
 def test_set_stream_inside_a_global_capture(dev, rfmip):
     """rrtmgpnn_context_set_stream called while the NEW stream is being captured into a hipGraph (global capture mode):
     the context's old stream is idle and not capturing, so set_stream synchronises it; the call must succeed, the
     kernel issued next must be captured, and the replay must give the eager result bit for bit."""
+    from rrtmgpnn.api import Context
     from rrtmgpnn.pipeline import ClearSkyStep
     prob = subset(rfmip, np.arange(1, 1800, 9))
-    st = ClearSkyStep(prob, device=0, overlap=False)
+    # a caller's context on torch's current stream (the legacy null stream), as a class-layer user holds it
+    st = ClearSkyStep(prob, device=0, overlap=False, ctx=Context(0))
     st.step()
     torch.cuda.synchronize()
     ref = st.fluxes()

@@ -253,12 +253,49 @@ def test_benchmarked_step_reproduces_reference_probe(dev, rfmip):
     from rrtmgpnn.pipeline import ClearSkyStep
     prob = subset(rfmip, [0, 1, 2, 3])
     step = ClearSkyStep(prob, device=0)
-    kd = dict(data.load_kdist("sw"))
-    kd["solar_source"] = np.ones(224, np.float32)
-    step.toa.copy_(T(data.toa_flux(prob, kd), dev))
+    # the probe's flat solar source, after set_tsi; the step renormalises it to each column's TSI itself
+    step.solar_source.copy_(T(data.set_tsi(np.ones(224, np.float32), 1361.0), dev))
     step.step()
     torch.cuda.synchronize()
     f = step.fluxes()
     for got, want in ((f["lw_up"][0, 0], 289.75), (f["lw_dn"][0, -1], 339.35), (f["sw_dn"][0, 0], 757.35),
                       (f["sw_up"][0, 0], 56.82), (f["sw_dn"][0, -1], 225.74)):
         assert abs(float(got) - want) <= 6e-3, (float(got), want)
+
+
+@pytest.mark.parametrize("which", ["rfmip", "synthetic", "sweep"])
+def test_sw_boundary_conditions_match_the_driver(dev, which):
+    """rrtmgpnn_sw_boundary_rfmip (the step's per-block SW boundary conditions, rrtmgp_rfmip_sw.F90:403-434) against the
+    host's restatement of the same driver lines, bit for bit: toa_flux = solar_source * tsi / def_tsi (data.toa_flux,
+    def_tsi summed in g order), the albedo expanded to every g-point, mu0 = merge(cos(sza deg_to_rad), 1, usecol) with
+    glibc's cosf (data.ref_cosf).  'sweep': 2 M zenith angles spread over every float exponent of (0, 180) degrees,
+    night columns included (usecol false: mu0 = 1)."""
+    from rrtmgpnn import _lib, data
+    from rrtmgpnn._lib import check
+    from rrtmgpnn.api import context
+    kd = data.load_kdist("sw")
+    if which == "rfmip":
+        prob = data.rfmip_problem()
+    elif which == "synthetic":
+        prob = data.synthetic_problem(3001, 60, seed=5)
+    else:
+        u = np.arange(np.float32(1e-6).view(np.uint32), np.float32(180.0).view(np.uint32), 541, dtype=np.uint32)
+        sza = u.view(np.float32)
+        n = sza.size
+        rng = np.random.default_rng(3)
+        usecol = sza < np.float32(90.0) - np.float32(2.0) * data.spacing(90.0)
+        deg_to_rad = np.float32(np.arccos(np.float32(-1.0)) / np.float32(180.0))
+        prob = {"ncol": n, "sza": sza, "tsi": rng.uniform(1300, 1400, n).astype(np.float32),
+                "sfc_alb": rng.uniform(0, 1, n).astype(np.float32),
+                "mu0": np.where(usecol, data.ref_cosf(sza * deg_to_rad), np.float32(1.0)).astype(np.float32)}
+    ncol, ngpt = prob["ncol"], int(kd["ngpt"])
+    sol = T(data.set_tsi(kd["solar_source"], 1361.0), dev)
+    ins = [T(prob[k], dev) for k in ("tsi", "sfc_alb", "sza")]
+    toa, alb = (torch.full((ncol, ngpt), float("nan"), device=dev) for _ in range(2))
+    mu0 = torch.full((ncol,), float("nan"), device=dev)
+    check(_lib.lib().rrtmgpnn_sw_boundary_rfmip(context(0).h, ngpt, ncol, sol.data_ptr(), *[t.data_ptr() for t in ins],
+                                                toa.data_ptr(), alb.data_ptr(), mu0.data_ptr()), "sw_boundary_rfmip")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(mu0.cpu().numpy().view(np.uint32), prob["mu0"].view(np.uint32))
+    np.testing.assert_array_equal(toa.cpu().numpy().view(np.uint32), data.toa_flux(prob, kd).view(np.uint32))
+    np.testing.assert_array_equal(alb.cpu().numpy(), np.repeat(prob["sfc_alb"][:, None], ngpt, axis=1))

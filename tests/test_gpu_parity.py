@@ -267,13 +267,14 @@ def test_column_subset_invariance_bitwise(dev, rfmip):
 
 
 def test_sw_tsi_linearity(dev, rfmip):
-    """tests/verification.py sw_clear_sky_tsi: fluxes scale linearly with the incident flux."""
+    """tests/verification.py sw_clear_sky_tsi: fluxes scale linearly with the incident flux (the step forms it from
+    each column's TSI every step: halving the TSI halves the incident flux exactly)."""
     from rrtmgpnn.pipeline import ClearSkyStep
     step = ClearSkyStep(subset(rfmip, np.arange(0, 1800, 9)), device=0)
     step.step()
     torch.cuda.synchronize()
     a = step.fluxes()
-    step.toa.mul_(0.5)
+    step.tsi.mul_(0.5)
     step.step()
     torch.cuda.synchronize()
     b = step.fluxes()

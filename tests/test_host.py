@@ -2,6 +2,7 @@
 column sharding used by the multi-GPU driver (gloo, world_size 2)."""
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -119,8 +120,31 @@ def _shard_worker(rank, world, port, q):
     o_lo, o_hi = shard.column_range(ncol, 1 - rank, world)
     bad[[o_lo, o_lo + 1]] = bad[[o_lo + 1, o_lo]]
     chk_bad = shard.verify_gather(bad, local, ncol, rank, world)
+    # real fluxes: each rank computes its half of 12 RFMIP columns (the oracle's clear-sky LW+SW, as a rank's step
+    # would) and the gathered (12, 5, 61) array must equal the whole problem's fluxes computed in one piece.  12 / 2
+    # shards are equal, so gather_columns sends the slab as it is into the one preallocated output
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from rrtmgpnn import data
+    orc = O.Oracle()
+    ms_lw = [data.load_model("lw_abs"), data.load_model("lw_pfrac")]
+    ms_sw = [data.load_model("sw_abs"), data.load_model("sw_ray")]
+    kd, kds = data.load_kdist("lw"), data.load_kdist("sw")
+
+    def fluxes(p):
+        lu, ld, _ = orc.clear_sky_lw(p, ms_lw, kd)
+        su, sd, sr, _ = orc.clear_sky_sw(p, ms_sw, kds)
+        return torch.from_numpy(np.stack([lu, ld, su, sd, sr], axis=1).astype(np.float32))
+
+    n2 = 12
+    a, b = shard.column_range(n2, rank, world)
+    whole = data.rfmip_columns(0, n2)
+    mine = fluxes(data.rfmip_columns(a, b - a))
+    got = shard.gather_columns(mine, n2, world)
+    real_ok = bool(torch.equal(got, fluxes(whole))) and shard.verify_gather(got, mine, n2, rank, world)["ok"]
     q.put((rank, lo, hi, bool(torch.equal(full[:, 0, 0], torch.arange(ncol, dtype=torch.float32))), chk["ok"],
-           chk_bad["ok"], chk_bad["own_slab_bitwise"]))
+           chk_bad["ok"], chk_bad["own_slab_bitwise"], real_ok, tuple(got.shape)))
     dist.destroy_process_group()
 
 
@@ -145,6 +169,27 @@ def test_column_sharding_gloo_world2():
     assert res[0][4] and res[1][4]              # the gather check passes on the true gather
     assert not res[0][5] and not res[1][5]      # ... and catches another rank's misplaced columns
     assert res[0][6] and res[1][6]              # (the rank's own slab was untouched)
+    assert res[0][7] and res[1][7]              # real fluxes gathered equal the whole problem's, bit for bit
+    assert res[0][8] == res[1][8] == (12, 5, 61)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_c5_global_chunk_plan(world):
+    """bench.py's c5_global (BASELINE configs[4], 1e6 columns x 137 layers) at the driver's N = 1, 2, 4, 8: every rank
+    streams equal 125 000-column chunks, so each rank captures ONE step shape (no second, short-chunk step), and the
+    ranks' flux slabs are equal, so the final gather sends each slab as it is into one preallocated output."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from rrtmgpnn import shard
+    plan = shard.chunk_plan(bench.C5_GLOBAL_COLS, world, bench.C5_CHUNK)
+    assert len(plan) == world
+    assert all(sizes == [125000] * (8 // world) for _, sizes in plan)
+    assert {n for _, sizes in plan for n in sizes} == {125000}
+    assert bench.C5_GLOBAL_COLS % world == 0
+    # the chunker itself: ragged ranges end in one short chunk, empty ranges are one empty chunk
+    assert shard.chunk_ranges(0, 300001, 125000) == [(0, 125000), (125000, 250000), (250000, 300001)]
+    assert shard.chunk_ranges(5, 5, 10) == [(5, 5)]
+    assert [len(s) for _, s in shard.chunk_plan(bench.C5_GLOBAL_COLS, 3, bench.C5_CHUNK)] == [3, 3, 3]
 
 
 def test_bench_launch_plan():
@@ -243,9 +288,9 @@ def test_issue_order_keeps_each_chain_in_order(allsky, lw_after):
     runs on one stream in issue order, so a call issued ahead of its producer would read the previous step's data --
     and with an LW gate the SW-chain calls up to the gate come first."""
     from rrtmgpnn.pipeline import FUSED_ORDER, SW_CHAIN, issue_order
-    names = ["predict_nn_lw", "lw_solver", "predict_nn_sw", "sw_solver"]
+    names = ["sw_boundary", "predict_nn_lw", "lw_solver", "predict_nn_sw", "sw_solver"]
     if allsky:
-        names = ["cloud_optics_lw"] + names[:2] + ["cloud_optics_sw", "delta_scale_sw"] + names[2:]
+        names = names[:1] + ["cloud_optics_lw"] + names[1:3] + ["cloud_optics_sw", "delta_scale_sw"] + names[3:]
     elif lw_after == "cloud_optics_sw":
         with pytest.raises(ValueError):
             issue_order([(n, None, ()) for n in names], True, lw_after)
@@ -256,8 +301,28 @@ def test_issue_order_keeps_each_chain_in_order(allsky, lw_after):
     for chain in (SW_CHAIN, set(names) - SW_CHAIN):
         got = [n for n in out if n in chain]
         assert got == sorted(got, key=FUSED_ORDER.index)
+    # the SW boundary conditions (LW stream) are issued first, ahead of the LW stream's gate wait
+    assert out[0] == "sw_boundary"
     if lw_after:
         cut = out.index(lw_after)
-        assert all(n in SW_CHAIN for n in out[:cut + 1])
-        assert [n for n in out[:cut + 1]] == [n for n in sorted(names, key=FUSED_ORDER.index)
-                                              if n in SW_CHAIN][:cut + 1]
+        assert all(n in SW_CHAIN for n in out[1:cut + 1])
+        assert [n for n in out[1:cut + 1]] == [n for n in sorted(names, key=FUSED_ORDER.index)
+                                               if n in SW_CHAIN][:cut]
+
+
+def test_ref_cosf_is_glibc_cosf():
+    """mu0 = cos(sza * deg_to_rad) as the reference driver forms it with glibc's cosf (rrtmgp_rfmip_sw.F90:431-434):
+    data.ref_cosf (the host restatement the problem builders use; the device's is libm_ref.hpp ref_cosf) equals the
+    host libm's cosf on a sample of every exponent of [-4, 4] and on every RFMIP zenith angle.  numpy's float32 cos,
+    which built mu0 before round 6, rounds differently on some of them (tools/check_libm_ref_cosf.c: every float)."""
+    import ctypes
+    from rrtmgpnn import data
+    libm = ctypes.CDLL("libm.so.6")
+    libm.cosf.restype, libm.cosf.argtypes = ctypes.c_float, [ctypes.c_float]
+    u = np.arange(0, np.float32(4.0).view(np.uint32), 4099, dtype=np.uint32)
+    d2r = np.float32(np.arccos(np.float32(-1.0)) / np.float32(180.0))
+    sza = np.asarray(data.rfmip_problem()["sza"], np.float32)
+    x = np.concatenate([u.view(np.float32), -u.view(np.float32), (sza * d2r).astype(np.float32)])
+    want = np.array([libm.cosf(float(v)) for v in x], np.float32)
+    np.testing.assert_array_equal(data.ref_cosf(x).view(np.uint32), want.view(np.uint32))
+    assert (np.cos(x, dtype=np.float32) != want).any()  # numpy's own cos is not the reference's

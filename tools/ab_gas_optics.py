@@ -9,6 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rte-rrtmgp-nn_amd"))
 from rrtmgpnn import _lib, data  # noqa: E402
 from rrtmgpnn._lib import check  # noqa: E402
+from rrtmgpnn.api import context  # noqa: E402
 from rrtmgpnn.pipeline import ClearSkyStep  # noqa: E402
 
 
@@ -27,8 +28,9 @@ def timeit(fns, reps=20):
 
 
 for cfg, prob in (("c3", data.rfmip_problem()), ("c4", data.synthetic_problem(10000, 60))):
-    sep = ClearSkyStep(prob, device=0, fused=False, overlap=False)
-    fus = ClearSkyStep(prob, device=0, fused=True, overlap=False)
+    # both on the default context (torch's current stream), where the timing events are recorded
+    sep = ClearSkyStep(prob, device=0, fused=False, overlap=False, ctx=context(0))
+    fus = ClearSkyStep(prob, device=0, fused=True, overlap=False, ctx=context(0))
     call = lambda st, n: (lambda: check(next(f for m, f, a in st.calls if m == n)(*next(a for m, f, a in st.calls if m == n)), n))  # noqa: E731
     for chain, names in (("lw", ("get_col_dry", "nn_inputs_lw", "predict_nn_lw")), ("sw", ("get_col_dry", "nn_inputs_sw", "predict_nn_sw"))):
         a = [call(sep, n) for n in names]

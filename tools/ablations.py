@@ -108,6 +108,65 @@ ABLATIONS.update({
 })
 
 
+ABLATIONS.update({
+    # VALU attribution (round 6, C5): every solver exp on the hardware exponential -- the direct-beam transmittance too
+    # (build with -DRRTMGPNN_FAST_LIBM=1, which already does the rest); the exps' share of SQ_INSTS_VALU by difference
+    "exp_hw_all": [("rte_device.hpp",
+                    "__device__ __forceinline__ float solver_exp_beam(float x, const uint64_t *tab) { return ref_expf_neg(x, tab); }",
+                    "__device__ __forceinline__ float solver_exp_neg(float x, const uint64_t *tab);\n"
+                    "__device__ __forceinline__ float solver_exp_beam(float x, const uint64_t *tab) { return solver_exp_neg(x, tab); }"
+                    "  // ablation exp_hw_all", "replace"),
+                   ("x2_device.hpp", """  constexpr int L = sizeof(V) / sizeof(float);
+  float xs[N * L], ys[N * L];
+#pragma unroll
+  for (int i = 0; i < N; i++) __builtin_memcpy(&xs[i * L], &x[i], sizeof(V));
+  ref_expf_neg_batch<N * L>(xs, ys, etab);
+#pragma unroll
+  for (int i = 0; i < N; i++) __builtin_memcpy(&y[i], &ys[i * L], sizeof(V));
+}
+
+// 8-byte""", """#pragma unroll
+  for (int i = 0; i < N; i++) y[i] = exp2v_beam(x[i], etab);  // ablation exp_hw_all
+}
+
+// 8-byte""", "replace")],
+    # VALU attribution: the solvers' correctly rounded divisions, reciprocals and square roots as the bare hardware
+    # estimates (v_rcp_f32, v_sqrt_f32): their share of SQ_INSTS_VALU by difference
+    "div_hw": [("libm_ref.hpp", """  float r = __builtin_amdgcn_rcpf(b);
+  r = fmaf(fmaf(-b, r, 1.0f), r, r);
+  return fmaf(fmaf(-b, r, 1.0f), r, r);
+}""", """  return __builtin_amdgcn_rcpf(b);  // ablation div_hw
+}""", "replace"),
+               ("libm_ref.hpp", """  float r = __builtin_amdgcn_rcpf(b);
+  r = fmaf(fmaf(-b, r, 1.0f), r, r);
+  float q = a * r;
+  q = fmaf(fmaf(-b, q, a), r, q);
+  return fmaf(fmaf(-b, q, a), r, q);
+}""", """  return a * __builtin_amdgcn_rcpf(b);  // ablation div_hw
+}""", "replace"),
+               ("libm_ref.hpp", """  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float em = fmaf(-sm, s, x), ep = fmaf(-sp, s, x);
+  float r = (em <= 0.0f) ? sm : s;
+  return (ep > 0.0f) ? sp : r;
+}""", """  return __builtin_amdgcn_sqrtf(x);  // ablation div_hw
+}""", "replace"),
+               ("x2_device.hpp", """  const f2 s = (f2){__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  const f2 sm""", """  return (f2){__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};  // ablation div_hw
+  const f2 s = (f2){__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  const f2 sm""", "replace"),
+               ("x2_device.hpp", """  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  const f2 one = splat(1.0f);""", """  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  return r;  // ablation div_hw
+  const f2 one = splat(1.0f);""", "replace"),
+               ("x2_device.hpp", """  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  r = vfma(vfma(-b, r, splat(1.0f)), r, r);
+  f2 q = a * r;""", """  f2 r = (f2){__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+  return a * r;  // ablation div_hw
+  f2 q = a * r;""", "replace")],
+})
+
+
 def parametric(name):
     """swck_small:K:R:W -- the small-grid SW instance's chunk length, ring levels and wave floor;
     swck_planes:T:E -- its beam-transmittance (T) and exp(-k tau) (E) workspace planes on (1) or off (0);

@@ -65,46 +65,48 @@ def main():
     step = ClearSkyStep(prob, device=0, clouds=clouds, overlap=False)
     step.step()
     torch.cuda.synchronize()
+    torch.cuda.set_stream(torch.cuda.default_stream(0))  # the variants' contexts run on the null stream
     calls = {n: (fn, args) for n, fn, args in step.calls}
-    fn0, args0 = calls[a.stage]
-    fname = fn0.__name__
-    outs = [getattr(step, o) for o in OUTPUTS.get(a.stage, []) if hasattr(step, o)]
     libs = [(os.path.basename(a.base), a.base)] + [(os.path.basename(p), p) for p in a.libs]
-    bound = []
-    ref = None
-    for label, path in libs:
-        L, h = bind(path)
-        f = getattr(L, fname)
-        args = list(args0)
-        args[0] = h
-        for o in outs:
-            o.zero_()
-        torch.cuda.synchronize()
-        rc = f(*args)
-        assert rc == 0, (label, rc, L.rrtmgpnn_last_error())
-        torch.cuda.synchronize()
-        got = [o.detach().cpu().numpy().copy() for o in outs]
-        if ref is None:
-            ref = got
-            same = "ref"
-        else:
-            same = "bitwise" if all(np.array_equal(x.view(np.uint32), y.view(np.uint32)) for x, y in zip(got, ref)) \
-                else "DIFFERENT(max %.3g)" % max(float(np.max(np.abs(x - y))) for x, y in zip(got, ref))
-        bound.append((label, f, args, same, []))
-    for _ in range(a.rounds):
-        for label, f, args, same, times in bound:
-            f(*args)
+    handles = [(label, bind(path)) for label, path in libs]
+    for stage in a.stage.split(","):  # several stages: each timed in turn, one profiler run covers them all
+        fn0, args0 = calls[stage]
+        fname = fn0.__name__
+        outs = [getattr(step, o) for o in OUTPUTS.get(stage, []) if hasattr(step, o)]
+        bound = []
+        ref = None
+        for label, (L, h) in handles:
+            f = getattr(L, fname)
+            args = list(args0)
+            args[0] = h
+            for o in outs:
+                o.zero_()
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
+            rc = f(*args)
+            assert rc == 0, (label, rc, L.rrtmgpnn_last_error())
+            torch.cuda.synchronize()
+            got = [o.detach().cpu().numpy().copy() for o in outs]
+            if ref is None:
+                ref = got
+                same = "ref"
+            else:
+                same = "bitwise" if all(np.array_equal(x.view(np.uint32), y.view(np.uint32)) for x, y in zip(got, ref)) \
+                    else "DIFFERENT(max %.3g)" % max(float(np.max(np.abs(x - y))) for x, y in zip(got, ref))
+            bound.append((label, f, args, same, []))
+        for _ in range(a.rounds):
+            for label, f, args, same, times in bound:
                 f(*args)
-            e1.record()
-            e1.synchronize()
-            times.append(e0.elapsed_time(e1) / a.iters)
-    for label, f, args, same, times in bound:
-        print("%-28s %s %s  median %.4f ms  min %.4f ms  %s" % (label, a.config, a.stage, statistics.median(times),
-                                                                 min(times), same), flush=True)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    f(*args)
+                e1.record()
+                e1.synchronize()
+                times.append(e0.elapsed_time(e1) / a.iters)
+        for label, f, args, same, times in bound:
+            print("%-28s %s %s  median %.4f ms  min %.4f ms  %s" % (label, a.config, stage, statistics.median(times),
+                                                                     min(times), same), flush=True)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,7 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 config = sys.argv[2] if len(sys.argv) > 2 else "c3"
 prob = data.rfmip_problem() if config == "c3" else data.synthetic_problem(10000, 60)
 step = ClearSkyStep(prob, device=0)
+torch.cuda.set_stream(step.ctx.stream)  # the raw calls below run on the step's own streams
 step.step()
 torch.cuda.synchronize()
 for _ in range(reps):
