@@ -135,6 +135,9 @@ def stage_work(name, step):
         return "byte", N * (2 * glw + step.nb_lw) * f4, None, None
     if name == "increment_sw":
         return "byte", N * (6 * gsw + 3 * step.nb_sw) * f4, None, None
+    if name == "sw_boundary":
+        # tsi, albedo, sza (+ the g-point source) read; toa and the per-g albedo (G) and mu0 written
+        return "byte", ncol * (3 + 2 * gsw + 1) * f4 + gsw * f4, None, None
     if name == "planck_source":
         # pfrac read, lay (in place) + lev + sfc + sfcJac written
         return "byte", ncol * ((glw * nlay + glw * nlay + glw * (nlay + 1) + 2 * glw) * f4), None, None
@@ -327,6 +330,36 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total_cols = global_cols * args.steps
     value = total_cols / elapsed
+
+    # ---- block stream (never `value`): the step's block streamed K times with its two chains free-running
+    # (ClearSkyStep.run_blocks: block b+1's SW chain beside block b's LW chain, no per-block join) -- the rate of a
+    # stream of independent blocks, the reference driver's block loop (rrtmgp_rfmip_lw.F90:364-446), whose OpenMP
+    # threads also run blocks side by side.  `value` keeps the joined step ----
+    block_stream = None
+    if step.overlap and step.sw and rank_run.single and use_graph:
+        step.capture_chains()
+        nb = max(args.steps, 50)
+        for _ in range(3):
+            step.run_blocks(max(1, args.warmup))
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        step.run_blocks(nb)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el_b = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el_b], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_b = float(t.item())
+        block_stream = {"value": round(global_cols * nb / el_b, 1), "unit": "columns/s", "blocks": nb,
+                        "ms_per_block": round(el_b / nb * 1e3, 4),
+                        "vs_joined_step": round((el_b / nb) / (elapsed / args.steps), 4),
+                        "note": "the step's block streamed `blocks` times per rank, LW and SW chains as two hipGraphs "
+                                "replayed free-running on their streams (block b+1's SW chain beside block b's LW "
+                                "chain); same fluxes bit for bit (tests/test_gpu_chunked.py); not `value`"}
 
     # ---- host-resident variant: pinned H2D of every input, the step, D2H of the fluxes (never `value`; one chunk) ----
     ins, outs = step.io_tensors()
@@ -546,6 +579,7 @@ def main():
             "gather_check": gather_check,
             "end_to_end": end_to_end,
             "host_resident": pcie,
+            "block_stream": block_stream,
             "c5_global": c5g,
         }
         if world > 1:

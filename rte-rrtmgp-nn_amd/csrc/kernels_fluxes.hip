@@ -7,8 +7,8 @@
 //                          toa_src over g-points in g order, toa = toa_src * tsi / def_tsi, the spectrally constant
 //                          surface albedo expanded to every g-point, mu0 = merge(cos(sza * deg_to_rad), 1, usecol)
 //                          with usecol = sza < 90 - 2 spacing(90) (rrtmgp_rfmip_sw.F90:236-238) and glibc's cosf
-//                          (libm_ref.hpp ref_cosf).  A block holds kBcCols columns: one lane per column forms its sum
-//                          (the reference's sequential order), then the block writes the (ngpt, kBcCols) slabs.
+//                          (libm_ref.hpp ref_cosf).  A block holds kBcCols columns; def_tsi in the reference's
+//                          sequential order, then the block writes the (ngpt, kBcCols) slabs.
 //
 //  * heating_rate_kernel : layer heating rates from the level fluxes and pressures, in the fork's (nlay+1, ncol)
 //                          level-fastest flux layout.  Two forms, both term by term:
@@ -25,8 +25,11 @@
 
 namespace rrtmgpnn {
 
-constexpr int kBcCols = 8;
+constexpr int kBcCols = 16, kSwBoundaryMaxG = 1024;
 
+// toa_src(igpt, icol) = solar_source(igpt) for every column (gas_optics_ext), so every column's def_tsi is the same
+// sequential sum: one lane forms it per block, over the source staged in LDS (a sum over dependent global loads took
+// 18 us at C3)
 __global__ void __launch_bounds__(256) sw_boundary_kernel(int ngpt, int ncol, const float *__restrict__ solar_source,
                                                           const float *__restrict__ tsi,
                                                           const float *__restrict__ sfc_alb,
@@ -34,21 +37,35 @@ __global__ void __launch_bounds__(256) sw_boundary_kernel(int ngpt, int ncol, co
                                                           float sza_max, float *__restrict__ toa,
                                                           float *__restrict__ alb, float *__restrict__ mu0)
 {
-  __shared__ float def_tsi[kBcCols];
+  __shared__ float src[kSwBoundaryMaxG];
+  __shared__ float def_tsi;
   const int c0 = blockIdx.x * kBcCols, t = threadIdx.x;
+  for (int g = t; g < ngpt; g += blockDim.x) src[g] = solar_source[g];
+  __syncthreads();
+  if (t == 0) {
+    float s = 0.0f;  // def_tsi_s = def_tsi_s + toa_flux(igpt, icol), igpt = 1..ngpt, in that order
+    int g = 0;
+    for (; g + 8 <= ngpt; g += 8) {  // eight LDS reads in flight, then the eight dependent adds
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = src[g + j];
+#pragma unroll
+      for (int j = 0; j < 8; j++) s = s + v[j];
+    }
+    for (; g < ngpt; g++) s = s + src[g];
+    def_tsi = s;
+  }
   if (t < kBcCols && c0 + t < ncol) {
-    float s = 0.0f;  // def_tsi_s = def_tsi_s + toa_flux(igpt, icol), igpt = 1..ngpt
-    for (int g = 0; g < ngpt; g++) s = s + solar_source[g];
-    def_tsi[t] = s;
     const float z = sza[c0 + t];
     mu0[c0 + t] = z < sza_max ? ref_cosf(z * deg_to_rad) : 1.0f;
   }
   __syncthreads();
+  const float d = def_tsi;
   const int nc = min(kBcCols, ncol - c0);
   for (int i = t; i < nc * ngpt; i += blockDim.x) {
     const int c = i / ngpt, g = i - c * ngpt;
     const size_t k = (size_t)(c0 + c) * ngpt + g;
-    toa[k] = solar_source[g] * tsi[c0 + c] / def_tsi[c];
+    toa[k] = src[g] * tsi[c0 + c] / d;
     alb[k] = sfc_alb[c0 + c];
   }
 }
@@ -57,6 +74,7 @@ int launch_sw_boundary(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *s
                        const float *sfc_alb, const float *sza, float *toa, float *alb, float *mu0)
 {
   if (ncol == 0) return RRTMGPNN_OK;
+  if (ngpt > kSwBoundaryMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw_boundary_rfmip: ngpt > 1024");
   // deg_to_rad = acos(-1._wp) / 180._wp in working precision (rrtmgp_rfmip_sw.F90:106); the usecol bound
   // 90 - 2 spacing(90) = 90 - 2^-16 (spacing(90.) = 2^-17 in fp32)
   volatile float pi = 3.14159265358979323846f;

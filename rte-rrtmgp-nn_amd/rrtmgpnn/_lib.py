@@ -158,17 +158,24 @@ def _hip_runtime():
         h = ctypes.CDLL("libamdhip64.so.7")
         h.hipStreamCreateWithPriority.restype = c_int
         h.hipStreamCreateWithPriority.argtypes = [P(c_vp), ctypes.c_uint, c_int]
-        h.hipStreamDestroy.restype = c_int
-        h.hipStreamDestroy.argtypes = [c_vp]
         h.hipSetDevice.restype = c_int
         h.hipSetDevice.argtypes = [c_int]
         _hip = h
     return _hip
 
 
-def stream_create(device, priority=0):
-    """A non-blocking HIP stream of the caller's own (not one of torch's pooled streams, which other objects are
-    handed round-robin): the raw handle; free it with stream_destroy once nothing uses it."""
+_free_streams = {}  # (device, priority) -> handles released by their last owner
+
+
+def stream_acquire(device, priority=0):
+    """A non-blocking HIP stream held by one owner at a time (ClearSkyStep), not one of torch's pooled streams, which
+    torch hands to every caller round-robin: a stream a closed owner released, or a new one.  Streams are never
+    destroyed: events recorded on a stream (torch's pinned-memory allocator keeps such events and queries them after
+    their tensors are freed) reference its queue, and a destroyed stream's queue is freed memory -- bench.py crashed in
+    exactly that way when close() destroyed the step's streams (round 6)."""
+    key = (int(device), int(priority))
+    if _free_streams.get(key):
+        return _free_streams[key].pop()
     h = _hip_runtime()
     s = c_vp()
     rc = h.hipSetDevice(int(device)) or h.hipStreamCreateWithPriority(ctypes.byref(s), 1, int(priority))
@@ -177,9 +184,11 @@ def stream_create(device, priority=0):
     return s.value
 
 
-def stream_destroy(handle):
+def stream_release(handle, device, priority=0):
+    """Give a stream back once its owner's work on it is complete (the next owner's work is ordered after it anyway:
+    the stream is in-order)."""
     if handle:
-        _hip_runtime().hipStreamDestroy(handle)
+        _free_streams.setdefault((int(device), int(priority)), []).append(handle)
 
 
 def check(rc, what=""):

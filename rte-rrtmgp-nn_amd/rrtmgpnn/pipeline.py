@@ -37,7 +37,8 @@ from .api import GAUSS_DS, GAUSS_WTS, Context
 
 
 # calls of the SW chain (issued on the second stream when overlapping)
-SW_CHAIN = {"nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw", "sw_solver"}
+SW_CHAIN = {"sw_boundary", "nn_inputs_sw", "predict_nn_sw", "cloud_optics_sw", "delta_scale_sw", "increment_sw",
+            "sw_solver"}
 
 
 # issue order of the fused step (stable sort; names not listed keep their place at the end)
@@ -60,9 +61,7 @@ def issue_order(calls, fused, lw_after=""):
             raise ValueError("lw_after: %r is not a call of this fused step's SW chain" % lw_after)
         cut = names.index(lw_after)
         head = [c for i, c in enumerate(calls) if c[0] in SW_CHAIN and i <= cut]
-        # the SW boundary conditions (LW stream) stay ahead of the gate: they run beside the SW network
-        pre = [c for c in calls if c[0] == "sw_boundary"]
-        calls = pre + head + [c for c in calls if c not in head and c not in pre]
+        calls = head + [c for c in calls if c not in head]
     return calls
 
 
@@ -81,7 +80,7 @@ class ClearSkyStep:
         self.allsky = clouds is not None
         self.fused = fused
         self._own_ctx = ctx is None  # a caller's context keeps its settings (the LW network's CU cap below)
-        # Streams: the step's own non-blocking HIP streams (_lib.stream_create), held for its lifetime, destroyed by
+        # Streams: non-blocking HIP streams this step alone holds for its lifetime (_lib.stream_acquire), released by
         # close() after its graph and contexts -- never torch's pooled streams, which torch hands out round-robin to
         # every caller, nor the legacy null stream.  Captures run on these same streams and replays launch on the LW
         # one (the round-5 host segfault).
@@ -225,9 +224,11 @@ class ClearSkyStep:
             self.calls = [c for c in self.calls if c[0] != "cloud_optics_sw"]
             self._finish(False)
             return
-        # the driver's SW boundary conditions, on the LW context: at the head of the LW stream, beside the SW network
-        # (the SW solver waits for it), not on the SW chain's critical path
-        self.calls.insert(0, ("sw_boundary", L.rrtmgpnn_sw_boundary_rfmip,
+        # the driver's SW boundary conditions, at the head of the SW chain.  Round 6: on the LW stream beside the SW
+        # network, with the SW solver waiting for it, the C3 step measured 0.497 ms against 0.43: the extra edge into the
+        # SW solver let the LW network take the CUs first (gpurun_out r06 bench2_noc5 -> profiles/r06)
+        # (unfused: after get_col_dry, the call the SW stream forks after)
+        self.calls.insert(0 if fused else 1, ("sw_boundary", L.rrtmgpnn_sw_boundary_rfmip,
                               (c, self.ng_sw, ncol, p(self.solar_source), p(self.tsi), p(self.sfc_alb), p(self.sza),
                                p(self.toa), p(self.alb), p(self.mu0))))
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
@@ -349,13 +350,13 @@ class ClearSkyStep:
             if self.sw_net_cus:
                 check(self.L.rrtmgpnn_context_set_mlp_max_cus(self.ctx2.h, self.sw_net_cus), "context_set_mlp_max_cus")
             self.calls = [(n, f, ((self.ctx2.h,) + tuple(a[1:])) if n in SW_CHAIN else a) for n, f, a in self.calls]
-            self._fork, self._join, self._bc = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
+            self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         self.graph = None
 
     def _new_stream(self, priority=0):
-        """A stream owned by this step (destroyed in close())."""
-        h = _lib.stream_create(self.dev.index, priority)
-        self._streams.append(h)
+        """A stream held by this step alone until close() (_lib.stream_acquire)."""
+        h = _lib.stream_acquire(self.dev.index, priority)
+        self._streams.append((h, priority))
         return torch.cuda.ExternalStream(h, device=self.dev)
 
     def _sw_stream(self):
@@ -378,7 +379,7 @@ class ClearSkyStep:
 
     def close(self):
         """Release the step's device state in dependency order: finish its work, destroy its hipGraph, then its
-        contexts (workspaces, buffer pools) and cloud-optics objects, then its streams.  Left to garbage collection the
+        contexts (workspaces, buffer pools) and cloud-optics objects, then hand its streams back.  Left to garbage collection the
         order is the attribute dict's (the contexts before the graph whose nodes address their workspaces).  Idempotent;
         the step is unusable afterwards."""
         if getattr(self, "_closed", True):
@@ -386,8 +387,10 @@ class ClearSkyStep:
         self._closed = True
         torch.cuda.synchronize(self.dev)
         g, self.graph = getattr(self, "graph", None), None
-        if g is not None:
-            g.reset()
+        for x in (g,) + tuple(getattr(self, "chain_graphs", ())):
+            if x is not None:
+                x.reset()
+        self.chain_graphs = ()
         for k in ("cloud_lw", "cloud_sw"):
             h = getattr(self, k, None)
             if h:
@@ -398,8 +401,8 @@ class ClearSkyStep:
         if self._own_ctx:
             self.ctx.close()
         streams, self._streams = self._streams, []
-        for h in streams:
-            _lib.stream_destroy(h)
+        for h, prio in streams:
+            _lib.stream_release(h, self.dev.index, prio)
 
     def __del__(self):
         try:
@@ -436,8 +439,6 @@ class ClearSkyStep:
         for name, fn, args in self.calls:
             if self.sw_after and name == "sw_solver":
                 self.ctx2.stream.wait_event(self._gate2)
-            if self.overlap and name == "sw_solver":  # its boundary conditions come from the LW stream
-                self.ctx2.stream.wait_event(self._bc)
             if timing is not None:
                 s = self.stream_for(name)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -448,8 +449,6 @@ class ClearSkyStep:
             if timing is not None:
                 e1.record(s)
                 timing.setdefault(name, []).append((e0, e1))
-            if self.overlap and name == "sw_boundary":
-                self._bc.record(self.ctx.stream)
             if self.overlap and name == fork_after:
                 self._fork.record(self.ctx.stream)
                 self.ctx2.stream.wait_event(self._fork)
@@ -472,7 +471,7 @@ class ClearSkyStep:
         if self.graph is not None:
             self.graph.reset()
             self.graph = None
-        self._fork, self._join, self._bc = torch.cuda.Event(), torch.cuda.Event(), torch.cuda.Event()
+        self._fork, self._join = torch.cuda.Event(), torch.cuda.Event()
         if self.lw_after:
             self._gate = torch.cuda.Event()
         if self.sw_after:
@@ -493,6 +492,46 @@ class ClearSkyStep:
                 self.ctx.use_stream(old)
         self.graph = g
         return g
+
+    def capture_chains(self):
+        """A stream of blocks (run_blocks): the SW chain (boundary conditions, network, solver) and the LW chain
+        (network, solver) captured as two hipGraphs, each on its own context's stream and alone -- no gate or join
+        between them."""
+        if not (self.overlap and self.sw):
+            raise ValueError("capture_chains: a step with its LW and SW chains on two streams")
+        self.step()  # warm-up outside capture
+        torch.cuda.synchronize(self.dev)
+        graphs = []
+        for chain, ctx in ((lambda n: n in SW_CHAIN, self.ctx2), (lambda n: n not in SW_CHAIN, self.ctx)):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=ctx.stream):
+                for name, fn, args in self.calls:
+                    if chain(name):
+                        rc = fn(*args)
+                        if rc:
+                            check(rc, name)
+            graphs.append(g)
+        self.chain_graphs = tuple(graphs)
+
+    def run_blocks(self, k):
+        """k blocks streamed through the step: each chain replays k times in its own stream's order, and block b+1's
+        SW chain starts as soon as block b's SW solver is done -- beside block b's LW chain -- instead of after
+        block b's join.  (A stream of distinct blocks needs each block's inputs and outputs in storage of its own;
+        this one re-runs the step's block, whose results are the same every time.)  Ordered after the caller's
+        current stream's work and before its later work."""
+        g_sw, g_lw = self.chain_graphs
+        cur = torch.cuda.current_stream(self.dev)
+        for s in (self.ctx2.stream, self.ctx.stream):
+            if s.cuda_stream != cur.cuda_stream:
+                s.wait_stream(cur)
+        for _ in range(k):
+            with torch.cuda.stream(self.ctx2.stream):
+                g_sw.replay()
+            with torch.cuda.stream(self.ctx.stream):
+                g_lw.replay()
+        for s in (self.ctx2.stream, self.ctx.stream):
+            if s.cuda_stream != cur.cuda_stream:
+                cur.wait_stream(s)
 
     def replay(self):
         """Launch the captured step on the step's stream, ordered after the caller's current stream's work and before

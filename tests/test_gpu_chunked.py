@@ -104,3 +104,73 @@ def test_chunked_rank_after_torn_down_ranks(dev):
                 np.testing.assert_array_equal(g[c0 - lo:c1 - lo], w[k], err_msg="%s, chunk %d..%d, run %d"
                                               % (k, c0, c1, rep))
     rank.close()
+
+
+def test_pinned_copies_on_a_closed_steps_stream(dev):
+    """bench.py's host-resident leg makes non-blocking copies between pinned host tensors and the step's tensors on
+    the step's own stream; torch's pinned-memory allocator keeps an event recorded on that stream and queries it when
+    the host tensors are freed -- after the step is closed.  Round 6 first destroyed the step's streams in close(),
+    and bench.py crashed in that query; streams are now handed back and reused, never destroyed.  The
+    sequence must run clean, and a step built afterwards (on a reused stream) must give the first step's fluxes."""
+    import gc
+    from rrtmgpnn.pipeline import ClearSkyStep
+    problem = _problem("rfmip")
+    p, _ = problem(0, 96)
+    st = ClearSkyStep(p, device=0)
+    st.capture()
+    torch.cuda.set_stream(st.ctx.stream)
+    try:
+        st.replay()
+        ins, outs = st.io_tensors()
+        h_ins = [t.cpu().pin_memory() for t in ins]
+        h_outs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in outs]
+        for _ in range(3):
+            for d, h in zip(ins, h_ins):
+                d.copy_(h, non_blocking=True)
+            st.replay()
+            for h, d in zip(h_outs, outs):
+                h.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+        want = [h.numpy().copy() for h in h_outs]
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    st.close()
+    del st, ins, outs, h_ins, h_outs
+    gc.collect()
+    torch.cuda.empty_cache()
+    again = ClearSkyStep(p, device=0)
+    again.capture()
+    again.replay()
+    torch.cuda.synchronize()
+    got = again.io_tensors()[1]
+    for w, g in zip(want, got):
+        np.testing.assert_array_equal(g.cpu().numpy(), w)
+    again.close()
+
+
+@pytest.mark.parametrize("config", ["rfmip", "allsky"])
+def test_block_stream_equals_step(dev, config):
+    """ClearSkyStep.run_blocks (the two chains replayed free-running, bench.py's block_stream): after any number of
+    blocks the fluxes are the joined step's, bit for bit, and a joined replay afterwards still gives them."""
+    from rrtmgpnn.pipeline import ClearSkyStep
+    p, c = _problem(config)(100, 100 + 333)
+    st = ClearSkyStep(p, device=0, clouds=c)
+    st.step()
+    torch.cuda.synchronize()
+    want = st.fluxes()
+    st.capture()
+    st.capture_chains()
+    keys = ("lw_up", "lw_dn", "sw_up", "sw_dn", "sw_dir")
+    for k in (1, 7):
+        for name in keys:
+            getattr(st, name).fill_(float("nan"))
+        st.run_blocks(k)
+        torch.cuda.synchronize()
+        got = st.fluxes()
+        for name in keys:
+            np.testing.assert_array_equal(got[name], want[name], err_msg="%s after %d blocks" % (name, k))
+    st.replay()
+    torch.cuda.synchronize()
+    for name, v in st.fluxes().items():
+        np.testing.assert_array_equal(v, want[name], err_msg=name)
+    st.close()

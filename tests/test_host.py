@@ -301,13 +301,12 @@ def test_issue_order_keeps_each_chain_in_order(allsky, lw_after):
     for chain in (SW_CHAIN, set(names) - SW_CHAIN):
         got = [n for n in out if n in chain]
         assert got == sorted(got, key=FUSED_ORDER.index)
-    # the SW boundary conditions (LW stream) are issued first, ahead of the LW stream's gate wait
-    assert out[0] == "sw_boundary"
+    assert out[0] == "sw_boundary"  # the head of the SW chain
     if lw_after:
         cut = out.index(lw_after)
-        assert all(n in SW_CHAIN for n in out[1:cut + 1])
-        assert [n for n in out[1:cut + 1]] == [n for n in sorted(names, key=FUSED_ORDER.index)
-                                               if n in SW_CHAIN][:cut]
+        assert all(n in SW_CHAIN for n in out[:cut + 1])
+        assert [n for n in out[:cut + 1]] == [n for n in sorted(names, key=FUSED_ORDER.index)
+                                              if n in SW_CHAIN][:cut + 1]
 
 
 def test_ref_cosf_is_glibc_cosf():

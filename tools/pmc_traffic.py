@@ -31,6 +31,7 @@ STAGES = [
     (re.compile(r"nn_inputs_kernel"), "nn_inputs"),
     (re.compile(r"expand_kernel"), "expand_emis"),
     (re.compile(r"col_dry_kernel"), "get_col_dry"),
+    (re.compile(r"sw_boundary_kernel"), "sw_boundary"),
 ]
 
 
