@@ -384,6 +384,18 @@ int rrtmgpnn_calc_heating_rate_k_day(rrtmgpnn_context *ctx, int ncol, int nlay, 
  * (ncol); outputs DEVICE toa_flux and sfc_alb_gpt (ngpt, ncol), mu0 (ncol). */
 int rrtmgpnn_sw_boundary_rfmip(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
                                const float *sfc_alb, const float *sza, float *toa_flux, float *sfc_alb_gpt, float *mu0);
+/* rrtmgpnn_sw_boundary_rfmip followed by rrtmgpnn_sw_solver_2stream (nbnd == 0) or rrtmgpnn_sw_solver_2stream_inc
+ * (nbnd > 0; band_lims_gpt, tau_bnd, ssa_bnd, g_bnd as there), with no diffuse incident flux and the albedo given for
+ * both the direct and the diffuse beam, as the RFMIP and all-sky drivers call rte_sw (rrtmgp_rfmip_sw.F90:403-441):
+ * the same fluxes, bit for bit.  The checkpointed solver forms the boundary conditions in its prologue (no separate
+ * launch); the other solver kernels read them from toa_flux, sfc_alb_gpt and mu0 (DEVICE scratch, (ngpt, ncol),
+ * (ngpt, ncol), (ncol); contents unspecified after the call). */
+int rrtmgpnn_sw_solver_2stream_rfmip(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                     const float *solar_source, const float *tsi, const float *sfc_alb, const float *sza,
+                                     const float *tau, const float *ssa, const float *g, int nbnd,
+                                     const int *band_lims_gpt, const float *tau_bnd, const float *ssa_bnd,
+                                     const float *g_bnd, float *toa_flux, float *sfc_alb_gpt, float *mu0,
+                                     float *flux_up, float *flux_dn, float *flux_dir);
 /* ty_optical_props_2str%delta_scale([for]) (rte/mo_optical_props.F90:576-604; kernels
  * rte/kernels/mo_optical_props_kernels.F90:41-92) on n values in place.  fwd == NULL: f = g**2. */
 int rrtmgpnn_delta_scale_2str(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);

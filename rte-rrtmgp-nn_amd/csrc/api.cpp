@@ -1104,6 +1104,31 @@ int rrtmgpnn_sw_boundary_rfmip(rrtmgpnn_context *ctx, int ngpt, int ncol, const 
   return launch_sw_boundary(ctx, ngpt, ncol, solar_source, tsi, sfc_alb, sza, toa_flux, sfc_alb_gpt, mu0);
 }
 
+int rrtmgpnn_sw_solver_2stream_rfmip(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1,
+                                     const float *solar_source, const float *tsi, const float *sfc_alb, const float *sza,
+                                     const float *tau, const float *ssa, const float *g, int nbnd,
+                                     const int *band_lims_gpt, const float *tau_bnd, const float *ssa_bnd,
+                                     const float *g_bnd, float *toa_flux, float *sfc_alb_gpt, float *mu0,
+                                     float *flux_up, float *flux_dn, float *flux_dir)
+{
+  if (int rc = check_ctx(ctx)) return rc;
+  if (!solar_source || !tsi || !sfc_alb || !sza || !tau || !ssa || !toa_flux || !sfc_alb_gpt || !mu0 || !flux_up ||
+      !flux_dn || !flux_dir || ngpt < 1 || nlay < 1 || ncol < 0 || nbnd < 0 ||
+      (nbnd > 0 && (!tau_bnd || !ssa_bnd || !g_bnd)))
+    return fail(RRTMGPNN_ERR_ARGUMENT, "sw_solver_2stream_rfmip: bad argument");
+  if (ngpt > kSwBoundaryMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw_solver_2stream_rfmip: ngpt > 1024");
+  const SwBc bc{solar_source, tsi, sfc_alb, sza, toa_flux, sfc_alb_gpt, mu0};
+  BandArgs b;
+  if (nbnd > 0) {
+    if (int rc = band_args(nbnd, band_lims_gpt, ngpt, b)) return rc;
+    if (int rc = bands_cover(b, ngpt)) return rc;
+  }
+  // inc_flux / mu0 / albedos: the scratch arrays, which the solver reads only when it does not form them itself
+  return launch_sw_2stream(ctx, ngpt, nlay, ncol, top_at_1, toa_flux, nullptr, tau, ssa, g, mu0, sfc_alb_gpt,
+                           sfc_alb_gpt, nbnd > 0 ? &b : nullptr, tau_bnd, ssa_bnd, g_bnd, flux_up, flux_dn, flux_dir,
+                           &bc);
+}
+
 // ---- data files: RBIN, classic netCDF, netCDF-4 (datafile.cpp) ----
 struct rrtmgpnn_file {
   DataFile df;

@@ -148,6 +148,20 @@ int launch_heating_rate(rrtmgpnn_context *ctx, int ncol, int nlay, int k_day, fl
                         const float *dn, const float *plev, float *hr);
 int launch_sw_boundary(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
                        const float *sfc_alb, const float *sza, float *toa, float *alb, float *mu0);
+// the RFMIP driver's SW boundary conditions as inputs of a solver launch (rrtmgpnn_sw_solver_2stream_rfmip): the
+// checkpointed solver forms them in its prologue; the other solver kernels get them from launch_sw_boundary, into
+// toa / alb / mu0 (scratch)
+struct SwBc {
+  const float *solar_source, *tsi, *sfc_alb, *sza;
+  float *toa, *alb, *mu0;
+};
+// the device-side part: the inputs and the driver's two constants (deg_to_rad, the usecol bound)
+struct SwBcDev {
+  const float *solar_source, *tsi, *sfc_alb, *sza;
+  float deg_to_rad, sza_max;
+};
+SwBcDev sw_boundary_device(const SwBc *bc);
+constexpr int kSwBoundaryMaxG = 1024;
 int launch_delta_scale(rrtmgpnn_context *ctx, long long n, float *tau, float *ssa, float *g, const float *fwd);
 // kernels_nn.hip
 struct GasArgs {
@@ -203,7 +217,7 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
                       const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                       const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                       const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, float *flux_up,
-                      float *flux_dn, float *flux_dir);
+                      float *flux_dn, float *flux_dir, const SwBc *bc = nullptr);
 // kernels_sw_x2.hip (called by launch_sw_2stream for even ngpt; ws sized by it)
 size_t sw_2stream_x2_layer_planes(bool inc);
 int launch_sw_2stream_x2(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
@@ -222,7 +236,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
-                         float *flux_dn, float *flux_dir, bool planes = true);
+                         float *flux_dn, float *flux_dir, bool planes = true, const SwBcDev *bc = nullptr);
 // kernels_lw_scat.hip
 int launch_lw_rescl(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, int nmus, const float *Ds,
                     const float *wts, const float *inc_flux, const float *tau, const float *ssa, const float *g,

@@ -8,7 +8,10 @@
 //                          surface albedo expanded to every g-point, mu0 = merge(cos(sza * deg_to_rad), 1, usecol)
 //                          with usecol = sza < 90 - 2 spacing(90) (rrtmgp_rfmip_sw.F90:236-238) and glibc's cosf
 //                          (libm_ref.hpp ref_cosf).  A block holds kBcCols columns; def_tsi in the reference's
-//                          sequential order, then the block writes the (ngpt, kBcCols) slabs.
+//                          sequential order, then the block writes the (ngpt, kBcCols) slabs.  The benchmarked step
+//                          forms the same values in the checkpointed SW solver's prologue instead
+//                          (rrtmgpnn_sw_solver_2stream_rfmip, kernels_sw_ck.hip); this kernel serves the class layer
+//                          and the other SW solver kernels.
 //
 //  * heating_rate_kernel : layer heating rates from the level fluxes and pressures, in the fork's (nlay+1, ncol)
 //                          level-fastest flux layout.  Two forms, both term by term:
@@ -25,7 +28,7 @@
 
 namespace rrtmgpnn {
 
-constexpr int kBcCols = 16, kSwBoundaryMaxG = 1024;
+constexpr int kBcCols = 16;
 
 // toa_src(igpt, icol) = solar_source(igpt) for every column (gas_optics_ext), so every column's def_tsi is the same
 // sequential sum: one lane forms it per block, over the source staged in LDS (a sum over dependent global loads took
@@ -70,17 +73,23 @@ __global__ void __launch_bounds__(256) sw_boundary_kernel(int ngpt, int ncol, co
   }
 }
 
+SwBcDev sw_boundary_device(const SwBc *bc)
+{
+  // deg_to_rad = acos(-1._wp) / 180._wp in working precision (rrtmgp_rfmip_sw.F90:106); the usecol bound
+  // 90 - 2 spacing(90) = 90 - 2^-16 (spacing(90.) = 2^-17 in fp32)
+  volatile float pi = 3.14159265358979323846f;
+  return SwBcDev{bc->solar_source, bc->tsi, bc->sfc_alb, bc->sza, pi / 180.0f, 90.0f - 2.0f * 0x1p-17f};
+}
+
 int launch_sw_boundary(rrtmgpnn_context *ctx, int ngpt, int ncol, const float *solar_source, const float *tsi,
                        const float *sfc_alb, const float *sza, float *toa, float *alb, float *mu0)
 {
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwBoundaryMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw_boundary_rfmip: ngpt > 1024");
-  // deg_to_rad = acos(-1._wp) / 180._wp in working precision (rrtmgp_rfmip_sw.F90:106); the usecol bound
-  // 90 - 2 spacing(90) = 90 - 2^-16 (spacing(90.) = 2^-17 in fp32)
-  volatile float pi = 3.14159265358979323846f;
-  const float deg_to_rad = pi / 180.0f, sza_max = 90.0f - 2.0f * 0x1p-17f;
+  const SwBc bc{solar_source, tsi, sfc_alb, sza, toa, alb, mu0};
+  const SwBcDev d = sw_boundary_device(&bc);
   hipLaunchKernelGGL(sw_boundary_kernel, dim3((unsigned)((ncol + kBcCols - 1) / kBcCols)), dim3(256), 0, ctx->stream,
-                     ngpt, ncol, solar_source, tsi, sfc_alb, sza, deg_to_rad, sza_max, toa, alb, mu0);
+                     ngpt, ncol, solar_source, tsi, sfc_alb, sza, d.deg_to_rad, d.sza_max, toa, alb, mu0);
   RRTMGPNN_LAUNCH_CHECK("sw_boundary_kernel");
   return RRTMGPNN_OK;
 }

@@ -725,7 +725,8 @@ static void sw_launch(rrtmgpnn_context *ctx, size_t lds, int threads, int ngpt, 
 int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int top_at_1, const float *inc_flux,
                       const float *inc_flux_dif, const float *tau, const float *ssa, const float *g, const float *mu0,
                       const float *alb_dir, const float *alb_dif, const BandArgs *bands, const float *tau_bnd,
-                      const float *ssa_bnd, const float *g_bnd, float *flux_up, float *flux_dn, float *flux_dir)
+                      const float *ssa_bnd, const float *g_bnd, float *flux_up, float *flux_dn, float *flux_dir,
+                      const SwBc *bc)
 {
   if (ncol == 0) return RRTMGPNN_OK;
   if (ngpt > kSwMaxG) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: too many g-points");
@@ -742,6 +743,19 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (gpt && inc) return fail(RRTMGPNN_ERR_UNSUPPORTED, "sw solver: g-point outputs with a fused increment");
   const bool ck = (ngpt % 2) == 0 && (mode == 3 || mode == 0 || gpt);
   const bool x2 = !ck && (ngpt % 2) == 0 && mode != 1;
+  // the RFMIP boundary conditions (rrtmgpnn_sw_solver_2stream_rfmip): formed in the checkpointed kernel's prologue;
+  // the other kernels read them from memory, formed there first by sw_boundary_kernel
+  SwBcDev bcd{};
+  if (bc && ck) {
+    bcd = sw_boundary_device(bc);
+  } else if (bc) {
+    if (int rc = launch_sw_boundary(ctx, ngpt, ncol, bc->solar_source, bc->tsi, bc->sfc_alb, bc->sza, bc->toa, bc->alb,
+                                    bc->mu0))
+      return rc;
+    inc_flux = bc->toa;
+    alb_dir = alb_dif = bc->alb;
+    mu0 = bc->mu0;
+  }
   void *ws = nullptr;
   const size_t nlp = x2 ? sw_2stream_x2_layer_planes(inc) : (inc ? 3 : 0);
   const bool small = ck && sw_ck_small(ctx, ngpt, ncol, g != nullptr, inc, gpt), nn = !g && !inc && !gpt;
@@ -765,7 +779,8 @@ int launch_sw_2stream(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, int t
   if (rc) return rc;
   if (ck)
     return launch_sw_2stream_ck(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
-                                alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir, planes);
+                                alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir, planes,
+                                bc ? &bcd : nullptr);
   if (x2)
     return launch_sw_2stream_x2(ctx, ngpt, nlay, ncol, top_at_1, inc_flux, inc_flux_dif, tau, ssa, g, mu0, alb_dir,
                                 alb_dif, bands, tau_bnd, ssa_bnd, g_bnd, ws, flux_up, flux_dn, flux_dir);

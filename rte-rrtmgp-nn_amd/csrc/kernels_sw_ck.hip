@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(512, WAVES)
                          const float *__restrict__ tau_bnd, const float *__restrict__ ssa_bnd,
                          const float *__restrict__ g_bnd, float *__restrict__ ws, float *__restrict__ flux_up,
                          float *__restrict__ flux_dn, float *__restrict__ flux_dir, float *__restrict__ gpt_up,
-                         float *__restrict__ gpt_dn, float *__restrict__ gpt_dir)
+                         float *__restrict__ gpt_dn, float *__restrict__ gpt_dir, SwBcDev bc)
 {
   static_assert(R % K == 0, "the flux ring must hold whole chunks");
   constexpr bool kG0 = !kHasG && !kInc;  // g is the literal 0 (the NN path)
@@ -208,6 +208,12 @@ __global__ void __launch_bounds__(512, WAVES)
   float *ring = smem + kExpTabFloats + (size_t)c * 3 * R * rs;
   uint64_t *etab = (uint64_t *)(smem + kExpTabOff);
   load_exp_table(etab);
+  // bc.tsi != NULL: the RFMIP driver's boundary conditions formed here (sw_boundary_kernel's expressions, same bits):
+  // the solar source is staged in the ring's LDS, which pass 3 first writes after a barrier below
+  const bool bcf = bc.tsi != nullptr;
+  float *const bsrc = smem + kExpTabFloats;
+  if (bcf)
+    for (int i = threadIdx.x; i < ngpt; i += blockDim.x) bsrc[i] = bc.solar_source[i];
   __syncthreads();
   const int dl_dn = top_at_1 ? 1 : -1;
   const uint32_t row = 4u * (uint32_t)ngpt;
@@ -245,12 +251,34 @@ __global__ void __launch_bounds__(512, WAVES)
     } else if constexpr (NPL == 2) return (f2){a.ld1(vb0, brow * (uint32_t)l), a.ld1(vb1, brow * (uint32_t)l)};
     else return a.ld1(vb0, brow * (uint32_t)l);
   };
-  const float mu0 = mu0p[icol], mu0_inv = 1.0f / mu0;
+  // mu0 = merge(cos(sza * deg_to_rad), 1, usecol) (rrtmgp_rfmip_sw.F90:236-238, 421-427) or the caller's
+  const float sza = bcf ? bc.sza[icol] : 0.0f;
+  const float mu0 = bcf ? (sza < bc.sza_max ? ref_cosf(sza * bc.deg_to_rad) : 1.0f) : mu0p[icol];
+  const float mu0_inv = 1.0f / mu0;
   // j counts layers from the top (clamped to the last layer); the result is the array layer
   auto lay = [&](int j) { return top_at_1 ? min(j, nlay - 1) : nlay - 1 - min(j, nlay - 1); };
   auto ld_col = [&](const float *p) -> V { return on ? *(const V *)(p + gc + (size_t)ngpt * icol) : (V)0.0f; };
   const int top = top_at_1 ? 0 : nlay;
-  const V Ftop = ld_col(inc_flux) * mu0;
+  // the incident flux toa = toa_src * tsi / def_tsi (rrtmgp_rfmip_sw.F90:403-418), def_tsi the source summed in g order
+  // by every lane (broadcast LDS reads; no barrier); or the caller's
+  auto bc_toa = [&]() -> V {
+    float s = 0.0f;
+    int i = 0;
+    for (; i + 8 <= ngpt; i += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) v[j] = bsrc[i + j];
+#pragma unroll
+      for (int j = 0; j < 8; j++) s = s + v[j];
+    }
+    for (; i < ngpt; i++) s = s + bsrc[i];
+    const float t = bc.tsi[icol];
+    if constexpr (NPL == 2) return on ? (V){bsrc[gc] * t / s, bsrc[gc + 1] * t / s} : (V)0.0f;
+    else return on ? (V)(bsrc[gc] * t / s) : (V)0.0f;
+  };
+  const V Ftop = (bcf ? bc_toa() : ld_col(inc_flux)) * mu0;
+  // the surface albedo, spectrally constant (rrtmgp_rfmip_sw.F90:428-433), or the caller's per g-point
+  const V alb_bc = on && bcf ? (V)bc.sfc_alb[icol] : (V)0.0f;
 
   // one chunk's optical properties (the band increment is formed as they are used, as inc_2str2 does), with the
   // checkpoints the pass reads for it: fb the beam at the chunk's top (pass 2), ae / se the albedo and source at its
@@ -358,8 +386,8 @@ __global__ void __launch_bounds__(512, WAVES)
     walk(load1, body1, np1, [](int i) { return i; }, A1, B1);
   }
   // ---- pass 2: bottom -> top adding; albedo / source checkpoint at every chunk top and at the surface ----
-  V alb_b = ld_col(alb_dif);
-  V src_b = Fd * ld_col(alb_dir);
+  V alb_b = bcf ? alb_bc : ld_col(alb_dif);
+  V src_b = Fd * (bcf ? alb_bc : ld_col(alb_dir));
   CW.stv(alb_b, vWs, sA0 + row * (uint32_t)nck);
   CW.stv(src_b, vWs, sS0 + row * (uint32_t)nck);
   {
@@ -444,6 +472,7 @@ __global__ void __launch_bounds__(512, WAVES)
   // 4: the flush's cost is its own latency inside each block, not the whole chip flushing at once.)
   constexpr int M = R / K;
   V Fdn = inc_dif ? ld_col(inc_dif) : (V)0.0f;
+  if (bcf) __syncthreads();  // every lane has read the staged solar source before the ring is written
   put(Fdn * alb_b + src_b, Fdn, Ftop, 0, top, true);
   flush(1, top, 1);
   {
@@ -541,11 +570,13 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
                          const float *inc_flux_dif, const float *tau, const float *ssa, const float *g,
                          const float *mu0, const float *alb_dir, const float *alb_dif, const BandArgs *bands,
                          const float *tau_bnd, const float *ssa_bnd, const float *g_bnd, void *ws, float *flux_up,
-                         float *flux_dn, float *flux_dir, bool planes)
+                         float *flux_dn, float *flux_dir, bool planes, const SwBcDev *bc)
 {
   const int ncb2 = 2 * (ngpt / 2) <= 512 ? 2 : 1;  // two columns per block where 512 lanes hold them
   const BandArgs nob{};
   const BandArgs &b = bands ? *bands : nob;
+  const SwBcDev nobc{};  // tsi == NULL: the caller's inc_flux, mu0 and albedos
+  const SwBcDev &bcd = bc ? *bc : nobc;
   const auto &ex = ctx->extras;
   // npl g-points per lane, ncb columns per block
   auto go = [&](auto kern, const float *tb, const float *sb, const float *gb, int ring = kCkRing, int npl = 2) -> int {
@@ -560,7 +591,7 @@ int launch_sw_2stream_ck(rrtmgpnn_context *ctx, int ngpt, int nlay, int ncol, in
       if (int rc = raise_lds_limit((const void *)kern)) return rc;
     hipLaunchKernelGGL(kern, grid, block, lds, ctx->stream, ngpt, nlay, ncol, top_at_1, ncb, inc_flux, inc_flux_dif,
                        tau, ssa, g, mu0, alb_dir, alb_dif, b, tb, sb, gb, (float *)ws, flux_up, flux_dn, flux_dir,
-                       ex.gpt_up, ex.gpt_dn, ex.gpt_dir);
+                       ex.gpt_up, ex.gpt_dn, ex.gpt_dir, bcd);
     RRTMGPNN_LAUNCH_CHECK("sw_2stream_ck_kernel");
     return RRTMGPNN_OK;
   };

@@ -110,6 +110,8 @@ SIGNATURES = {
     "rrtmgpnn_increment": (c_int, [c_vp, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_delta_scale_2str": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp]),
     "rrtmgpnn_sw_boundary_rfmip": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rrtmgpnn_sw_solver_2stream_rfmip": (c_int, [c_vp, c_int, c_int, c_int, c_int] + [c_vp] * 7
+                                         + [c_int, P(c_int)] + [c_vp] * 9),
     "rrtmgpnn_file_open": (c_int, [c_char_p, P(c_vp)]),
     "rrtmgpnn_file_close": (c_int, [c_vp]),
     "rrtmgpnn_file_nvars": (c_int, [c_vp, P(c_int)]),

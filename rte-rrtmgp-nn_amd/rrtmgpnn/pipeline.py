@@ -17,8 +17,9 @@ What one step computes is exactly the drivers' per-block work
 compute_nn_inputs, get_col_dry, both NN models per stream with post-processing, the Planck sources,
 the band->g emissivity expansion, the SW boundary conditions (gas_optics_ext's incident flux
 renormalised to each column's TSI, the per-g-point surface albedo and mu0 = cos(sza), formed from the
-block's TSI, albedo and zenith angle: rrtmgpnn_sw_boundary_rfmip, rrtmgp_rfmip_sw.F90:403-434), both
-solvers and the broadband reductions.  The step's inputs are the driver's per-column state; the only
+block's TSI, albedo and zenith angle, rrtmgp_rfmip_sw.F90:403-434: in the fused step inside the SW
+solver, rrtmgpnn_sw_solver_2stream_rfmip; unfused rrtmgpnn_sw_boundary_rfmip), both solvers and the
+broadband reductions.  The step's inputs are the driver's per-column state; the only
 data prepared once are the model's (network weights, the Planck table, solar_source after set_tsi).
 The unfused step computes col_dry once and shares it between LW and SW (same h2o and plev).
 
@@ -125,7 +126,8 @@ class ClearSkyStep:
         self.sw = sw
         if sw:
             self.tau_sw, self.ssa_sw = f(ncol, nlay, self.ng_sw), f(ncol, nlay, self.ng_sw)
-            # the SW boundary conditions, formed every step (rrtmgpnn_sw_boundary_rfmip)
+            # the SW boundary conditions, formed every step (unfused: rrtmgpnn_sw_boundary_rfmip; fused: in the SW
+            # solver, which uses these only as scratch when its kernel does not form them itself)
             self.toa, self.alb, self.mu0 = f(ncol, self.ng_sw), f(ncol, self.ng_sw), f(ncol)
         if not fused:  # arrays the fused step never materialises
             self.lev_src = f(ncol, nlay + 1, self.ng_lw)
@@ -224,13 +226,15 @@ class ClearSkyStep:
             self.calls = [c for c in self.calls if c[0] != "cloud_optics_sw"]
             self._finish(False)
             return
-        # the driver's SW boundary conditions, at the head of the SW chain.  Round 6: on the LW stream beside the SW
-        # network, with the SW solver waiting for it, the C3 step measured 0.497 ms against 0.43: the extra edge into the
-        # SW solver let the LW network take the CUs first (gpurun_out r06 bench2_noc5 -> profiles/r06)
-        # (unfused: after get_col_dry, the call the SW stream forks after)
-        self.calls.insert(0 if fused else 1, ("sw_boundary", L.rrtmgpnn_sw_boundary_rfmip,
-                              (c, self.ng_sw, ncol, p(self.solar_source), p(self.tsi), p(self.sfc_alb), p(self.sza),
-                               p(self.toa), p(self.alb), p(self.mu0))))
+        # the driver's SW boundary conditions.  Fused: formed in the SW solver's prologue
+        # (rrtmgpnn_sw_solver_2stream_rfmip).  Round 6 before that: a kernel at the head of the SW chain (7.7 us at C3);
+        # on the LW stream beside the SW network, with the SW solver waiting for it, the C3 step measured 0.497 ms against
+        # 0.43 (the extra edge into the SW solver let the LW network take the CUs first; profiles/r06/README.md).
+        # Unfused (the class layer's calls): the kernel after get_col_dry, the call the SW stream forks after
+        if not fused:
+            self.calls.insert(1, ("sw_boundary", L.rrtmgpnn_sw_boundary_rfmip,
+                                  (c, self.ng_sw, ncol, p(self.solar_source), p(self.tsi), p(self.sfc_alb),
+                                   p(self.sza), p(self.toa), p(self.alb), p(self.mu0))))
         # g == NULL: the NN path's asymmetry parameter is identically zero (quirk B-6); the SW kernels take
         # that as a literal 0 instead of writing and re-reading a zero array (same fluxes, bit for bit)
         g_sw = None if fused else p(self.g_sw)
@@ -263,12 +267,16 @@ class ClearSkyStep:
                      (c, ncol, nlay, self.ng_sw, self.nb_sw, self._lims_sw, p(self.tau_sw), p(self.ssa_sw), g_sw,
                       p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw))),
                 ]
-        if self.allsky and fused:  # clouds%increment(atmos) fused into the solver (rrtmgpnn_sw_solver_2stream_inc)
+        if fused:
+            # the boundary conditions and (all sky) clouds%increment(atmos) fused into the solver
+            # (rrtmgpnn_sw_solver_2stream_rfmip; same bits as sw_boundary_rfmip + sw_solver_2stream[_inc])
+            bnd = (self.nb_sw, self._lims_sw, p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw)) \
+                if self.allsky else (0, None, None, None, None)
             self.calls += [
-                ("sw_solver", L.rrtmgpnn_sw_solver_2stream_inc,
-                 (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.toa), None, p(self.tau_sw), p(self.ssa_sw), None,
-                  self.nb_sw, self._lims_sw, p(self.cld_tau_sw), p(self.cld_ssa_sw), p(self.cld_g_sw), p(self.mu0),
-                  p(self.alb), p(self.alb), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
+                ("sw_solver", L.rrtmgpnn_sw_solver_2stream_rfmip,
+                 (c, self.ng_sw, nlay, ncol, self.top_at_1, p(self.solar_source), p(self.tsi), p(self.sfc_alb),
+                  p(self.sza), p(self.tau_sw), p(self.ssa_sw), None) + bnd
+                 + (p(self.toa), p(self.alb), p(self.mu0), p(self.sw_up), p(self.sw_dn), p(self.sw_dir))),
             ]
         else:
             self.calls += [

@@ -299,3 +299,61 @@ def test_sw_boundary_conditions_match_the_driver(dev, which):
     np.testing.assert_array_equal(mu0.cpu().numpy().view(np.uint32), prob["mu0"].view(np.uint32))
     np.testing.assert_array_equal(toa.cpu().numpy().view(np.uint32), data.toa_flux(prob, kd).view(np.uint32))
     np.testing.assert_array_equal(alb.cpu().numpy(), np.repeat(prob["sfc_alb"][:, None], ngpt, axis=1))
+
+
+@pytest.mark.parametrize("case", ["clear_small", "clear_large", "g", "allsky"])
+@pytest.mark.parametrize("top_at_1", [True, False])
+def test_sw_solver_rfmip_equals_boundary_then_solver(dev, case, top_at_1, sw_kernel):
+    """rrtmgpnn_sw_solver_2stream_rfmip (the boundary conditions formed in the checkpointed solver's prologue; the
+    other kernels get them from sw_boundary_kernel first) == rrtmgpnn_sw_boundary_rfmip then
+    rrtmgpnn_sw_solver_2stream[_inc], bit for bit: the small-grid and large-grid clear-sky instances (g = NULL), a
+    non-zero g, the fused cloud increment; night columns (mu0 = 1) among random zenith angles."""
+    from rrtmgpnn import _lib, data
+    from rrtmgpnn._lib import check, int_array
+    from rrtmgpnn.api import context
+    L = _lib.lib()
+    ks = data.load_kdist("sw")
+    ng, nb = int(ks["ngpt"]), int(ks["nband"])
+    ncol, nlay = {"clear_small": (300, 40), "clear_large": (3001, 12), "g": (257, 30), "allsky": (190, 33)}[case]
+    rng = np.random.default_rng(11 + 2 * top_at_1 + len(case))
+    t = lambda a: T(a, dev)  # noqa: E731
+    tau = t(rng.lognormal(-2, 2, (ncol, nlay, ng)))
+    ssa = t(rng.uniform(0, 1, (ncol, nlay, ng)))
+    gg = t(rng.uniform(0, 0.8, (ncol, nlay, ng))) if case == "g" else None
+    sol = t(data.set_tsi(ks["solar_source"], 1361.0))
+    sza = t(np.where(rng.uniform(size=ncol) < 0.15, rng.uniform(90, 180, ncol), rng.uniform(0, 89.9, ncol)))
+    tsi = t(rng.uniform(1300, 1400, ncol))
+    alb = t(rng.uniform(0, 1, ncol))
+    if case == "allsky":
+        lims = int_array(ks["band_lims_gpt"].ravel())
+        cl = rng.uniform(size=(ncol, nlay, nb)) < 0.4
+        s = (ncol, nlay, nb)
+        bnd = [t(np.where(cl, rng.lognormal(0, 1, s), 0)), t(np.where(cl, rng.uniform(0.5, 1, s), 0)),
+               t(np.where(cl, rng.uniform(0, 0.9, s), 0))]
+        bargs = (nb, lims) + tuple(b.data_ptr() for b in bnd)
+    else:
+        bargs = (0, None, None, None, None)
+    f = lambda *s: torch.full(s, float("nan"), device=dev)  # noqa: E731
+    toa, albg, mu0 = f(ncol, ng), f(ncol, ng), f(ncol)
+    ctx = context(0).h
+    gp = gg.data_ptr() if gg is not None else None
+    outs = [[f(ncol, nlay + 1) for _ in range(3)] for _ in range(2)]
+    check(L.rrtmgpnn_sw_solver_2stream_rfmip(ctx, ng, nlay, ncol, int(top_at_1), sol.data_ptr(), tsi.data_ptr(),
+                                             alb.data_ptr(), sza.data_ptr(), tau.data_ptr(), ssa.data_ptr(), gp, *bargs,
+                                             toa.data_ptr(), albg.data_ptr(), mu0.data_ptr(),
+                                             *[o.data_ptr() for o in outs[0]]), "sw_solver_2stream_rfmip")
+    check(L.rrtmgpnn_sw_boundary_rfmip(ctx, ng, ncol, sol.data_ptr(), tsi.data_ptr(), alb.data_ptr(), sza.data_ptr(),
+                                       toa.data_ptr(), albg.data_ptr(), mu0.data_ptr()), "sw_boundary_rfmip")
+    if case == "allsky":
+        check(L.rrtmgpnn_sw_solver_2stream_inc(ctx, ng, nlay, ncol, int(top_at_1), toa.data_ptr(), None, tau.data_ptr(),
+                                               ssa.data_ptr(), gp, *bargs, mu0.data_ptr(), albg.data_ptr(),
+                                               albg.data_ptr(), *[o.data_ptr() for o in outs[1]]), "sw_solver_2stream_inc")
+    else:
+        check(L.rrtmgpnn_sw_solver_2stream(ctx, ng, nlay, ncol, int(top_at_1), toa.data_ptr(), None, tau.data_ptr(),
+                                           ssa.data_ptr(), gp, mu0.data_ptr(), albg.data_ptr(), albg.data_ptr(),
+                                           *[o.data_ptr() for o in outs[1]]), "sw_solver_2stream")
+    torch.cuda.synchronize()
+    assert (mu0 == 1).any() and (mu0 < 1).any()
+    for a, b, name in zip(outs[0], outs[1], ("up", "dn", "dir")):
+        assert not torch.isnan(a).any(), name
+        np.testing.assert_array_equal(a.cpu().numpy().view(np.uint32), b.cpu().numpy().view(np.uint32), err_msg=name)
