@@ -45,8 +45,8 @@ def main():
     A, B = st.ctx.stream, st.ctx2.stream
     swn = ("sw_boundary", "cloud_optics_sw", "delta_scale_sw", "predict_nn_sw", "sw_solver")
     lw = [(n, f, a) for n, f, a in st.calls if n not in swn]
-    # the SW boundary conditions at the head of the SW stream here (in the step they run on the LW stream, beside the
-    # SW network): the pipelined SW chain then depends on nothing of the LW stream
+    # a separate SW boundary kernel (trees before the fused SW solver entry) goes at the head of the SW stream, so the
+    # pipelined SW chain depends on nothing of the LW stream; the fused step forms them inside its SW solver
     sw = [(n, f, ((st.ctx2.h,) + tuple(a[1:])) if n == "sw_boundary" else a) for n, f, a in st.calls if n in swn]
     gate_after = "predict_nn_sw"
     evs = [torch.cuda.Event() for _ in range(4)]
