@@ -502,7 +502,7 @@ class ClearSkyStep:
         return g
 
     def capture_chains(self):
-        """A stream of blocks (run_blocks): the SW chain (boundary conditions, network, solver) and the LW chain
+        """A stream of blocks (run_blocks): the SW chain (network, solver with the boundary conditions) and the LW chain
         (network, solver) captured as two hipGraphs, each on its own context's stream and alone -- no gate or join
         between them."""
         if not (self.overlap and self.sw):
