@@ -301,7 +301,7 @@ def test_sw_boundary_conditions_match_the_driver(dev, which):
     np.testing.assert_array_equal(alb.cpu().numpy(), np.repeat(prob["sfc_alb"][:, None], ngpt, axis=1))
 
 
-@pytest.mark.parametrize("case", ["clear_small", "clear_large", "g", "allsky"])
+@pytest.mark.parametrize("case", ["clear_small", "clear_large", "g", "allsky", "one_column", "one_layer"])
 @pytest.mark.parametrize("top_at_1", [True, False])
 def test_sw_solver_rfmip_equals_boundary_then_solver(dev, case, top_at_1, sw_kernel):
     """rrtmgpnn_sw_solver_2stream_rfmip (the boundary conditions formed in the checkpointed solver's prologue; the
@@ -314,7 +314,8 @@ def test_sw_solver_rfmip_equals_boundary_then_solver(dev, case, top_at_1, sw_ker
     L = _lib.lib()
     ks = data.load_kdist("sw")
     ng, nb = int(ks["ngpt"]), int(ks["nband"])
-    ncol, nlay = {"clear_small": (300, 40), "clear_large": (3001, 12), "g": (257, 30), "allsky": (190, 33)}[case]
+    ncol, nlay = {"clear_small": (300, 40), "clear_large": (3001, 12), "g": (257, 30), "allsky": (190, 33),
+                  "one_column": (1, 7), "one_layer": (5, 1)}[case]
     rng = np.random.default_rng(11 + 2 * top_at_1 + len(case))
     t = lambda a: T(a, dev)  # noqa: E731
     tau = t(rng.lognormal(-2, 2, (ncol, nlay, ng)))
@@ -353,7 +354,8 @@ def test_sw_solver_rfmip_equals_boundary_then_solver(dev, case, top_at_1, sw_ker
                                            ssa.data_ptr(), gp, mu0.data_ptr(), albg.data_ptr(), albg.data_ptr(),
                                            *[o.data_ptr() for o in outs[1]]), "sw_solver_2stream")
     torch.cuda.synchronize()
-    assert (mu0 == 1).any() and (mu0 < 1).any()
+    if ncol > 20:
+        assert (mu0 == 1).any() and (mu0 < 1).any()
     for a, b, name in zip(outs[0], outs[1], ("up", "dn", "dir")):
         assert not torch.isnan(a).any(), name
         np.testing.assert_array_equal(a.cpu().numpy().view(np.uint32), b.cpu().numpy().view(np.uint32), err_msg=name)
