@@ -275,9 +275,24 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
   constexpr bool kPair = MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR;
   extern __shared__ floatx4 lds4[];
   {
+    // The weight images into LDS, kStage loads in flight per thread: a load-then-store loop waits out every load's
+    // latency in turn (the LW pair's 108 KB took 13 such round trips per block before the first tile)
+    constexpr int kStage = 8;
     const int n4 = (a.imgA_floats + (kPair ? a.imgB_floats : 0)) / 4, nA4 = a.imgA_floats / 4;
     const floatx4 *srcA = (const floatx4 *)a.imgA, *srcB = (const floatx4 *)a.imgB;
-    for (int i = threadIdx.x; i < n4; i += blockDim.x) lds4[i] = i < nA4 ? srcA[i] : srcB[i - nA4];
+    for (int i0 = threadIdx.x; i0 < n4; i0 += kStage * (int)blockDim.x) {
+      floatx4 v[kStage];
+#pragma unroll
+      for (int u = 0; u < kStage; u++) {
+        const int i = min(i0 + u * (int)blockDim.x, n4 - 1);  // clamped: every load issues, past-the-end ones unused
+        v[u] = i < nA4 ? srcA[i] : srcB[i - nA4];
+      }
+#pragma unroll
+      for (int u = 0; u < kStage; u++) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < n4) lds4[i] = v[u];
+      }
+    }
   }
   __syncthreads();
   const float *imgA = (const float *)lds4;

@@ -171,11 +171,31 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     // band Planck values for this column: B_b(tlay(l)) at [b][l], B_b(tlev(l)) at [b][nlay+l], B_b(tsfc) at
     // [nbnd*brow + b]; interpolate1D of compute_Planck_source_nn
     const float *tl = pl.tlay + (size_t)nlay * icol, *tv = pl.tlev + (size_t)nlev * icol;
-    for (int i = threadIdx.x; i < bands.nbnd * (brow + 1); i += blockDim.x) {
-      const int b = i < bands.nbnd * brow ? i / brow : i - bands.nbnd * brow;
-      const int k = i < bands.nbnd * brow ? i - b * brow : -1;
-      const float T = k < 0 ? pl.tsfc[icol] : (k < nlay ? tl[k] : tv[k - nlay]);
-      btab[i] = interp1d(T, pl.tmin, pl.tdelta, pl.ntemp, pl.totplnk + (size_t)pl.ntemp * b);
+    // kBtabU entries per thread per round, their loads issued together: the temperatures, then the table pairs (a
+    // loop of one entry per round waits out two dependent load latencies per entry, ~16 per block at C3)
+    constexpr int kBtabU = 8;
+    const int ntab = bands.nbnd * (brow + 1), nrow = bands.nbnd * brow;
+    for (int i0 = threadIdx.x; i0 < ntab; i0 += kBtabU * (int)blockDim.x) {
+      float T[kBtabU];
+      int bb[kBtabU];
+#pragma unroll
+      for (int u = 0; u < kBtabU; u++) {
+        const int i = min(i0 + u * (int)blockDim.x, ntab - 1);  // clamped: past-the-end entries are not stored
+        const int b = i < nrow ? i / brow : i - nrow;
+        const int k = i < nrow ? i - b * brow : -1;
+        bb[u] = b;
+        const float *p = k < 0 ? pl.tsfc + icol : (k < nlay ? tl + k : tv + (k - nlay));  // one load, no branch
+        T[u] = *p;
+      }
+      float v[kBtabU];
+#pragma unroll
+      for (int u = 0; u < kBtabU; u++)
+        v[u] = interp1d(T[u], pl.tmin, pl.tdelta, pl.ntemp, pl.totplnk + (size_t)pl.ntemp * bb[u]);
+#pragma unroll
+      for (int u = 0; u < kBtabU; u++) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < ntab) btab[i] = v[u];
+      }
     }
     const int b = band_of(bands, gc);
     bl = btab + (size_t)b * brow;
