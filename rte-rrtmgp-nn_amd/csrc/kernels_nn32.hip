@@ -274,27 +274,6 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
 {
   constexpr bool kPair = MODE == MLP_LW_PAIR || MODE == MLP_SW_PAIR;
   extern __shared__ floatx4 lds4[];
-  {
-    // The weight images into LDS, kStage loads in flight per thread: a load-then-store loop waits out every load's
-    // latency in turn (the LW pair's 108 KB took 13 such round trips per block before the first tile)
-    constexpr int kStage = 8;
-    const int n4 = (a.imgA_floats + (kPair ? a.imgB_floats : 0)) / 4, nA4 = a.imgA_floats / 4;
-    const floatx4 *srcA = (const floatx4 *)a.imgA, *srcB = (const floatx4 *)a.imgB;
-    for (int i0 = threadIdx.x; i0 < n4; i0 += kStage * (int)blockDim.x) {
-      floatx4 v[kStage];
-#pragma unroll
-      for (int u = 0; u < kStage; u++) {
-        const int i = min(i0 + u * (int)blockDim.x, n4 - 1);  // clamped: every load issues, past-the-end ones unused
-        v[u] = i < nA4 ? srcA[i] : srcB[i - nA4];
-      }
-#pragma unroll
-      for (int u = 0; u < kStage; u++) {
-        const int i = i0 + u * (int)blockDim.x;
-        if (i < n4) lds4[i] = v[u];
-      }
-    }
-  }
-  __syncthreads();
   const float *imgA = (const float *)lds4;
   const float *imgB = imgA + a.imgA_floats;
   float *cds = (float *)lds4 + a.imgA_floats + (kPair ? a.imgB_floats : 0);
@@ -384,6 +363,29 @@ __global__ __launch_bounds__(NT, WPE) void mlp32_kernel(Mlp32Args a)
 
   float xn[NR];  // the next tile's inputs, loaded before this tile's stores
   load_x(blockIdx.x * nwaves + wave, xn);
+  {
+    // The weight images into LDS, kStage loads in flight per thread, with the first tile's inputs already on their way
+    // (issued above: after the barrier they would wait for the staging).  A load-then-store loop waits out every
+    // load's latency in turn: the LW pair's 108 KB took 13 such round trips per block before the first tile.  C3
+    // (alone, round 6): LW network -4 %; the first tile's loads first: steps -0.5 % (profiles/r06/mlpstage_*.txt)
+    constexpr int kStage = 8;
+    const int n4 = (a.imgA_floats + (kPair ? a.imgB_floats : 0)) / 4, nA4 = a.imgA_floats / 4;
+    const floatx4 *srcA = (const floatx4 *)a.imgA, *srcB = (const floatx4 *)a.imgB;
+    for (int i0 = threadIdx.x; i0 < n4; i0 += kStage * (int)blockDim.x) {
+      floatx4 v[kStage];
+#pragma unroll
+      for (int u = 0; u < kStage; u++) {
+        const int i = min(i0 + u * (int)blockDim.x, n4 - 1);  // clamped: every load issues, past-the-end ones unused
+        v[u] = i < nA4 ? srcA[i] : srcB[i - nA4];
+      }
+#pragma unroll
+      for (int u = 0; u < kStage; u++) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < n4) lds4[i] = v[u];
+      }
+    }
+  }
+  __syncthreads();
   for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += tstride) {
     float xv[NR];
 #pragma unroll

@@ -166,6 +166,31 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   const ColArr Tinc(kInc ? tau_bnd : tau, kInc ? (size_t)bands.nbnd * nlay * icol : 0, irow * nlay);
   auto ld_inc = [&](int l) { return kInc ? Tinc.ld(vb, irow * (uint32_t)l) : 0.0f; };
   auto tau_of = [&](float t, float ti) { return kInc ? t + ti : t; };
+  // the value to load for lev index li: lev_source(li), or pfrac(min(li, nlay-1)) when fused
+  auto lev_ld = [&](int li) {
+    return kFused ? Tlay.ld(vg, row * (uint32_t)min(li, nlay - 1)) : Tlev.ld(vg, row * (uint32_t)li);
+  };
+  // j-th layer from the top is l = lay_dn(j)
+  auto lay_dn = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
+  // The first angle's first kPF layers, the surface Planck fraction, the emissivity and the incident flux are loaded
+  // here, ahead of the prologue's barriers (which would hold the loads back until the Planck table is built).  Only in
+  // the fused clear-sky instance: in the others the early layers' registers spill (64 VGPRs, the 8-wave bound).
+  constexpr bool kEarly = kFused && !kInc;
+  float pt0[kPF], py0[kPF], pv0[kPF], pi0[kPF];
+#pragma unroll
+  for (int p = 0; p < kPF; p++) {
+    const int l = lay_dn(min(p, nlay - 1));
+    pt0[p] = kEarly ? Ttau.ld(vg, row * l) : 0.0f;
+    py0[p] = kEarly ? Tlay.ld(vg, row * l) : 0.0f;
+    pi0[p] = 0.0f;
+    pv0[p] = (kEarly && !kFused) ? lev_ld(l + 1) : 0.0f;
+  }
+  const float ysfc = kFused ? Tlay.ld(vg, row * (uint32_t)(pl.sfc_lay - 1)) : 0.0f;
+  // emissivity per g-point, or (fused, emis_by_band) the band value rte_lw's expand would copy there
+  const float e = !on ? 0.0f
+                      : (kFused && pl.emis_by_band ? emis[band_of(bands, g) + (size_t)bands.nbnd * icol]
+                                                   : emis[g + (size_t)ngpt * icol]);
+  const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   float ss;
   if constexpr (kFused) {
     // band Planck values for this column: B_b(tlay(l)) at [b][l], B_b(tlev(l)) at [b][nlay+l], B_b(tsfc) at
@@ -200,17 +225,12 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     const int b = band_of(bands, gc);
     bl = btab + (size_t)b * brow;
     __syncthreads();
-    ss = Tlay.ld(vg, row * (uint32_t)(pl.sfc_lay - 1)) * btab[(size_t)bands.nbnd * brow + b];
+    ss = ysfc * btab[(size_t)bands.nbnd * brow + b];
   } else {
     __syncthreads();
     ss = on ? sfc[g + (size_t)ngpt * icol] : 0.0f;
   }
   const float tau_thresh = sqrtf(FLT_EPSILON);
-  // emissivity per g-point, or (fused, emis_by_band) the band value rte_lw's expand would copy there
-  const float e = !on ? 0.0f
-                      : (kFused && pl.emis_by_band ? emis[band_of(bands, g) + (size_t)bands.nbnd * icol]
-                                                   : emis[g + (size_t)ngpt * icol]);
-  const float inc = (on && inc_flux) ? inc_flux[g + (size_t)ngpt * icol] : 0.0f;
   const int top = top_at_1 ? 0 : nlay, sfcl = top_at_1 ? nlay : 0;
   // stage one level's value v = fac * radiance: slot r of the ring, or (kMulti) the per-g accumulator of plane q
   // (the radiance itself with ang.rad)
@@ -236,10 +256,6 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
   // layer source and the level source on the side given by `li` (lev index, 0..nlay)
   auto lay_src = [&](float y, int l) { return kFused ? y * bl[l] : y; };
   auto lev_src = [&](float v, int li) { return kFused ? v * bl[nlay + li] : v; };
-  // the value to load for lev index li: lev_source(li), or pfrac(min(li, nlay-1)) when fused
-  auto lev_ld = [&](int li) {
-    return kFused ? Tlay.ld(vg, row * (uint32_t)min(li, nlay - 1)) : Tlev.ld(vg, row * (uint32_t)li);
-  };
   float *pdn = part, *pup = part + (size_t)nlev * 4;
   const int dl_dn = top_at_1 ? 1 : -1;  // level index step going down
 
@@ -253,15 +269,21 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
     float I = inc / (2.0f * kPi * ang.w[imu]);
     put(fac * I, I, 0, 0, top, acc);
     flush(pdn, 1, top, 1);
-    // downward: lw_transport_noscat_dn (:982-1009); j-th layer from the top is l = lay_dn(j)
-    auto lay_dn = [&](int j) { return top_at_1 ? j : nlay - 1 - j; };
+    // downward: lw_transport_noscat_dn (:982-1009)
     {
       float pt[kPF], py[kPF], pv[kPF], pi[kPF];
+      if (kEarly && imu == 0) {  // loaded ahead of the prologue
 #pragma unroll
-      for (int p = 0; p < kPF; p++) {
-        const int l = lay_dn(min(p, nlay - 1));
-        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
-        if constexpr (!kFused) pv[p] = lev_ld(l + 1);
+        for (int p = 0; p < kPF; p++) {
+          pt[p] = pt0[p]; py[p] = py0[p]; pi[p] = pi0[p]; pv[p] = pv0[p];
+        }
+      } else {
+#pragma unroll
+        for (int p = 0; p < kPF; p++) {
+          const int l = lay_dn(min(p, nlay - 1));
+          pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
+          if constexpr (!kFused) pv[p] = lev_ld(l + 1);
+        }
       }
       // fused: lev(l+1)'s Planck fraction pfrac(min(l+1, nlay-1)) is a neighbour's in walk order, already loaded --
       // the next layer's (top_at_1: in the other prefetch slot) or the previous one's (bottom first) -- and the
