@@ -214,7 +214,9 @@ __global__ void __launch_bounds__(512, WAVES)
   float *const bsrc = smem + kExpTabFloats;
   if (bcf)
     for (int i = threadIdx.x; i < ngpt; i += blockDim.x) bsrc[i] = bc.solar_source[i];
-  __syncthreads();
+  // small-grid instance: the barrier comes after pass 1's first loads (kEarly below)
+  constexpr bool kEarly = !kInc && WAVES == kCkWavesSmall;
+  if constexpr (!kEarly) __syncthreads();
   const int dl_dn = top_at_1 ? 1 : -1;
   const uint32_t row = 4u * (uint32_t)ngpt;
   const uint32_t vL = 4u * (uint32_t)gc + (uint32_t)c * row * nlay;
@@ -259,6 +261,29 @@ __global__ void __launch_bounds__(512, WAVES)
   auto lay = [&](int j) { return top_at_1 ? min(j, nlay - 1) : nlay - 1 - min(j, nlay - 1); };
   auto ld_col = [&](const float *p) -> V { return on ? *(const V *)(p + gc + (size_t)ngpt * icol) : (V)0.0f; };
   const int top = top_at_1 ? 0 : nlay;
+  // the surface albedo, spectrally constant (rrtmgp_rfmip_sw.F90:428-433), or the caller's per g-point
+  const V alb_bc = on && bcf ? (V)bc.sfc_alb[icol] : (V)0.0f;
+  // Pass 1 reads P1 = kCkP1 * K layers per step (little arithmetic per layer: it needs many loads in flight).  In the
+  // small-grid instance (one round of blocks: every block's prologue is on the kernel's path) its first step's loads go
+  // out here, ahead of the prologue's barrier, which would hold them back until the exp table and the solar source are
+  // in LDS.  Round 6, C3: the solver alone -1.3 %; in the large clear-sky instance C5 steps +0.3 % (2 pairs), so not
+  // there (profiles/r06/swearly_*.txt)
+  constexpr int P1 = P1C * K;
+  struct Buf1 {
+    V t[P1];
+  } A1, B1;
+  auto load1 = [&](Buf1 &b, int c1) {
+#pragma unroll
+    for (int p = 0; p < P1; p++) {
+      const int l = lay(c1 * P1 + p);
+      b.t[p] = Ttau.ldv(vL, row * (uint32_t)l);
+      if constexpr (kInc) b.t[p] += ld_bnd(Bt, l);
+    }
+  };
+  if constexpr (kEarly) {
+    load1(A1, 0);
+    __syncthreads();
+  }
   // the incident flux toa = toa_src * tsi / def_tsi (rrtmgp_rfmip_sw.F90:403-418), def_tsi the source summed in g order
   // by every lane (broadcast LDS reads; no barrier); or the caller's
   auto bc_toa = [&]() -> V {
@@ -277,8 +302,6 @@ __global__ void __launch_bounds__(512, WAVES)
     else return on ? (V)(bsrc[gc] * t / s) : (V)0.0f;
   };
   const V Ftop = (bcf ? bc_toa() : ld_col(inc_flux)) * mu0;
-  // the surface albedo, spectrally constant (rrtmgp_rfmip_sw.F90:428-433), or the caller's per g-point
-  const V alb_bc = on && bcf ? (V)bc.sfc_alb[icol] : (V)0.0f;
 
   // one chunk's optical properties (the band increment is formed as they are used, as inc_2str2 does), with the
   // checkpoints the pass reads for it: fb the beam at the chunk's top (pass 2), ae / se the albedo and source at its
@@ -327,8 +350,8 @@ __global__ void __launch_bounds__(512, WAVES)
   // use (the compiler sinks loads past such a branch).  No scheduling fences between the loads and the bodies: the
   // scheduler may then start a chunk's independent coefficient algebra under the previous chunk's recurrence (round
   // 4: C3 SW solver -0.6 to -2.5 %, C4 -1.1 %, tools/kernel_ab.py).
-  auto walk = [&](auto &&load, auto &&body, int count, auto &&idx, auto &A, auto &B) {
-    load(A, idx(0));
+  auto walk = [&](auto &&load, auto &&body, int count, auto &&idx, auto &A, auto &B, bool preloaded = false) {
+    if (!preloaded) load(A, idx(0));
     for (int i = 0; i < count; i += 2) {
       load(B, idx(min(i + 1, count - 1)));
       body(A, idx(i), true);
@@ -350,23 +373,10 @@ __global__ void __launch_bounds__(512, WAVES)
     }
   };
 
-  // ---- pass 1: direct beam, checkpoint at every chunk top ----
-  // Steps of P1 = kCkP1 * K layers: pass 1 has little arithmetic per layer, so it needs many loads in flight.
+  // ---- pass 1: direct beam, checkpoint at every chunk top (steps of P1 layers, A1 / B1 / load1 above) ----
   V Fd = Ftop;
   {
-    constexpr int P1 = P1C * K;
     const int np1 = (nlay + P1 - 1) / P1;
-    struct Buf1 {
-      V t[P1];
-    } A1, B1;
-    auto load1 = [&](Buf1 &b, int c1) {
-#pragma unroll
-      for (int p = 0; p < P1; p++) {
-        const int l = lay(c1 * P1 + p);
-        b.t[p] = Ttau.ldv(vL, row * (uint32_t)l);
-        if constexpr (kInc) b.t[p] += ld_bnd(Bt, l);
-      }
-    };
     auto body1 = [&](Buf1 &b, int c1, bool valid) {
       const int n = valid ? min(P1, nlay - c1 * P1) : 0;
       V arg[P1], Tn[P1];
@@ -383,7 +393,7 @@ __global__ void __launch_bounds__(512, WAVES)
         Fd = (p < n) ? Tn[p] * Fd : Fd;
       }
     };
-    walk(load1, body1, np1, [](int i) { return i; }, A1, B1);
+    walk(load1, body1, np1, [](int i) { return i; }, A1, B1, kEarly);
   }
   // ---- pass 2: bottom -> top adding; albedo / source checkpoint at every chunk top and at the surface ----
   V alb_b = bcf ? alb_bc : ld_col(alb_dif);
