@@ -318,19 +318,34 @@ __global__ void LW_BOUNDS lw_noscat_kernel(int ngpt, int nlay, int ncol, int top
         flush(pdn, min(kRing, nlay - j0), top + dl_dn * (j0 + 1), dl_dn);
       }
     }
+    // upward: lw_transport_noscat_up (:950-980); j-th layer from the surface is l = lay_up(j).  With one angle its first
+    // kPF layers are loaded before the surface level's flush, whose barrier would otherwise hold the loads back (with
+    // several angles there is no flush, and the registers would spill)
+    auto lay_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
+    float ptu[kPF], pyu[kPF], pvu[kPF], piu[kPF];
+    if constexpr (!kMulti) {
+#pragma unroll
+      for (int p = 0; p < kPF; p++) {
+        const int l = lay_up(min(p, nlay - 1));
+        ptu[p] = Ttau.ld(vg, row * l); pyu[p] = Tlay.ld(vg, row * l); piu[p] = ld_inc(l);
+        pvu[p] = kFused ? 0.0f : Tlev.ld(vg, row * l);
+      }
+    }
     // surface reflection and emission (:269)
     float U = I * (1.0f - e) + e * ss;
     put(fac * U, U, 0, 1, sfcl, acc);
     flush(pup, 1, sfcl, 1);
-    // upward: lw_transport_noscat_up (:950-980); j-th layer from the surface is l = lay_up(j)
-    auto lay_up = [&](int j) { return top_at_1 ? nlay - 1 - j : j; };
     {
       float pt[kPF], py[kPF], pv[kPF], pi[kPF];
 #pragma unroll
       for (int p = 0; p < kPF; p++) {
-        const int l = lay_up(min(p, nlay - 1));
-        pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
-        if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * l);
+        if constexpr (!kMulti) {
+          pt[p] = ptu[p]; py[p] = pyu[p]; pi[p] = piu[p]; pv[p] = pvu[p];
+        } else {
+          const int l = lay_up(min(p, nlay - 1));
+          pt[p] = Ttau.ld(vg, row * l); py[p] = Tlay.ld(vg, row * l); pi[p] = ld_inc(l);
+          if constexpr (!kFused) pv[p] = Tlev.ld(vg, row * l);
+        }
       }
       auto step = [&](int j, int r) {
         const int p = r % kPF, l = lay_up(min(j, nlay - 1));
