@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--sw-net-cus", type=int, default=0, help="the SW network's blocks on at most this many CUs (0: all)")
     ap.add_argument("--lw-net-cus", type=int, default=None,
                     help="the LW network's blocks on at most this many CUs (0: all; default: the library pipeline's "
-                         "choice: 5/8 of the CUs at small grids, where the LW chain follows the SW network)")
+                         "choice: 3/8 of the CUs at small grids, where the LW chain follows the SW network)")
     ap.add_argument("--unfused", action="store_true",
                     help="issue the class layer's exact call sequence (Planck sources and g materialised in HBM)")
     ap.add_argument("--sw-kernel", type=int, default=0, choices=[0, 1, 2, 3],

@@ -317,12 +317,14 @@ class ClearSkyStep:
             self._gate = torch.cuda.Event()
         # lw_net_cus: the LW network's blocks on at most that many CUs (rrtmgpnn_context_set_mlp_max_cus; 0: all).
         # Default with the LW chain gated on the SW network and an SW solver grid that fits in one round of resident
-        # waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane, against 16 per CU; C3): 5/8 of the CUs.
-        # Each LW network block holds a whole CU's LDS (117 KB), so on the full chip it kept the SW solver, launched
+        # waves (ncol * ngpt_sw / 128 waves of 64 lanes, 2 g-points per lane, against 16 per CU; C3): 3/8 of the CUs.
+        # Each LW network block holds most of a CU's LDS (108 KB), so on the full chip it kept the SW solver, launched
         # beside it, off every CU for its first 75 us at C3; confined, it leaves the SW solver the other CUs from the
         # start.  Round 4, C3 whole steps (3 alternating rounds, one box): 0.4350-0.4368 ms on 160 CUs, 0.4374-0.4379
-        # on 192, 0.4417-0.4434 on 224, 0.4456-0.4462 on all 256.  With more columns (C4) the cap costs 2 % (the SW
-        # solver is throughput-bound there; 2.705-2.726 on 192 against 2.651-2.664 ms); C5 equal.
+        # on 192, 0.4417-0.4434 on 224, 0.4456-0.4462 on all 256.  Round 6, on the kernels with their prologue loads in
+        # flight (4 alternating rounds, profiles/r06/lwcap*_c3.txt): 96 CUs 1.1 % faster than 160 (every round), 128
+        # 0.6-1.1 %, 64 and 144 equal.  With more columns (C4) the cap costs 2 % (the SW solver is throughput-bound
+        # there; 2.705-2.726 on 192 against 2.651-2.664 ms); C5 equal.
         # A caller's context is left as it is unless lw_net_cus is given.  The caps are overlap measures: without a
         # second stream both networks run on self.ctx, so a cap would confine the SW network too -- refused.
         explicit = lw_net_cus is not None
@@ -332,7 +334,7 @@ class ClearSkyStep:
             lw_net_cus = 0
             cus = torch.cuda.get_device_properties(self.dev).multi_processor_count
             if self._own_ctx and self.overlap and self.lw_after and self.ncol * self.ng_sw <= 2048 * cus:
-                lw_net_cus = 5 * cus // 8
+                lw_net_cus = 3 * cus // 8
         if self._own_ctx or explicit:
             self.ctx.set_mlp_max_cus(int(lw_net_cus))
         # the cap in force on the LW context (a caller's context may carry its own), which bench.py's serialised stage
